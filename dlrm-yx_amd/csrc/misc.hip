@@ -1,0 +1,391 @@
+// Small fused kernels of the DLRM step: bias-gradient column sums, the last layer +
+// sigmoid + loss head, ReLU-masked outer product, dense optimizers, device RNG fills.
+//
+//  * dlrm_colsum_f32: Linear bias gradient (sum of dY over the batch), deterministic
+//    two-pass (fixed 64-row chunks, then chunk partials in order), optional fused SGD.
+//  * dlrm_head_forward_backward: top-MLP last layer (K -> 1) + nn.Sigmoid + loss_fn
+//    (MSELoss / BCELoss mean, dlrm_s_pytorch.py:504-516, 170-178) and d loss / d logit
+//    in one wave-per-row pass; the batch mean is a fixed-order block reduction.
+//  * dlrm_sgd_update / dlrm_adagrad_update: torch.optim.SGD dense step and the dense
+//    branch of RWSAdagrad (optim/rwsadagrad.py:117-120) on a flat parameter bucket.
+#include "common.hpp"
+
+namespace {
+
+constexpr int kRowsPerChunk = 64;
+
+__global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t M, int64_t N,
+                                                             const float* __restrict__ Y,
+                                                             int64_t ldy,
+                                                             const float* __restrict__ scale,
+                                                             float* __restrict__ part) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t ms = blockIdx.y;
+  if (n >= N) return;
+  const int64_t m0 = ms * kRowsPerChunk;
+  const int64_t m1 = (m0 + kRowsPerChunk < M) ? m0 + kRowsPerChunk : M;
+  float s = 0.f;
+  if (scale) {
+    for (int64_t m = m0; m < m1; ++m) s = fmaf(scale[m], Y[m * ldy + n], s);
+  } else {
+    for (int64_t m = m0; m < m1; ++m) s += Y[m * ldy + n];
+  }
+  part[ms * N + n] = s;
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(int64_t N, int64_t MS,
+                                                           const float* __restrict__ part,
+                                                           float alpha, float* __restrict__ out,
+                                                           int accumulate,
+                                                           float* __restrict__ sgd_param,
+                                                           float lr) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int64_t ms = 0; ms < MS; ++ms) s += part[ms * N + n];
+  if (out) out[n] = accumulate ? out[n] + alpha * s : alpha * s;
+  if (sgd_param) sgd_param[n] = fmaf(-lr, s, sgd_param[n]);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void head_rows_kernel(int64_t M, int64_t K,
+                                                        const float* __restrict__ X, int64_t ldx,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bptr,
+                                                        const float* __restrict__ target,
+                                                        int loss_kind, float lo, float gscale,
+                                                        float* __restrict__ prob,
+                                                        float* __restrict__ dz,
+                                                        float* __restrict__ row_loss) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const float bias = bptr ? bptr[0] : 0.f;
+  const float invM = 1.f / (float)M;
+  for (int64_t m = wave; m < M; m += nw) {
+    const float* xr = X + m * ldx;
+    float s = 0.f;
+    for (int64_t k = lane; k < K; k += 64) s = fmaf(xr[k], w[k], s);
+    s = wave_sum(s);
+    if (lane == 0) {
+      const float z = s + bias;
+      const float p = 1.f / (1.f + expf(-z));
+      float pc = p;
+      bool pass = true;
+      if (lo > 0.f && lo < 0.5f) {
+        const float hi = 1.f - lo;
+        pass = (p >= lo) && (p <= hi);
+        pc = fminf(fmaxf(p, lo), hi);
+      }
+      const float t = target ? target[m] : 0.f;
+      float l, dp;
+      if (loss_kind == DLRM_LOSS_BCE) {
+        const float lp = fmaxf(logf(pc), -100.f);
+        const float l1p = fmaxf(logf(1.f - pc), -100.f);
+        l = -(t * lp + (1.f - t) * l1p);
+        dp = (pc - t) / fmaxf((1.f - pc) * pc, 1e-12f) * invM;
+      } else {
+        const float d = pc - t;
+        l = d * d;
+        dp = 2.f * d * invM;
+      }
+      dp *= gscale;
+      if (!pass) dp = 0.f;
+      if (prob) prob[m] = pc;
+      if (dz) dz[m] = dp * (1.f - p) * p;
+      row_loss[m] = l;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void mean_kernel(int64_t M, const float* __restrict__ v,
+                                                   float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += 256) s += v[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0] / (float)M;
+}
+
+__global__ __launch_bounds__(256) void outer_drelu_kernel(int64_t M, int64_t K,
+                                                          const float* __restrict__ dz,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ X,
+                                                          int64_t ldx, int mask,
+                                                          float* __restrict__ dX, int64_t lddx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * K) return;
+  const int64_t m = i / K, k = i - m * K;
+  float v = dz[m] * w[k];
+  if (mask && !(X[m * ldx + k] > 0.f)) v = 0.f;
+  dX[m * lddx + k] = v;
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p,
+                                                  const float* __restrict__ g, int64_t n,
+                                                  float lr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = i; j < n; j += stride) p[j] = fmaf(-lr, g[j], p[j]);
+}
+
+__global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ p,
+                                                      const float* __restrict__ g,
+                                                      float* __restrict__ ss, int64_t n,
+                                                      float clr, float eps) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = i; j < n; j += stride) {
+    const float gj = g[j];
+    const float s = fmaf(gj, gj, ss[j]);
+    ss[j] = s;
+    p[j] = fmaf(-clr, gj / (sqrtf(s) + eps), p[j]);
+  }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ x, int64_t n, float a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = i; j < n; j += stride) x[j] *= a;
+}
+
+__global__ __launch_bounds__(256) void sigmoid_fwd_kernel(int64_t n, const float* __restrict__ x,
+                                                          float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = i; j < n; j += stride) y[j] = 1.f / (1.f + expf(-x[j]));
+}
+
+__global__ __launch_bounds__(256) void sigmoid_bwd_kernel(int64_t n, const float* __restrict__ dy,
+                                                          const float* __restrict__ y,
+                                                          float* __restrict__ dx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = i; j < n; j += stride) dx[j] = dy[j] * (1.f - y[j]) * y[j];
+}
+
+__global__ __launch_bounds__(256) void relu_bwd_kernel(int64_t n, const float* __restrict__ dy,
+                                                       const float* __restrict__ y,
+                                                       float* __restrict__ dx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = i; j < n; j += stride) dx[j] = y[j] > 0.f ? dy[j] : 0.f;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void uniform_fill_kernel(float* __restrict__ out, int64_t n,
+                                                           float lo, float hi, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const uint64_t key = splitmix64(seed);
+  for (int64_t j = i; j < n; j += stride) {
+    const uint64_t x = splitmix64(key ^ (uint64_t)j);
+    const float u = (float)(x >> 40) * (1.f / 16777216.f);
+    out[j] = lo + (hi - lo) * u;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void uniform_int_kernel(T* __restrict__ out, int64_t n,
+                                                          uint64_t hi, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const uint64_t key = splitmix64(seed);
+  for (int64_t j = i; j < n; j += stride) {
+    const uint64_t x = splitmix64(key ^ (uint64_t)j);
+    out[j] = (T)__umul64hi(x, hi);
+  }
+}
+
+int grid_stride_blocks(int64_t n) {
+  int64_t b = dlrm::ceil_div(n, 256);
+  if (b > 16384) b = 16384;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" size_t dlrm_colsum_workspace_size(int64_t M, int64_t N) {
+  const int64_t ms = dlrm::ceil_div(M > 0 ? M : 1, kRowsPerChunk);
+  return (size_t)(ms * (N > 0 ? N : 1)) * sizeof(float) + 256;
+}
+
+extern "C" int dlrm_colsum_f32(int64_t M, int64_t N, const float* Y, int64_t ldy,
+                               const float* scale, float alpha, float* out, int32_t accumulate,
+                               float* sgd_param, float lr, void* workspace,
+                               size_t workspace_bytes, dlrm_stream_t stream) {
+  const char* name = "dlrm_colsum_f32";
+  DLRM_ARG(M >= 0 && N >= 0, "%s: negative size", name);
+  if (N == 0) return DLRM_OK;
+  DLRM_ARG(M == 0 || (Y && ldy >= N), "%s: bad Y", name);
+  DLRM_ARG(workspace, "%s: null workspace", name);
+  DLRM_REQUIRE(workspace_bytes >= dlrm_colsum_workspace_size(M, N), DLRM_ERR_WORKSPACE,
+               "%s: workspace too small", name);
+  hipStream_t st = dlrm::as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  const int64_t ms = M > 0 ? dlrm::ceil_div(M, kRowsPerChunk) : 0;
+  if (ms > 0) {
+    DLRM_REQUIRE(ms < 65536, DLRM_ERR_UNSUPPORTED, "%s: M too large", name);
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(dlrm::ceil_div(N, 256), ms), dim3(256), 0, st,
+                       M, N, Y, ldy, scale, part);
+    DLRM_LAUNCH_CHECK(name);
+  }
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(dlrm::ceil_div(N, 256)), dim3(256), 0, st, N, ms,
+                     part, alpha, out, accumulate, sgd_param, lr);
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+extern "C" size_t dlrm_head_workspace_size(int64_t M) {
+  return (size_t)(M > 0 ? M : 1) * sizeof(float) + 256;
+}
+
+extern "C" int dlrm_head_forward_backward(int64_t M, int64_t K, const float* X, int64_t ldx,
+                                          const float* w, const float* b, const float* target,
+                                          int32_t loss_kind, float clamp_lo, float grad_scale,
+                                          float* prob_out, float* dz_out, float* loss_out,
+                                          void* workspace, size_t workspace_bytes,
+                                          dlrm_stream_t stream) {
+  const char* name = "dlrm_head_forward_backward";
+  DLRM_ARG(M > 0 && K > 0, "%s: bad sizes", name);
+  DLRM_ARG(X && w && ldx >= K, "%s: bad X/w", name);
+  DLRM_ARG(loss_kind == DLRM_LOSS_MSE || loss_kind == DLRM_LOSS_BCE, "%s: bad loss", name);
+  DLRM_ARG(workspace, "%s: null workspace", name);
+  DLRM_REQUIRE(workspace_bytes >= dlrm_head_workspace_size(M), DLRM_ERR_WORKSPACE,
+               "%s: workspace too small", name);
+  DLRM_ARG(target || (!dz_out && !loss_out), "%s: loss/grad need target", name);
+  hipStream_t st = dlrm::as_stream(stream);
+  float* row_loss = static_cast<float*>(workspace);
+  int64_t blocks = dlrm::ceil_div(M, 4);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(head_rows_kernel, dim3(blocks), dim3(256), 0, st, M, K, X, ldx, w, b,
+                     target, loss_kind, clamp_lo, grad_scale, prob_out, dz_out, row_loss);
+  DLRM_LAUNCH_CHECK(name);
+  if (loss_out) {
+    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(256), 0, st, M, row_loss, loss_out);
+    DLRM_LAUNCH_CHECK(name);
+  }
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_outer_drelu(int64_t M, int64_t K, const float* dz, const float* w,
+                                const float* X, int64_t ldx, int32_t relu_mask, float* dX,
+                                int64_t lddx, dlrm_stream_t stream) {
+  const char* name = "dlrm_outer_drelu";
+  DLRM_ARG(M >= 0 && K >= 0, "%s: bad sizes", name);
+  if (M == 0 || K == 0) return DLRM_OK;
+  DLRM_ARG(dz && w && dX && lddx >= K, "%s: null pointer", name);
+  DLRM_ARG(!relu_mask || (X && ldx >= K), "%s: mask needs X", name);
+  hipLaunchKernelGGL(outer_drelu_kernel, dim3(dlrm::ceil_div(M * K, 256)), dim3(256), 0,
+                     dlrm::as_stream(stream), M, K, dz, w, X, ldx, relu_mask, dX, lddx);
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_sgd_update(float* param, const float* grad, int64_t n, float lr,
+                               dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_sgd_update: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(param && grad, "dlrm_sgd_update: null pointer");
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), param, grad, n, lr);
+  DLRM_LAUNCH_CHECK("dlrm_sgd_update");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_adagrad_update(float* param, const float* grad, float* state_sum, int64_t n,
+                                   float clr, float eps, dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_adagrad_update: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(param && grad && state_sum, "dlrm_adagrad_update: null pointer");
+  hipLaunchKernelGGL(adagrad_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), param, grad, state_sum, n, clr, eps);
+  DLRM_LAUNCH_CHECK("dlrm_adagrad_update");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_scale_f32(float* x, int64_t n, float alpha, dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_scale_f32: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(x, "dlrm_scale_f32: null pointer");
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), x, n, alpha);
+  DLRM_LAUNCH_CHECK("dlrm_scale_f32");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_uniform_fill(float* out, int64_t n, float lo, float hi, uint64_t seed,
+                                 dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_uniform_fill: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(out, "dlrm_uniform_fill: null pointer");
+  hipLaunchKernelGGL(uniform_fill_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), out, n, lo, hi, seed);
+  DLRM_LAUNCH_CHECK("dlrm_uniform_fill");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_uniform_int_fill(void* out, int32_t out_bits, int64_t n, int64_t hi,
+                                     uint64_t seed, dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0 && hi > 0, "dlrm_uniform_int_fill: bad n/hi");
+  DLRM_ARG(out_bits == 32 || out_bits == 64, "dlrm_uniform_int_fill: bad out_bits");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(out, "dlrm_uniform_int_fill: null pointer");
+  hipStream_t st = dlrm::as_stream(stream);
+  if (out_bits == 32)
+    hipLaunchKernelGGL(uniform_int_kernel<int32_t>, dim3(grid_stride_blocks(n)), dim3(256), 0, st,
+                       static_cast<int32_t*>(out), n, (uint64_t)hi, seed);
+  else
+    hipLaunchKernelGGL(uniform_int_kernel<int64_t>, dim3(grid_stride_blocks(n)), dim3(256), 0, st,
+                       static_cast<int64_t*>(out), n, (uint64_t)hi, seed);
+  DLRM_LAUNCH_CHECK("dlrm_uniform_int_fill");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_sigmoid_forward(int64_t n, const float* x, float* y, dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_sigmoid_forward: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(x && y, "dlrm_sigmoid_forward: null pointer");
+  hipLaunchKernelGGL(sigmoid_fwd_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), n, x, y);
+  DLRM_LAUNCH_CHECK("dlrm_sigmoid_forward");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_sigmoid_backward(int64_t n, const float* dy, const float* y, float* dx,
+                                     dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_sigmoid_backward: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(dy && y && dx, "dlrm_sigmoid_backward: null pointer");
+  hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), n, dy, y, dx);
+  DLRM_LAUNCH_CHECK("dlrm_sigmoid_backward");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_relu_backward(int64_t n, const float* dy, const float* y, float* dx,
+                                  dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_relu_backward: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(dy && y && dx, "dlrm_relu_backward: null pointer");
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), n, dy, y, dx);
+  DLRM_LAUNCH_CHECK("dlrm_relu_backward");
+  return DLRM_OK;
+}

@@ -1,0 +1,819 @@
+// Table-batched EmbeddingBag (sum pooling) for gfx950: forward gather-reduce and
+// deterministic sorted backward with the optimizer fused in.
+//
+// Semantics follow nn.EmbeddingBag(mode="sum") as DLRM_Net.apply_emb calls it
+// (dlrm_s_pytorch.py:526-587) in the table-batched CSR layout of
+// dlrm_data_pytorch.py:748-753 / TableBatchedEmbeddingBags (dlrm_s_pytorch.py:321-334):
+// bag (t, b) = t*B + b owns lookups [offsets[bag], offsets[bag+1]).
+//
+// Design (MI355X-first, not a translation of yx_modfs/table_batched_embeddings_cuda_yx.cu):
+//  * one lane-group of LPB lanes per bag (LPB = D/4 rounded to a power of two, <= 64),
+//    64/LPB bags per wave64, so a D=128 row is one coalesced 512-B float4 sweep by 32 lanes;
+//  * the group loads up to LPB indices of its bag in one coalesced load and broadcasts
+//    them with wave shuffles (ds_bpermute), four row fetches in flight per lane;
+//  * 64-bit row bases (a 54 M x 128 table set is 6.9e9 elements);
+//  * backward: stable LSD radix sort of (global row, lookup) pairs, run-length encode,
+//    then one lane-group per unique row reads the row once, applies its lookups'
+//    gradient in lookup order, and writes it once — bitwise reproducible.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+
+namespace {
+
+using dlrm::kWave;
+
+template <int VW>
+struct VecT;
+template <>
+struct VecT<4> {
+  using T = float4;
+};
+template <>
+struct VecT<1> {
+  using T = float;
+};
+
+__device__ __forceinline__ void vzero(float4& a) { a = make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ void vzero(float& a) { a = 0.f; }
+__device__ __forceinline__ void vadd(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+__device__ __forceinline__ void vadd(float& a, const float& b) { a += b; }
+__device__ __forceinline__ void vfma(float4& a, float w, const float4& b) {
+  a.x = fmaf(w, b.x, a.x);
+  a.y = fmaf(w, b.y, a.y);
+  a.z = fmaf(w, b.z, a.z);
+  a.w = fmaf(w, b.w, a.w);
+}
+__device__ __forceinline__ void vfma(float& a, float w, const float& b) { a = fmaf(w, b, a); }
+__device__ __forceinline__ void vscale(float4& a, float w) {
+  a.x *= w;
+  a.y *= w;
+  a.z *= w;
+  a.w *= w;
+}
+__device__ __forceinline__ void vscale(float& a, float w) { a *= w; }
+__device__ __forceinline__ float vdot(const float4& a) {
+  return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+}
+__device__ __forceinline__ float vdot(const float& a) { return a * a; }
+
+// ----------------------------------------------------------------- forward --
+template <int LPB, int VW, int MAXV, typename IdxT, typename OffT>
+__global__ __launch_bounds__(256) void tbe_fwd_kernel(
+    const float* __restrict__ W, int64_t D, const int64_t* __restrict__ row_base, int T, int B,
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const float* __restrict__ psw,
+    float* __restrict__ out, int64_t out_bs, int32_t* __restrict__ err) {
+  using V = typename VecT<VW>::T;
+  constexpr int GPW = kWave / LPB;  // bags per wave
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPB;
+  const int gl = lane - g * LPB;
+  const int nchunks = (int)(D / VW);
+  const int64_t nbags = (int64_t)T * B;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
+
+  for (int64_t bag0 = wave_id * GPW; bag0 < nbags; bag0 += nwaves * GPW) {
+    const int64_t bag = bag0 + g;
+    const bool active = bag < nbags;
+    int t = 0, b = 0;
+    int64_t start = 0, end = 0, base = 0, nrows = 0;
+    if (active) {
+      t = (int)(bag / B);
+      b = (int)(bag - (int64_t)t * B);
+      start = (int64_t)off[bag];
+      end = (int64_t)off[bag + 1];
+      base = row_base[t];
+      nrows = row_base[t + 1] - base;
+    }
+    V acc[MAXV];
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) vzero(acc[c]);
+
+    for (int64_t l0 = start; l0 < end; l0 += LPB) {
+      const int n = (int)((end - l0) < LPB ? (end - l0) : LPB);
+      int64_t my_row = -1;
+      float my_w = 1.f;
+      if (gl < n) {
+        int64_t r = (int64_t)idx[l0 + gl];
+        if (r < 0 || r >= nrows) {
+          if (err) *err = 1;
+          r = -1;
+        }
+        my_row = r;
+        if (psw) my_w = psw[l0 + gl];
+      }
+      for (int j = 0; j < n; j += 4) {
+        int64_t r[4];
+        float w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = g * LPB + ((j + u) < LPB ? (j + u) : 0);
+          r[u] = __shfl(my_row, src, kWave);
+          w[u] = __shfl(my_w, src, kWave);
+          if (j + u >= n) r[u] = -1;
+        }
+        V v[4][MAXV];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int c = 0; c < MAXV; ++c) {
+            const int chunk = gl + c * LPB;
+            if (r[u] >= 0 && chunk < nchunks) {
+              v[u][c] = reinterpret_cast<const V*>(W + (base + r[u]) * D)[chunk];
+            } else {
+              vzero(v[u][c]);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (r[u] >= 0) {
+#pragma unroll
+            for (int c = 0; c < MAXV; ++c) {
+              if (psw)
+                vfma(acc[c], w[u], v[u][c]);
+              else
+                vadd(acc[c], v[u][c]);
+            }
+          }
+        }
+      }
+    }
+    if (active) {
+      V* o = reinterpret_cast<V*>(out + (int64_t)b * out_bs + (int64_t)t * D);
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c) {
+        const int chunk = gl + c * LPB;
+        if (chunk < nchunks) o[chunk] = acc[c];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- backward --
+// Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags).
+template <typename IdxT, typename OffT, typename KeyT>
+__global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
+    int T, int B, int64_t N, KeyT sentinel, KeyT* __restrict__ keys, int32_t* __restrict__ pos,
+    int32_t* __restrict__ bag_of) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= N) return;
+  const int64_t nb = (int64_t)T * B;
+  KeyT key = sentinel;
+  int32_t bag = -1;
+  if (p >= (int64_t)off[0] && p < (int64_t)off[nb]) {
+    int64_t lo = 0, hi = nb;  // invariant off[lo] <= p < off[hi]
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)off[mid] <= p)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const int t = (int)(lo / B);
+    const int64_t r = (int64_t)idx[p];
+    const int64_t nrows = row_base[t + 1] - row_base[t];
+    if (r >= 0 && r < nrows) {
+      key = (KeyT)(row_base[t] + r);
+      bag = (int32_t)lo;
+    }
+  }
+  keys[p] = key;
+  pos[p] = (int32_t)p;
+  bag_of[p] = bag;
+}
+
+enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2 };
+
+template <int LPB, int VW, int MAXV, typename KeyT, int MODE>
+__global__ __launch_bounds__(256) void tbe_bwd_update_kernel(
+    float* __restrict__ W, float* __restrict__ mom, int64_t D, int B,
+    const KeyT* __restrict__ uniq, const int32_t* __restrict__ counts,
+    const int32_t* __restrict__ starts, const int32_t* __restrict__ num_runs,
+    const int32_t* __restrict__ pos_sorted, const int32_t* __restrict__ bag_of,
+    const float* __restrict__ psw, const float* __restrict__ gout, int64_t gbs, float lr,
+    float eps, KeyT sentinel) {
+  using V = typename VecT<VW>::T;
+  constexpr int GPW = kWave / LPB;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPB;
+  const int gl = lane - g * LPB;
+  const int nchunks = (int)(D / VW);
+  const int64_t nruns = (int64_t)(*num_runs);
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
+
+  for (int64_t run0 = wave_id * GPW; run0 < nruns; run0 += nwaves * GPW) {
+    const int64_t run = run0 + g;
+    if (run >= nruns) continue;
+    const KeyT row = uniq[run];
+    if (row == sentinel) continue;
+    const int64_t s0 = starts[run];
+    const int cnt = counts[run];
+    float* wrow = W + (int64_t)row * D;
+
+    V acc[MAXV];  // SGD: the weights being updated; others: gradient sum
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int chunk = gl + c * LPB;
+      if (MODE == MODE_SGD && chunk < nchunks)
+        acc[c] = reinterpret_cast<const V*>(wrow)[chunk];
+      else
+        vzero(acc[c]);
+    }
+    for (int i = 0; i < cnt; i += 4) {
+      int32_t bags[4];
+      float ws[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        bags[u] = -1;
+        ws[u] = 1.f;
+        if (i + u < cnt) {
+          const int32_t p = pos_sorted[s0 + i + u];
+          bags[u] = bag_of[p];
+          if (psw) ws[u] = psw[p];
+        }
+      }
+      V gv[4][MAXV];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = bags[u] >= 0 ? bags[u] / B : 0;
+        const int b = bags[u] >= 0 ? bags[u] - t * B : 0;
+        const V* grow = reinterpret_cast<const V*>(gout + (int64_t)b * gbs + (int64_t)t * D);
+#pragma unroll
+        for (int c = 0; c < MAXV; ++c) {
+          const int chunk = gl + c * LPB;
+          if (bags[u] >= 0 && chunk < nchunks) {
+            gv[u][c] = grow[chunk];
+            if (psw) vscale(gv[u][c], ws[u]);
+          } else {
+            vzero(gv[u][c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i + u < cnt) {
+#pragma unroll
+          for (int c = 0; c < MAXV; ++c) {
+            if (MODE == MODE_SGD)
+              vfma(acc[c], -lr, gv[u][c]);
+            else
+              vadd(acc[c], gv[u][c]);
+          }
+        }
+      }
+    }
+
+    if (MODE == MODE_SGD) {
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c) {
+        const int chunk = gl + c * LPB;
+        if (chunk < nchunks) reinterpret_cast<V*>(wrow)[chunk] = acc[c];
+      }
+    } else if (MODE == MODE_DENSE) {
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c) {
+        const int chunk = gl + c * LPB;
+        if (chunk < nchunks) {
+          V cur = reinterpret_cast<const V*>(wrow)[chunk];
+          vadd(cur, acc[c]);
+          reinterpret_cast<V*>(wrow)[chunk] = cur;
+        }
+      }
+    } else {  // row-wise Adagrad on the coalesced gradient
+      float sq = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c) {
+        const int chunk = gl + c * LPB;
+        if (chunk < nchunks) sq += vdot(acc[c]);
+      }
+#pragma unroll
+      for (int m = LPB / 2; m >= 1; m >>= 1) sq += __shfl_xor(sq, m, kWave);
+      const float mnew = mom[row] + sq / (float)D;
+      if (gl == 0) mom[row] = mnew;
+      const float denom = sqrtf(mnew) + eps;
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c) {
+        const int chunk = gl + c * LPB;
+        if (chunk < nchunks) {
+          V cur = reinterpret_cast<const V*>(wrow)[chunk];
+          V upd = acc[c];
+          if constexpr (VW == 4) {
+            upd.x /= denom;
+            upd.y /= denom;
+            upd.z /= denom;
+            upd.w /= denom;
+          } else {
+            upd /= denom;
+          }
+          vfma(cur, -lr, upd);
+          reinterpret_cast<V*>(wrow)[chunk] = cur;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------- sparse-grad expansion ----
+template <typename OffT>
+__global__ __launch_bounds__(256) void tbe_expand_grad_kernel(int64_t D, int T, int B,
+                                                              const OffT* __restrict__ off,
+                                                              int64_t N,
+                                                              const float* __restrict__ psw,
+                                                              const float* __restrict__ gout,
+                                                              int64_t gbs,
+                                                              float* __restrict__ values) {
+  // One wave per lookup; lanes sweep D.
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t nb = (int64_t)T * B;
+  for (int64_t p = wave; p < N; p += nw) {
+    float* vrow = values + p * D;
+    if (p < (int64_t)off[0] || p >= (int64_t)off[nb]) {
+      for (int64_t d = lane; d < D; d += 64) vrow[d] = 0.f;
+      continue;
+    }
+    int64_t lo = 0, hi = nb;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)off[mid] <= p)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const int t = (int)(lo / B);
+    const int b = (int)(lo - (int64_t)t * B);
+    const float w = psw ? psw[p] : 1.f;
+    const float* grow = gout + (int64_t)b * gbs + (int64_t)t * D;
+    for (int64_t d = lane; d < D; d += 64) vrow[d] = psw ? w * grow[d] : grow[d];
+  }
+}
+
+// ------------------------------------------------------------------- QR ----
+template <typename IdxT>
+__global__ __launch_bounds__(256) void qr_split_kernel(const IdxT* __restrict__ idx, int64_t n,
+                                                       int64_t c, int64_t* __restrict__ q,
+                                                       int64_t* __restrict__ r) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t v = (int64_t)idx[i];
+  // (input / num_collisions).long(): true division in fp32, truncated.
+  const float qf = (float)v / (float)c;
+  q[i] = (int64_t)qf;
+  int64_t rr = v % c;  // torch.remainder: sign of the divisor
+  if (rr != 0 && ((rr < 0) != (c < 0))) rr += c;
+  r[i] = rr;
+}
+
+__global__ __launch_bounds__(256) void qr_combine_fwd_kernel(int op, int64_t nrows, int64_t D,
+                                                             const float* __restrict__ eq,
+                                                             const float* __restrict__ er,
+                                                             float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows * D) return;
+  if (op == DLRM_QR_MULT) {
+    out[i] = eq[i] * er[i];
+  } else if (op == DLRM_QR_ADD) {
+    out[i] = eq[i] + er[i];
+  } else {
+    const int64_t m = i / D, d = i - m * D;
+    out[m * 2 * D + d] = eq[i];
+    out[m * 2 * D + D + d] = er[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void qr_combine_bwd_kernel(int op, int64_t nrows, int64_t D,
+                                                             const float* __restrict__ eq,
+                                                             const float* __restrict__ er,
+                                                             const float* __restrict__ go,
+                                                             float* __restrict__ geq,
+                                                             float* __restrict__ ger) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows * D) return;
+  if (op == DLRM_QR_MULT) {
+    const float g = go[i];
+    geq[i] = g * er[i];
+    ger[i] = g * eq[i];
+  } else if (op == DLRM_QR_ADD) {
+    geq[i] = go[i];
+    ger[i] = go[i];
+  } else {
+    const int64_t m = i / D, d = i - m * D;
+    geq[i] = go[m * 2 * D + d];
+    ger[i] = go[m * 2 * D + D + d];
+  }
+}
+
+// ------------------------------------------------------------ CSR build ----
+struct CsrArgs {
+  const int64_t* off[64];
+  int64_t start[65];
+};
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void csr_from_tables_kernel(int T, int B, CsrArgs a,
+                                                              OutT* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nb = (int64_t)T * B;
+  if (i > nb) return;
+  if (i == nb) {
+    out[nb] = (OutT)a.start[T];
+    return;
+  }
+  const int t = (int)(i / B);
+  const int b = (int)(i - (int64_t)t * B);
+  out[i] = (OutT)(a.start[t] + a.off[t][b]);
+}
+
+// ------------------------------------------------------------- dispatch ----
+template <typename IdxT, typename OffT>
+int launch_fwd(const float* W, int64_t D, const int64_t* row_base, int T, int B, const void* idx,
+               const void* off, const float* psw, float* out, int64_t out_bs, int32_t* err,
+               hipStream_t st) {
+  const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
+                    ((reinterpret_cast<uintptr_t>(out) & 15) == 0) && (out_bs % 4 == 0);
+  const int64_t nchunks = vec4 ? D / 4 : D;
+  int lpb = 1;
+  while (lpb < nchunks && lpb < 64) lpb <<= 1;
+  const int64_t maxv = dlrm::ceil_div(nchunks, lpb);
+  DLRM_REQUIRE(maxv <= 8, DLRM_ERR_UNSUPPORTED, "tbe_forward: D=%lld too large",
+               (long long)D);
+  const int64_t nbags = (int64_t)T * B;
+  const int gpw = 64 / lpb;
+  int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(nbags, gpw), 4);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  const IdxT* ip = static_cast<const IdxT*>(idx);
+  const OffT* op = static_cast<const OffT*>(off);
+#define FWD(LPB, VW, MV)                                                                   \
+  hipLaunchKernelGGL((tbe_fwd_kernel<LPB, VW, MV, IdxT, OffT>), dim3(blocks), dim3(256), 0, \
+                     st, W, D, row_base, T, B, ip, op, psw, out, out_bs, err)
+#define FWD_LPB(VW)                        \
+  switch (lpb) {                           \
+    case 1: FWD(1, VW, 1); break;          \
+    case 2: FWD(2, VW, 1); break;          \
+    case 4: FWD(4, VW, 1); break;          \
+    case 8: FWD(8, VW, 1); break;          \
+    case 16: FWD(16, VW, 1); break;        \
+    case 32: FWD(32, VW, 1); break;        \
+    default:                               \
+      if (maxv == 1) FWD(64, VW, 1);       \
+      else if (maxv == 2) FWD(64, VW, 2);  \
+      else if (maxv <= 4) FWD(64, VW, 4);  \
+      else FWD(64, VW, 8);                 \
+  }
+  if (vec4) {
+    FWD_LPB(4)
+  } else {
+    FWD_LPB(1)
+  }
+#undef FWD_LPB
+#undef FWD
+  DLRM_LAUNCH_CHECK("dlrm_tbe_forward");
+  return DLRM_OK;
+}
+
+inline int bit_width_u64(uint64_t v) {
+  int b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b < 1 ? 1 : b;
+}
+
+template <typename KeyT>
+struct BwdWs {
+  KeyT* keys_in;
+  KeyT* keys_out;
+  int32_t* pos_in;
+  int32_t* pos_out;
+  int32_t* bag_of;
+  KeyT* uniq;
+  int32_t* counts;
+  int32_t* starts;
+  int32_t* num_runs;
+  void* temp;
+  size_t temp_bytes;
+  size_t total;
+};
+
+template <typename KeyT>
+BwdWs<KeyT> carve_bwd_ws(void* base, int64_t N, int end_bit) {
+  BwdWs<KeyT> w{};
+  WsCarver c(base);
+  w.keys_in = c.take<KeyT>(N);
+  w.keys_out = c.take<KeyT>(N);
+  w.pos_in = c.take<int32_t>(N);
+  w.pos_out = c.take<int32_t>(N);
+  w.bag_of = c.take<int32_t>(N);
+  w.uniq = c.take<KeyT>(N);
+  w.counts = c.take<int32_t>(N);
+  w.starts = c.take<int32_t>(N);
+  w.num_runs = c.take<int32_t>(1);
+  size_t s1 = 0, s2 = 0, s3 = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s1, (KeyT*)nullptr, (KeyT*)nullptr,
+                                     (int32_t*)nullptr, (int32_t*)nullptr, (int)N, 0, end_bit);
+  (void)hipcub::DeviceRunLengthEncode::Encode(nullptr, s2, (KeyT*)nullptr, (KeyT*)nullptr,
+                                        (int32_t*)nullptr, (int32_t*)nullptr, (int)N);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s3, (int32_t*)nullptr, (int32_t*)nullptr, (int)N);
+  size_t s = s1 > s2 ? s1 : s2;
+  s = s > s3 ? s : s3;
+  w.temp_bytes = s + 256;
+  w.temp = c.take<char>(w.temp_bytes);
+  w.total = c.used + 256;
+  return w;
+}
+
+template <typename KeyT, typename IdxT, typename OffT>
+int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
+               const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
+               const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
+               hipStream_t st, const char* name) {
+  if (N == 0) return DLRM_OK;
+  const KeyT sentinel = (KeyT)total_rows;
+  const int end_bit = bit_width_u64((uint64_t)total_rows);
+  BwdWs<KeyT> w = carve_bwd_ws<KeyT>(ws, N, end_bit);
+  DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
+               name, ws_bytes, w.total);
+  const int64_t kblocks = dlrm::ceil_div(N, 256);
+  hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(kblocks), dim3(256), 0, st,
+                     static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base, T,
+                     B, N, sentinel, w.keys_in, w.pos_in, w.bag_of);
+  DLRM_LAUNCH_CHECK(name);
+  size_t tb = w.temp_bytes;
+  DLRM_HIP_CALL(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in,
+                                                   w.pos_out, (int)N, 0, end_bit, st),
+                name);
+  DLRM_HIP_CALL(hipMemsetAsync(w.counts, 0, sizeof(int32_t) * N, st), name);
+  tb = w.temp_bytes;
+  DLRM_HIP_CALL(hipcub::DeviceRunLengthEncode::Encode(w.temp, tb, w.keys_out, w.uniq, w.counts,
+                                                      w.num_runs, (int)N, st),
+                name);
+  tb = w.temp_bytes;
+  DLRM_HIP_CALL(hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.counts, w.starts, (int)N, st),
+                name);
+
+  const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
+                    ((reinterpret_cast<uintptr_t>(gout) & 15) == 0) && (gbs % 4 == 0);
+  const int64_t nchunks = vec4 ? D / 4 : D;
+  int lpb = 1;
+  while (lpb < nchunks && lpb < 64) lpb <<= 1;
+  const int64_t maxv = dlrm::ceil_div(nchunks, lpb);
+  DLRM_REQUIRE(maxv <= 8, DLRM_ERR_UNSUPPORTED, "%s: D=%lld too large", name, (long long)D);
+  const int gpw = 64 / lpb;
+  int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(N, gpw), 4);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+#define UPD(LPB, VW, MV, MODE)                                                              \
+  hipLaunchKernelGGL((tbe_bwd_update_kernel<LPB, VW, MV, KeyT, MODE>), dim3(blocks),        \
+                     dim3(256), 0, st, W, mom, D, B, w.uniq, w.counts, w.starts, w.num_runs, \
+                     w.pos_out, w.bag_of, psw, gout, gbs, lr, eps, sentinel)
+#define UPD_LPB(VW, MODE)                        \
+  switch (lpb) {                                 \
+    case 1: UPD(1, VW, 1, MODE); break;          \
+    case 2: UPD(2, VW, 1, MODE); break;          \
+    case 4: UPD(4, VW, 1, MODE); break;          \
+    case 8: UPD(8, VW, 1, MODE); break;          \
+    case 16: UPD(16, VW, 1, MODE); break;        \
+    case 32: UPD(32, VW, 1, MODE); break;        \
+    default:                                     \
+      if (maxv == 1) UPD(64, VW, 1, MODE);       \
+      else if (maxv == 2) UPD(64, VW, 2, MODE);  \
+      else if (maxv <= 4) UPD(64, VW, 4, MODE);  \
+      else UPD(64, VW, 8, MODE);                 \
+  }
+#define UPD_MODE(VW)                                 \
+  if (mode == MODE_SGD) {                            \
+    UPD_LPB(VW, MODE_SGD)                            \
+  } else if (mode == MODE_ADAGRAD) {                 \
+    UPD_LPB(VW, MODE_ADAGRAD)                        \
+  } else {                                           \
+    UPD_LPB(VW, MODE_DENSE)                          \
+  }
+  if (vec4) {
+    UPD_MODE(4)
+  } else {
+    UPD_MODE(1)
+  }
+#undef UPD_MODE
+#undef UPD_LPB
+#undef UPD
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T,
+                 int B, const void* idx, int ib, const void* off, int ob, int64_t N,
+                 int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
+                 float eps, void* ws, size_t ws_bytes, dlrm_stream_t stream, const char* name) {
+  DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
+  DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
+  DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
+  DLRM_ARG(ob == 32 || ob == 64, "%s: offset_bits must be 32 or 64", name);
+  DLRM_REQUIRE(N < (int64_t)INT32_MAX && (int64_t)T * B < (int64_t)INT32_MAX,
+               DLRM_ERR_UNSUPPORTED, "%s: more than 2^31 lookups/bags per call", name);
+  DLRM_ARG(gbs >= (int64_t)T * D, "%s: grad_batch_stride < T*D", name);
+  hipStream_t st = dlrm::as_stream(stream);
+  const bool k32 = (uint64_t)total_rows < 0xFFFFFFFFull;
+#define BWD(K, I, O)                                                                     \
+  return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
+                             gout, gbs, lr, eps, ws, ws_bytes, st, name)
+  if (k32) {
+    if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
+    if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
+    if (ib == 64 && ob == 32) BWD(uint32_t, int64_t, int32_t);
+    BWD(uint32_t, int64_t, int64_t);
+  } else {
+    if (ib == 32 && ob == 32) BWD(uint64_t, int32_t, int32_t);
+    if (ib == 32 && ob == 64) BWD(uint64_t, int32_t, int64_t);
+    if (ib == 64 && ob == 32) BWD(uint64_t, int64_t, int32_t);
+    BWD(uint64_t, int64_t, int64_t);
+  }
+#undef BWD
+}
+
+}  // namespace
+
+extern "C" int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base,
+                                int32_t T, int32_t B, const void* indices, int32_t index_bits,
+                                const void* offsets, int32_t offset_bits,
+                                const float* per_sample_weights, float* out,
+                                int64_t out_batch_stride, int32_t* error_flag,
+                                dlrm_stream_t stream) {
+  DLRM_ARG(weights && row_base && out && offsets, "dlrm_tbe_forward: null pointer");
+  DLRM_ARG(T > 0 && B > 0 && D > 0, "dlrm_tbe_forward: bad sizes T=%d B=%d D=%lld", T, B,
+           (long long)D);
+  DLRM_ARG(index_bits == 32 || index_bits == 64, "dlrm_tbe_forward: index_bits must be 32|64");
+  DLRM_ARG(offset_bits == 32 || offset_bits == 64,
+           "dlrm_tbe_forward: offset_bits must be 32|64");
+  DLRM_ARG(out_batch_stride >= (int64_t)T * D, "dlrm_tbe_forward: out_batch_stride < T*D");
+  hipStream_t st = dlrm::as_stream(stream);
+  if (index_bits == 32 && offset_bits == 32)
+    return launch_fwd<int32_t, int32_t>(weights, D, row_base, T, B, indices, offsets,
+                                        per_sample_weights, out, out_batch_stride, error_flag, st);
+  if (index_bits == 32)
+    return launch_fwd<int32_t, int64_t>(weights, D, row_base, T, B, indices, offsets,
+                                        per_sample_weights, out, out_batch_stride, error_flag, st);
+  if (offset_bits == 32)
+    return launch_fwd<int64_t, int32_t>(weights, D, row_base, T, B, indices, offsets,
+                                        per_sample_weights, out, out_batch_stride, error_flag, st);
+  return launch_fwd<int64_t, int64_t>(weights, D, row_base, T, B, indices, offsets,
+                                      per_sample_weights, out, out_batch_stride, error_flag, st);
+}
+
+extern "C" size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows) {
+  if (num_lookups <= 0) return 256;
+  const int end_bit = bit_width_u64((uint64_t)(total_rows > 0 ? total_rows : 1));
+  if ((uint64_t)total_rows < 0xFFFFFFFFull)
+    return carve_bwd_ws<uint32_t>(nullptr, num_lookups, end_bit).total;
+  return carve_bwd_ws<uint64_t>(nullptr, num_lookups, end_bit).total;
+}
+
+extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base,
+                                     int32_t T, int32_t B, const void* indices,
+                                     int32_t index_bits, const void* offsets,
+                                     int32_t offset_bits, int64_t num_lookups,
+                                     int64_t total_rows, const float* per_sample_weights,
+                                     const float* grad_out, int64_t grad_batch_stride, float lr,
+                                     void* workspace, size_t workspace_bytes,
+                                     dlrm_stream_t stream) {
+  return bwd_dispatch(MODE_SGD, weights, nullptr, D, row_base, T, B, indices, index_bits,
+                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
+                      grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes, stream,
+                      "dlrm_tbe_backward_sgd");
+}
+
+extern "C" int dlrm_tbe_backward_rowwise_adagrad(
+    float* weights, float* momentum, int64_t D, const int64_t* row_base, int32_t T, int32_t B,
+    const void* indices, int32_t index_bits, const void* offsets, int32_t offset_bits,
+    int64_t num_lookups, int64_t total_rows, const float* per_sample_weights,
+    const float* grad_out, int64_t grad_batch_stride, float lr, float eps, void* workspace,
+    size_t workspace_bytes, dlrm_stream_t stream) {
+  DLRM_ARG(momentum, "dlrm_tbe_backward_rowwise_adagrad: null momentum");
+  return bwd_dispatch(MODE_ADAGRAD, weights, momentum, D, row_base, T, B, indices, index_bits,
+                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
+                      grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes, stream,
+                      "dlrm_tbe_backward_rowwise_adagrad");
+}
+
+extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_base,
+                                       int32_t T, int32_t B, const void* indices,
+                                       int32_t index_bits, const void* offsets,
+                                       int32_t offset_bits, int64_t num_lookups,
+                                       int64_t total_rows, const float* per_sample_weights,
+                                       const float* grad_out, int64_t grad_batch_stride,
+                                       void* workspace, size_t workspace_bytes,
+                                       dlrm_stream_t stream) {
+  return bwd_dispatch(MODE_DENSE, grad_weights, nullptr, D, row_base, T, B, indices, index_bits,
+                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
+                      grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes, stream,
+                      "dlrm_tbe_backward_dense");
+}
+
+extern "C" int dlrm_qr_split_indices(const void* indices, int32_t index_bits, int64_t n,
+                                     int64_t collisions, int64_t* q_out, int64_t* r_out,
+                                     dlrm_stream_t stream) {
+  DLRM_ARG(n == 0 || (indices && q_out && r_out), "dlrm_qr_split_indices: null pointer");
+  DLRM_ARG(collisions > 0, "dlrm_qr_split_indices: collisions must be > 0");
+  DLRM_ARG(index_bits == 32 || index_bits == 64, "dlrm_qr_split_indices: bad index_bits");
+  if (n == 0) return DLRM_OK;
+  hipStream_t st = dlrm::as_stream(stream);
+  const int64_t blocks = dlrm::ceil_div(n, 256);
+  if (index_bits == 32)
+    hipLaunchKernelGGL(qr_split_kernel<int32_t>, dim3(blocks), dim3(256), 0, st,
+                       static_cast<const int32_t*>(indices), n, collisions, q_out, r_out);
+  else
+    hipLaunchKernelGGL(qr_split_kernel<int64_t>, dim3(blocks), dim3(256), 0, st,
+                       static_cast<const int64_t*>(indices), n, collisions, q_out, r_out);
+  DLRM_LAUNCH_CHECK("dlrm_qr_split_indices");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_qr_combine_forward(int32_t op, int64_t n_rows, int64_t D, const float* eq,
+                                       const float* er, float* out, dlrm_stream_t stream) {
+  DLRM_ARG(op >= 0 && op <= 2, "dlrm_qr_combine_forward: bad op");
+  DLRM_ARG(n_rows >= 0 && D > 0, "dlrm_qr_combine_forward: bad sizes");
+  if (n_rows == 0) return DLRM_OK;
+  DLRM_ARG(eq && er && out, "dlrm_qr_combine_forward: null pointer");
+  hipLaunchKernelGGL(qr_combine_fwd_kernel, dim3(dlrm::ceil_div(n_rows * D, 256)), dim3(256), 0,
+                     dlrm::as_stream(stream), op, n_rows, D, eq, er, out);
+  DLRM_LAUNCH_CHECK("dlrm_qr_combine_forward");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_qr_combine_backward(int32_t op, int64_t n_rows, int64_t D, const float* eq,
+                                        const float* er, const float* grad_out, float* grad_eq,
+                                        float* grad_er, dlrm_stream_t stream) {
+  DLRM_ARG(op >= 0 && op <= 2, "dlrm_qr_combine_backward: bad op");
+  DLRM_ARG(n_rows >= 0 && D > 0, "dlrm_qr_combine_backward: bad sizes");
+  if (n_rows == 0) return DLRM_OK;
+  DLRM_ARG(eq && er && grad_out && grad_eq && grad_er, "dlrm_qr_combine_backward: null pointer");
+  hipLaunchKernelGGL(qr_combine_bwd_kernel, dim3(dlrm::ceil_div(n_rows * D, 256)), dim3(256), 0,
+                     dlrm::as_stream(stream), op, n_rows, D, eq, er, grad_out, grad_eq, grad_er);
+  DLRM_LAUNCH_CHECK("dlrm_qr_combine_backward");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_csr_from_tables(int32_t T, int32_t B, const int64_t* const* table_offsets,
+                                    const int64_t* table_nnz, void* out_offsets,
+                                    int32_t out_offset_bits, dlrm_stream_t stream) {
+  DLRM_ARG(T > 0 && T <= 64 && B > 0, "dlrm_csr_from_tables: need 0 < T <= 64, B > 0");
+  DLRM_ARG(table_offsets && table_nnz && out_offsets, "dlrm_csr_from_tables: null pointer");
+  DLRM_ARG(out_offset_bits == 32 || out_offset_bits == 64, "dlrm_csr_from_tables: bad bits");
+  CsrArgs a{};
+  a.start[0] = 0;
+  for (int t = 0; t < T; ++t) {
+    DLRM_ARG(table_offsets[t] != nullptr, "dlrm_csr_from_tables: null table offsets");
+    a.off[t] = table_offsets[t];
+    a.start[t + 1] = a.start[t] + table_nnz[t];
+  }
+  const int64_t n = (int64_t)T * B + 1;
+  hipStream_t st = dlrm::as_stream(stream);
+  if (out_offset_bits == 32) {
+    DLRM_REQUIRE(a.start[T] < (int64_t)INT32_MAX, DLRM_ERR_UNSUPPORTED,
+                 "dlrm_csr_from_tables: int32 offsets overflow");
+    hipLaunchKernelGGL(csr_from_tables_kernel<int32_t>, dim3(dlrm::ceil_div(n, 256)), dim3(256),
+                       0, st, T, B, a, static_cast<int32_t*>(out_offsets));
+  } else {
+    hipLaunchKernelGGL(csr_from_tables_kernel<int64_t>, dim3(dlrm::ceil_div(n, 256)), dim3(256),
+                       0, st, T, B, a, static_cast<int64_t*>(out_offsets));
+  }
+  DLRM_LAUNCH_CHECK("dlrm_csr_from_tables");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_tbe_expand_grad(int64_t D, int32_t T, int32_t B, const void* offsets,
+                                    int32_t offset_bits, int64_t num_lookups,
+                                    const float* per_sample_weights, const float* grad_out,
+                                    int64_t grad_batch_stride, float* values,
+                                    dlrm_stream_t stream) {
+  const char* name = "dlrm_tbe_expand_grad";
+  DLRM_ARG(D > 0 && T > 0 && B > 0 && num_lookups >= 0, "%s: bad sizes", name);
+  if (num_lookups == 0) return DLRM_OK;
+  DLRM_ARG(offsets && grad_out && values, "%s: null pointer", name);
+  DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: bad offset_bits", name);
+  DLRM_ARG(grad_batch_stride >= (int64_t)T * D, "%s: grad_batch_stride < T*D", name);
+  int64_t blocks = dlrm::ceil_div(num_lookups, 4);
+  if (blocks > 16384) blocks = 16384;
+  hipStream_t st = dlrm::as_stream(stream);
+  if (offset_bits == 32)
+    hipLaunchKernelGGL(tbe_expand_grad_kernel<int32_t>, dim3(blocks), dim3(256), 0, st, D, T, B,
+                       static_cast<const int32_t*>(offsets), num_lookups, per_sample_weights,
+                       grad_out, grad_batch_stride, values);
+  else
+    hipLaunchKernelGGL(tbe_expand_grad_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, D, T, B,
+                       static_cast<const int64_t*>(offsets), num_lookups, per_sample_weights,
+                       grad_out, grad_batch_stride, values);
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}

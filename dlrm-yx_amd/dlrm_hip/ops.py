@@ -1,0 +1,368 @@
+"""Tensor-level launchers over the C-ABI (one function per dlrm_* entry point).
+
+Every launcher enqueues on ``torch.cuda.current_stream()`` and returns without
+synchronising; all device buffers (outputs, workspaces) are allocated here by the
+torch caching allocator and handed to the C-ABI as raw pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+
+EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_DRELU, EPI_SGD, EPI_ACCUM = range(6)
+LOSS_MSE, LOSS_BCE = 0, 1
+QR_OPS = {"mult": 0, "add": 1, "concat": 2}
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: Optional[torch.device] = None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _check_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("dlrm_hip ops take device tensors (got a CPU tensor)")
+
+
+def _bits(t: torch.Tensor) -> int:
+    if t.dtype == torch.int32:
+        return 32
+    if t.dtype == torch.int64:
+        return 64
+    raise TypeError(f"index/offset tensors must be int32 or int64, got {t.dtype}")
+
+
+class Workspace:
+    """Grow-only device scratch buffer (one per owner, reused across calls)."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != torch.device(device):
+            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        return self.buf
+
+
+_default_ws = {}
+
+
+def _ws(tag: str, nbytes: int, device) -> torch.Tensor:
+    key = (tag, str(device))
+    w = _default_ws.get(key)
+    if w is None:
+        w = _default_ws[key] = Workspace()
+    return w.get(nbytes, device)
+
+
+# ------------------------------------------------------------------ TBE ----
+def tbe_forward(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
+                indices: torch.Tensor, offsets: torch.Tensor,
+                per_sample_weights: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, out_batch_stride: Optional[int] = None,
+                error_flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Pooled-sum lookup -> [B, T, D] (or into ``out`` with a custom batch stride)."""
+    _check_cuda(weights, row_base, indices, offsets, per_sample_weights)
+    D = weights.shape[1]
+    if out is None:
+        out = torch.empty((B, T, D), dtype=torch.float32, device=weights.device)
+        out_batch_stride = T * D
+    elif out_batch_stride is None:
+        out_batch_stride = T * D
+    _lib.call("dlrm_tbe_forward", _p(weights), D, _p(row_base), T, B, _p(indices),
+              _bits(indices), _p(offsets), _bits(offsets), _p(per_sample_weights), _p(out),
+              out_batch_stride, _p(error_flag), _stream(weights.device))
+    return out
+
+
+def tbe_backward_workspace_size(num_lookups: int, total_rows: int) -> int:
+    return _lib.query("dlrm_tbe_backward_workspace_size", num_lookups, total_rows)
+
+
+def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
+                 indices: torch.Tensor, offsets: torch.Tensor, grad_out: torch.Tensor,
+                 lr: float = 0.0, eps: float = 0.0, momentum: Optional[torch.Tensor] = None,
+                 per_sample_weights: Optional[torch.Tensor] = None,
+                 grad_batch_stride: Optional[int] = None,
+                 workspace: Optional[torch.Tensor] = None) -> None:
+    """mode: 'sgd' (fused exact SGD), 'rowwise_adagrad' (fused RWSAdagrad) or
+    'dense' (weights is a gradient buffer to accumulate into)."""
+    _check_cuda(weights, row_base, indices, offsets, grad_out, momentum, per_sample_weights)
+    D = weights.shape[1]
+    N = indices.numel()
+    total_rows = weights.shape[0]
+    if grad_batch_stride is None:
+        grad_batch_stride = T * D
+    need = tbe_backward_workspace_size(N, total_rows)
+    if workspace is None:
+        workspace = _ws("tbe_bwd", need, weights.device)
+    args_common = (D, _p(row_base), T, B, _p(indices), _bits(indices), _p(offsets),
+                   _bits(offsets), N, total_rows, _p(per_sample_weights), _p(grad_out),
+                   grad_batch_stride)
+    st = _stream(weights.device)
+    if mode == "sgd":
+        _lib.call("dlrm_tbe_backward_sgd", _p(weights), *args_common, lr, _p(workspace),
+                  workspace.numel(), st)
+    elif mode == "rowwise_adagrad":
+        _lib.call("dlrm_tbe_backward_rowwise_adagrad", _p(weights), _p(momentum), *args_common,
+                  lr, eps, _p(workspace), workspace.numel(), st)
+    elif mode == "dense":
+        _lib.call("dlrm_tbe_backward_dense", _p(weights), *args_common, _p(workspace),
+                  workspace.numel(), st)
+    else:
+        raise ValueError(mode)
+
+
+def tbe_expand_grad(D: int, T: int, B: int, offsets: torch.Tensor, num_lookups: int,
+                    grad_out: torch.Tensor, per_sample_weights: Optional[torch.Tensor] = None,
+                    grad_batch_stride: Optional[int] = None) -> torch.Tensor:
+    _check_cuda(offsets, grad_out, per_sample_weights)
+    values = torch.empty((num_lookups, D), dtype=torch.float32, device=grad_out.device)
+    if grad_batch_stride is None:
+        grad_batch_stride = T * D
+    _lib.call("dlrm_tbe_expand_grad", D, T, B, _p(offsets), _bits(offsets), num_lookups,
+              _p(per_sample_weights), _p(grad_out), grad_batch_stride, _p(values),
+              _stream(grad_out.device))
+    return values
+
+
+# ------------------------------------------------------------------- QR ----
+def qr_split_indices(indices: torch.Tensor, collisions: int):
+    _check_cuda(indices)
+    n = indices.numel()
+    q = torch.empty(n, dtype=torch.int64, device=indices.device)
+    r = torch.empty(n, dtype=torch.int64, device=indices.device)
+    _lib.call("dlrm_qr_split_indices", _p(indices), _bits(indices), n, collisions, _p(q), _p(r),
+              _stream(indices.device))
+    return q, r
+
+
+def qr_combine_forward(op: str, eq: torch.Tensor, er: torch.Tensor) -> torch.Tensor:
+    n, D = eq.shape
+    out = torch.empty((n, 2 * D if op == "concat" else D), dtype=torch.float32, device=eq.device)
+    _lib.call("dlrm_qr_combine_forward", QR_OPS[op], n, D, _p(eq), _p(er), _p(out),
+              _stream(eq.device))
+    return out
+
+
+def qr_combine_backward(op: str, eq: torch.Tensor, er: torch.Tensor, grad_out: torch.Tensor):
+    n, D = eq.shape
+    geq = torch.empty_like(eq)
+    ger = torch.empty_like(er)
+    _lib.call("dlrm_qr_combine_backward", QR_OPS[op], n, D, _p(eq), _p(er),
+              _p(grad_out.contiguous()), _p(geq), _p(ger), _stream(eq.device))
+    return geq, ger
+
+
+# ---------------------------------------------------------- interaction ----
+def _feature_arrays(feats: Sequence[torch.Tensor], strides: Sequence[int]):
+    F = len(feats)
+    ptrs = (ctypes.c_void_p * F)(*[t.data_ptr() for t in feats])
+    bs = (ctypes.c_int64 * F)(*[int(s) for s in strides])
+    return ptrs, bs
+
+
+def feature_views(x: torch.Tensor, ly) -> tuple:
+    """(tensors, batch strides, D) for feature 0 = x and ly = [B,T,D] tensor or list of [B,D]."""
+    feats = [x]
+    strides = [x.stride(0)]
+    if isinstance(ly, torch.Tensor):
+        ly = [ly]
+    for y in ly:
+        if y.dim() == 3:  # [B, T, D], rows contiguous in D
+            if y.stride(2) != 1:
+                raise ValueError("interaction features must be contiguous in D")
+            for t in range(y.shape[1]):
+                feats.append(y[:, t, :])
+                strides.append(y.stride(0))
+        else:
+            if y.stride(1) != 1:
+                raise ValueError("interaction features must be contiguous in D")
+            feats.append(y)
+            strides.append(y.stride(0))
+    return feats, strides
+
+
+def interact_forward(op: str, x: torch.Tensor, ly, self_interaction: bool = False,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    feats, strides = feature_views(x, ly)
+    _check_cuda(*feats)
+    B, D = x.shape
+    F = len(feats)
+    ptrs, bs = _feature_arrays(feats, strides)
+    if op == "dot":
+        npairs = F * (F + 1) // 2 if self_interaction else F * (F - 1) // 2
+        if out is None:
+            out = torch.empty((B, D + npairs), dtype=torch.float32, device=x.device)
+        _lib.call("dlrm_interact_dot_forward", B, F, D, ptrs, bs, int(self_interaction), _p(out),
+                  out.stride(0), _stream(x.device))
+    elif op == "cat":
+        if out is None:
+            out = torch.empty((B, F * D), dtype=torch.float32, device=x.device)
+        _lib.call("dlrm_interact_cat_forward", B, F, D, ptrs, bs, _p(out), out.stride(0),
+                  _stream(x.device))
+    else:
+        raise ValueError(op)
+    return out
+
+
+def interact_backward(op: str, x: torch.Tensor, ly, grad_out: torch.Tensor,
+                      self_interaction: bool = False, grad_x: Optional[torch.Tensor] = None,
+                      grad_ly=None):
+    """Returns (grad_x, grad_ly) with grad_ly shaped like ly ([B,T,D] or list of [B,D])."""
+    feats, strides = feature_views(x, ly)
+    B, D = x.shape
+    F = len(feats)
+    if grad_x is None:
+        grad_x = torch.empty_like(x, memory_format=torch.contiguous_format)
+    if grad_ly is None:
+        if isinstance(ly, torch.Tensor):
+            grad_ly = torch.empty(ly.shape, dtype=torch.float32, device=x.device)
+        else:
+            grad_ly = [torch.empty(y.shape, dtype=torch.float32, device=x.device) for y in ly]
+    gfeats, gstrides = feature_views(grad_x, grad_ly)
+    ptrs, bs = _feature_arrays(feats, strides)
+    gptrs, gbs = _feature_arrays(gfeats, gstrides)
+    g = grad_out.contiguous()
+    if op == "dot":
+        _lib.call("dlrm_interact_dot_backward", B, F, D, ptrs, bs, int(self_interaction), _p(g),
+                  g.stride(0), gptrs, gbs, _stream(x.device))
+    else:
+        _lib.call("dlrm_interact_cat_backward", B, F, D, _p(g), g.stride(0), gptrs, gbs,
+                  _stream(x.device))
+    return grad_x, grad_ly
+
+
+# ------------------------------------------------------------------ MLP ----
+def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+         C: Optional[torch.Tensor] = None, alpha: float = 1.0, epilogue: int = EPI_STORE,
+         bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D operands (unit inner stride)."""
+    _check_cuda(A, B, C, bias, aux)
+    if A.stride(1) != 1 or B.stride(1) != 1:
+        raise ValueError("gemm operands need unit inner stride")
+    M = A.shape[1] if trans_a else A.shape[0]
+    K = A.shape[0] if trans_a else A.shape[1]
+    N = B.shape[0] if trans_b else B.shape[1]
+    Kb = B.shape[1] if trans_b else B.shape[0]
+    if K != Kb:
+        raise ValueError(f"gemm inner dims differ: {K} vs {Kb}")
+    if C is None:
+        C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    _lib.call("dlrm_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), _p(A),
+              A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0), epilogue, _p(bias), _p(aux),
+              aux.stride(0) if aux is not None else 0, _stream(A.device))
+    return C
+
+
+def colsum(Y: torch.Tensor, scale: Optional[torch.Tensor] = None, alpha: float = 1.0,
+           out: Optional[torch.Tensor] = None, accumulate: bool = False,
+           sgd_param: Optional[torch.Tensor] = None, lr: float = 0.0,
+           workspace: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    M, N = Y.shape
+    need = _lib.query("dlrm_colsum_workspace_size", M, N)
+    if workspace is None or workspace.numel() < need:
+        workspace = _ws("colsum", need, Y.device)
+    _lib.call("dlrm_colsum_f32", M, N, _p(Y), Y.stride(0), _p(scale), float(alpha), _p(out),
+              int(accumulate), _p(sgd_param), float(lr), _p(workspace), workspace.numel(),
+              _stream(Y.device))
+    return out
+
+
+def head_forward_backward(X: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
+                          target: Optional[torch.Tensor], loss: str = "mse",
+                          clamp_lo: float = 0.0, grad_scale: float = 1.0,
+                          prob: Optional[torch.Tensor] = None, dz: Optional[torch.Tensor] = None,
+                          loss_out: Optional[torch.Tensor] = None,
+                          workspace: Optional[torch.Tensor] = None):
+    M, K = X.shape
+    need = _lib.query("dlrm_head_workspace_size", M)
+    if workspace is None or workspace.numel() < need:
+        workspace = _ws("head", need, X.device)
+    _lib.call("dlrm_head_forward_backward", M, K, _p(X), X.stride(0), _p(w), _p(b), _p(target),
+              LOSS_BCE if loss == "bce" else LOSS_MSE, float(clamp_lo), float(grad_scale),
+              _p(prob), _p(dz), _p(loss_out), _p(workspace), workspace.numel(), _stream(X.device))
+    return prob, dz, loss_out
+
+
+def outer_drelu(dz: torch.Tensor, w: torch.Tensor, X: Optional[torch.Tensor], relu_mask: bool,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    M = dz.shape[0]
+    K = w.numel()
+    if out is None:
+        out = torch.empty((M, K), dtype=torch.float32, device=dz.device)
+    _lib.call("dlrm_outer_drelu", M, K, _p(dz), _p(w), _p(X), X.stride(0) if X is not None else 0,
+              int(relu_mask), _p(out), out.stride(0), _stream(dz.device))
+    return out
+
+
+def sigmoid_forward(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    x = x.contiguous()
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("dlrm_sigmoid_forward", x.numel(), _p(x), _p(out), _stream(x.device))
+    return out
+
+
+def sigmoid_backward(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    dy = dy.contiguous()
+    dx = torch.empty_like(dy)
+    _lib.call("dlrm_sigmoid_backward", dy.numel(), _p(dy), _p(y), _p(dx), _stream(dy.device))
+    return dx
+
+
+def relu_backward(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    dy = dy.contiguous()
+    dx = torch.empty_like(dy)
+    _lib.call("dlrm_relu_backward", dy.numel(), _p(dy), _p(y), _p(dx), _stream(dy.device))
+    return dx
+
+
+# ----------------------------------------------------------- optimizers ----
+def sgd_update(param: torch.Tensor, grad: torch.Tensor, lr: float) -> None:
+    _lib.call("dlrm_sgd_update", _p(param), _p(grad), param.numel(), float(lr),
+              _stream(param.device))
+
+
+def adagrad_update(param: torch.Tensor, grad: torch.Tensor, state_sum: torch.Tensor, clr: float,
+                   eps: float) -> None:
+    _lib.call("dlrm_adagrad_update", _p(param), _p(grad), _p(state_sum), param.numel(),
+              float(clr), float(eps), _stream(param.device))
+
+
+def scale_(x: torch.Tensor, alpha: float) -> None:
+    _lib.call("dlrm_scale_f32", _p(x), x.numel(), float(alpha), _stream(x.device))
+
+
+# -------------------------------------------------------------- utility ----
+def uniform_fill_(out: torch.Tensor, lo: float, hi: float, seed: int) -> torch.Tensor:
+    _lib.call("dlrm_uniform_fill", _p(out), out.numel(), float(lo), float(hi),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(out.device))
+    return out
+
+
+def uniform_int_fill_(out: torch.Tensor, hi: int, seed: int) -> torch.Tensor:
+    _lib.call("dlrm_uniform_int_fill", _p(out), _bits(out), out.numel(), int(hi),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(out.device))
+    return out
+
+
+def csr_from_tables(table_offsets: Sequence[torch.Tensor], table_nnz: Sequence[int], B: int,
+                    out_dtype=torch.int32) -> torch.Tensor:
+    """Device CSR builder: per-table int64 offsets [B] -> batched offsets [T*B+1]."""
+    T = len(table_offsets)
+    offs = [o if o.dtype == torch.int64 else o.long() for o in table_offsets]
+    _check_cuda(*offs)
+    out = torch.empty(T * B + 1, dtype=out_dtype, device=offs[0].device)
+    ptrs = (ctypes.c_void_p * T)(*[o.data_ptr() for o in offs])
+    nnz = (ctypes.c_int64 * T)(*[int(n) for n in table_nnz])
+    _lib.call("dlrm_csr_from_tables", T, B, ptrs, nnz, _p(out),
+              32 if out_dtype == torch.int32 else 64, _stream(offs[0].device))
+    return out

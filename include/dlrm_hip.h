@@ -1,0 +1,283 @@
+/*
+ * dlrm_hip.h — C-ABI of the MI355X-native (gfx950) DLRM training hot path.
+ *
+ * This is the drop-in boundary between the Python host layer (a mirror of the
+ * reference's DLRM_Net / TableBatchedEmbeddingBags / ext_dist surface) and the
+ * hand-written CDNA4 HIP kernels in dlrm-yx_amd/csrc.  Every entry point:
+ *   - takes plain device pointers, sizes and a hipStream_t (no torch types);
+ *   - enqueues asynchronously on the caller's stream and never synchronises,
+ *     allocates or frees device memory (workspaces come from the caller, sized
+ *     by the *_workspace_size() queries) — so every call is hipGraph-capturable;
+ *   - returns an int status (DLRM_OK == 0) and never exit()s; the message for
+ *     the last failure on the calling thread is in dlrm_last_error();
+ *   - is reentrant: no mutable global state.
+ *
+ * Reference interfaces replaced (file:line in YuxinxinChen/dlrm-yx):
+ *   dlrm_tbe_forward          <- torch.ops.batched_forward.forward
+ *                                (yx_modfs/batched_forward.cpp:4-13,
+ *                                 yx_modfs/table_batched_embeddings_cuda_yx.cu:317-389)
+ *                                and nn.EmbeddingBag(mode="sum") forward as called by
+ *                                DLRM_Net.apply_emb (dlrm_s_pytorch.py:526-587),
+ *                                TableBatchedEmbeddingBags.__call__ (dlrm_s_pytorch.py:321-334,589-591)
+ *   dlrm_tbe_backward_sgd     <- EmbeddingBag sparse backward + torch.optim.SGD sparse
+ *                                add_ (dlrm_s_pytorch.py:1923-1934), i.e. the exact-SGD
+ *                                TBE backward of create_emb_batched (dlrm_s_pytorch.py:321-334)
+ *   dlrm_tbe_backward_rowwise_adagrad
+ *                             <- RWSAdagrad.step sparse branch (optim/rwsadagrad.py:92-115)
+ *   dlrm_qr_split_indices / dlrm_qr_combine_* <- QREmbeddingBag.forward
+ *                                (tricks/qr_embedding_bag.py:156-174)
+ *   dlrm_interact_dot_*       <- DLRM_Net.interact_features, "dot" branch
+ *                                (dlrm_s_pytorch.py:627-659)
+ *   dlrm_interact_cat_*       <- DLRM_Net.interact_features, "cat" branch
+ *                                (dlrm_s_pytorch.py:660-665)
+ *   dlrm_gemm_f32             <- nn.Linear (+ReLU) forward/backward inside
+ *                                DLRM_Net.create_mlp/apply_mlp (dlrm_s_pytorch.py:227-265,518-524)
+ *   dlrm_colsum_f32           <- Linear bias gradient (sum over the batch)
+ *   dlrm_head_forward_backward<- last Linear + Sigmoid + loss_fn_wrap (mse/bce)
+ *                                (dlrm_s_pytorch.py:170-178,504-516,1907)
+ *   dlrm_sgd_update / dlrm_adagrad_update
+ *                             <- torch.optim.SGD.step dense branch / RWSAdagrad dense
+ *                                branch (optim/rwsadagrad.py:117-120)
+ *   dlrm_uniform_fill         <- np.random.uniform table init (dlrm_s_pytorch.py:304-308),
+ *                                device-side for tables too large for host init
+ *   dlrm_csr_from_tables      <- table-batched CSR flatten (dlrm_data_pytorch.py:748-753,834-843)
+ */
+#ifndef DLRM_HIP_H_
+#define DLRM_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* hipStream_t is an opaque pointer; declared here so the header needs no HIP headers. */
+typedef struct ihipStream_t* dlrm_stream_t;
+
+enum dlrm_status {
+  DLRM_OK = 0,
+  DLRM_ERR_INVALID_ARG = 1, /* null pointer / bad enum / negative size          */
+  DLRM_ERR_SHAPE = 2,       /* inconsistent shapes or alignment                 */
+  DLRM_ERR_UNSUPPORTED = 3, /* shape the kernels do not handle                  */
+  DLRM_ERR_WORKSPACE = 4,   /* workspace smaller than *_workspace_size()        */
+  DLRM_ERR_HIP = 5          /* a HIP launch/runtime error                       */
+};
+
+/* GEMM epilogues (C[m][n] <- f(alpha * acc[m][n], ...)). */
+enum dlrm_epilogue {
+  DLRM_EPI_STORE = 0,     /* C = alpha*acc                                      */
+  DLRM_EPI_BIAS = 1,      /* C = alpha*acc + bias[n]                            */
+  DLRM_EPI_BIAS_RELU = 2, /* C = max(alpha*acc + bias[n], 0)      (Linear+ReLU) */
+  DLRM_EPI_DRELU = 3,     /* C = alpha*acc * (aux[m][n] > 0)      (ReLU bwd)    */
+  DLRM_EPI_SGD = 4,       /* C = C - alpha*acc                    (fused SGD)   */
+  DLRM_EPI_ACCUM = 5      /* C = C + alpha*acc                                  */
+};
+
+enum dlrm_loss { DLRM_LOSS_MSE = 0, DLRM_LOSS_BCE = 1 };
+
+enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
+
+/* ---------------------------------------------------------------- library -- */
+int dlrm_abi_version(void);
+const char* dlrm_last_error(void);
+
+/* ------------------------------------------------ table-batched embedding -- */
+/*
+ * Pooled-sum lookup for T tables stored row-concatenated in one [total_rows][D]
+ * fp32 buffer.  Table t owns rows [row_base[t], row_base[t+1]) (row_base: device
+ * int64 [T+1]).  Bags are the CSR of the reference's batched layout: bag
+ * (t, b) = t*B + b covers lookups [offsets[bag], offsets[bag+1]), offsets has
+ * T*B+1 entries (device, int32 or int64 by offset_bits), indices are table-local
+ * rows (device, int32 or int64 by index_bits).
+ *   out[b*out_batch_stride + t*D + d] = sum_l w_l * W[row_base[t] + indices[l]][d]
+ * (w_l = per_sample_weights[l], or 1 when per_sample_weights == NULL), summed in
+ * lookup order in fp32.  An out-of-range index contributes nothing and sets
+ * *error_flag = 1 (error_flag may be NULL).
+ */
+int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base, int32_t T,
+                     int32_t B, const void* indices, int32_t index_bits, const void* offsets,
+                     int32_t offset_bits, const float* per_sample_weights, float* out,
+                     int64_t out_batch_stride, int32_t* error_flag, dlrm_stream_t stream);
+
+/* Workspace for the deterministic (sorted, segment-reduced) backward. */
+size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows);
+
+/*
+ * Exact-SGD backward fused with the update: for every lookup l of bag (t,b),
+ *   W[row_base[t]+indices[l]] -= lr * w_l * grad_out[b*grad_batch_stride + t*D + :]
+ * Duplicate rows are combined deterministically: lookups are radix-sorted by
+ * global row (stable), and each unique row is read once, updated in lookup order
+ * and written once.  num_lookups = length of indices.
+ */
+int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, int32_t T,
+                          int32_t B, const void* indices, int32_t index_bits,
+                          const void* offsets, int32_t offset_bits, int64_t num_lookups,
+                          int64_t total_rows, const float* per_sample_weights,
+                          const float* grad_out, int64_t grad_batch_stride, float lr,
+                          void* workspace, size_t workspace_bytes, dlrm_stream_t stream);
+
+/*
+ * Row-wise sparse Adagrad (RWSAdagrad, optim/rwsadagrad.py:92-115) fused into the
+ * backward: per unique row r with coalesced gradient g_r (sum over its lookups),
+ *   momentum[r] += mean_d(g_r[d]^2);  W[r] -= lr * g_r / (sqrt(momentum[r]) + eps)
+ * momentum: device fp32 [total_rows].
+ */
+int dlrm_tbe_backward_rowwise_adagrad(float* weights, float* momentum, int64_t D,
+                                      const int64_t* row_base, int32_t T, int32_t B,
+                                      const void* indices, int32_t index_bits,
+                                      const void* offsets, int32_t offset_bits,
+                                      int64_t num_lookups, int64_t total_rows,
+                                      const float* per_sample_weights, const float* grad_out,
+                                      int64_t grad_batch_stride, float lr, float eps,
+                                      void* workspace, size_t workspace_bytes,
+                                      dlrm_stream_t stream);
+
+/*
+ * Dense (non-fused) embedding-bag gradient scatter: grad_weights[row] += w_l * g
+ * for every lookup, deterministic (same sort), into a zero-initialised (or
+ * accumulating) [total_rows][D] buffer.  Used when the caller owns the optimizer.
+ */
+int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_base,
+                            int32_t T, int32_t B, const void* indices, int32_t index_bits,
+                            const void* offsets, int32_t offset_bits, int64_t num_lookups,
+                            int64_t total_rows, const float* per_sample_weights,
+                            const float* grad_out, int64_t grad_batch_stride, void* workspace,
+                            size_t workspace_bytes, dlrm_stream_t stream);
+
+/*
+ * Sparse-gradient values of an EmbeddingBag(sparse=True) backward
+ * (torch _embedding_bag_sparse_backward as reached from dlrm_s_pytorch.py:1929):
+ *   values[l][:] = w_l * grad_out[b*grad_batch_stride + t*D + :] for lookup l of bag (t,b)
+ * values: [num_lookups][D]; lookups outside every bag get zeros.
+ */
+int dlrm_tbe_expand_grad(int64_t D, int32_t T, int32_t B, const void* offsets,
+                         int32_t offset_bits, int64_t num_lookups,
+                         const float* per_sample_weights, const float* grad_out,
+                         int64_t grad_batch_stride, float* values, dlrm_stream_t stream);
+
+/* -------------------------------------------------- QR embeddings (C4) ---- */
+/* q[l] = trunc((float)idx[l] / (float)collisions), r[l] = idx[l] mod collisions
+ * (tricks/qr_embedding_bag.py:157-158 semantics, float division included). */
+int dlrm_qr_split_indices(const void* indices, int32_t index_bits, int64_t n,
+                          int64_t collisions, int64_t* q_out, int64_t* r_out,
+                          dlrm_stream_t stream);
+/* out = op(eq, er) elementwise over n_rows rows of D (concat: out row = [eq|er]). */
+int dlrm_qr_combine_forward(int32_t op, int64_t n_rows, int64_t D, const float* eq,
+                            const float* er, float* out, dlrm_stream_t stream);
+int dlrm_qr_combine_backward(int32_t op, int64_t n_rows, int64_t D, const float* eq,
+                             const float* er, const float* grad_out, float* grad_eq,
+                             float* grad_er, dlrm_stream_t stream);
+
+/* ------------------------------------------------------------ interaction -- */
+/*
+ * Feature f of sample b lives at feat_ptrs[f] + b*feat_bstrides[f] (D floats);
+ * feature 0 is the bottom-MLP output.  feat_ptrs / feat_bstrides are HOST arrays
+ * of F entries (copied into kernel arguments; F <= 64).
+ * Dot: out[b][0:D] = feature0, out[b][D + p] = <T_i, T_j> for the p-th pair of the
+ * row-major lower triangle (i > j, or i >= j when self_interaction), as
+ * torch.tril_indices(F, F, -1 or 0).
+ */
+int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D, const float* const* feat_ptrs,
+                              const int64_t* feat_bstrides, int32_t self_interaction,
+                              float* out, int64_t ld_out, dlrm_stream_t stream);
+/* Writes (overwrites) grad of every feature: grad_ptrs[f] + b*grad_bstrides[f]. */
+int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
+                               const float* const* feat_ptrs, const int64_t* feat_bstrides,
+                               int32_t self_interaction, const float* grad_out,
+                               int64_t ld_gout, float* const* grad_ptrs,
+                               const int64_t* grad_bstrides, dlrm_stream_t stream);
+/* Cat: out[b][f*D:(f+1)*D] = feature f. */
+int dlrm_interact_cat_forward(int32_t B, int32_t F, int32_t D, const float* const* feat_ptrs,
+                              const int64_t* feat_bstrides, float* out, int64_t ld_out,
+                              dlrm_stream_t stream);
+int dlrm_interact_cat_backward(int32_t B, int32_t F, int32_t D, const float* grad_out,
+                               int64_t ld_gout, float* const* grad_ptrs,
+                               const int64_t* grad_bstrides, dlrm_stream_t stream);
+
+/* ------------------------------------------------------------------- MLP --- */
+/*
+ * C[M][N] = epilogue(alpha * op(A)[M][K] . op(B)[K][N]) in exact fp32 on the
+ * gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32), row-major everywhere:
+ *   op(A)(m,k) = trans_a ? A[k*lda + m] : A[m*lda + k]
+ *   op(B)(k,n) = trans_b ? B[n*ldb + k] : B[k*ldb + n]
+ * Linear forward  Y = X W^T + b : trans_a=0, trans_b=1, EPI_BIAS[_RELU]
+ * Linear dgrad    dX = dY W     : trans_a=0, trans_b=0, EPI_STORE / EPI_DRELU
+ * Linear wgrad    dW = dY^T X   : trans_a=1, trans_b=0, EPI_STORE / EPI_SGD
+ */
+int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                  float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
+                  float* C, int64_t ldc, int32_t epilogue, const float* bias,
+                  const float* aux, int64_t ld_aux, dlrm_stream_t stream);
+
+/* Workspace for dlrm_colsum_f32 (deterministic two-pass column reduction). */
+size_t dlrm_colsum_workspace_size(int64_t M, int64_t N);
+/*
+ * s[n] = sum_m scale[m] * Y[m*ldy + n]   (scale may be NULL == 1), fixed order.
+ * If out != NULL: out[n] = alpha * s[n] (or out[n] += alpha*s[n] when accumulate).
+ * If sgd_param != NULL: sgd_param[n] -= lr * s[n].
+ */
+int dlrm_colsum_f32(int64_t M, int64_t N, const float* Y, int64_t ldy, const float* scale,
+                    float alpha, float* out, int32_t accumulate, float* sgd_param, float lr,
+                    void* workspace, size_t workspace_bytes, dlrm_stream_t stream);
+
+/* Workspace for dlrm_head_forward_backward. */
+size_t dlrm_head_workspace_size(int64_t M);
+/*
+ * Last layer (K -> 1) + sigmoid + mean loss + its gradient, fused:
+ *   z[m] = X[m].w + b; p[m] = sigmoid(z[m]); (optional clamp to [lo, 1-lo] when
+ *   0 < clamp_lo < 0.5); loss = mean_m l(p_c[m], t[m]) (mse | bce with log >= -100)
+ *   dz[m] = grad_scale * dloss/dz[m]
+ * prob_out[M], dz_out[M] and *loss_out are device buffers (any may be NULL).
+ */
+int dlrm_head_forward_backward(int64_t M, int64_t K, const float* X, int64_t ldx,
+                               const float* w, const float* b, const float* target,
+                               int32_t loss_kind, float clamp_lo, float grad_scale,
+                               float* prob_out, float* dz_out, float* loss_out, void* workspace,
+                               size_t workspace_bytes, dlrm_stream_t stream);
+
+/* Elementwise: dX[m][k] = dz[m] * w[k] * (relu_mask ? (X[m][k] > 0) : 1). */
+int dlrm_outer_drelu(int64_t M, int64_t K, const float* dz, const float* w, const float* X,
+                     int64_t ldx, int32_t relu_mask, float* dX, int64_t lddx,
+                     dlrm_stream_t stream);
+
+/* ----------------------------------------------------------- optimizers ---- */
+int dlrm_sgd_update(float* param, const float* grad, int64_t n, float lr, dlrm_stream_t stream);
+/* state_sum += g^2; param -= clr * g / (sqrt(state_sum) + eps) */
+int dlrm_adagrad_update(float* param, const float* grad, float* state_sum, int64_t n, float clr,
+                        float eps, dlrm_stream_t stream);
+int dlrm_scale_f32(float* x, int64_t n, float alpha, dlrm_stream_t stream);
+
+/* Elementwise activations (nn.Sigmoid / nn.ReLU forward & backward on n floats). */
+int dlrm_sigmoid_forward(int64_t n, const float* x, float* y, dlrm_stream_t stream);
+/* dx = dy * (1 - y) * y */
+int dlrm_sigmoid_backward(int64_t n, const float* dy, const float* y, float* dx,
+                          dlrm_stream_t stream);
+/* dx = dy * (y > 0) */
+int dlrm_relu_backward(int64_t n, const float* dy, const float* y, float* dx,
+                       dlrm_stream_t stream);
+
+/* ------------------------------------------------------------- utilities --- */
+/* out[i] = lo + (hi - lo) * u_i, u_i uniform in [0,1) from a counter hash of (seed, i). */
+int dlrm_uniform_fill(float* out, int64_t n, float lo, float hi, uint64_t seed,
+                      dlrm_stream_t stream);
+/* Integer uniform draws in [0, hi) for synthetic indices (int32 or int64 out). */
+int dlrm_uniform_int_fill(void* out, int32_t out_bits, int64_t n, int64_t hi, uint64_t seed,
+                          dlrm_stream_t stream);
+
+/*
+ * Device CSR builder (dlrm_data_pytorch.py:748-753): T per-table offset arrays
+ * (each B starts, table-local, first == 0) + per-table index counts ->
+ * batched offsets [T*B+1] (int32/int64 by out_offset_bits):
+ *   out[t*B + b] = table_start[t] + offsets_t[b], out[T*B] = table_start[T]
+ * table_offsets: host array of T device pointers (int64 each, B entries);
+ * table_nnz: host int64 [T] (indices per table).
+ */
+int dlrm_csr_from_tables(int32_t T, int32_t B, const int64_t* const* table_offsets,
+                         const int64_t* table_nnz, void* out_offsets, int32_t out_offset_bits,
+                         dlrm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLRM_HIP_H_ */

@@ -1,0 +1,329 @@
+"""HIP kernels (through the C-ABI) vs the oracle / golden fixtures, on the GPU."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import fp32_close
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from dlrm_hip import ops as _ops
+    return _ops
+
+
+def _csr_from_golden(g, idx_dtype=torch.int32):
+    T = len(g["rows"])
+    lo = [torch.tensor(g[f"lS_o{t}"]) for t in range(T)]
+    li = [torch.tensor(g[f"lS_i{t}"]) for t in range(T)]
+    off, idx = O.batched_csr(lo, li)
+    rows = [int(r) for r in g["rows"]]
+    row_base = torch.tensor(np.concatenate([[0], np.cumsum(rows)]), dtype=torch.int64)
+    W = torch.cat([torch.tensor(g[f"w0_{t}"]) for t in range(T)], 0)
+    return off, idx.to(idx_dtype), row_base, W, rows
+
+
+@pytest.mark.parametrize("D", [4, 16, 64, 128])
+@pytest.mark.parametrize("idx_dtype", [torch.int32, torch.int64])
+def test_tbe_forward_golden(ops, golden, D, idx_dtype):
+    g = golden(f"tbe_D{D}.npz")
+    off, idx, row_base, W, rows = _csr_from_golden(g, idx_dtype)
+    T, B = len(rows), int(g["B"][0])
+    out = ops.tbe_forward(W.to(dev), row_base.to(dev), T, B, idx.to(dev),
+                          off.to(dev, idx_dtype)).cpu()
+    for t in range(T):  # sequential fp32 sum in lookup order == CPU EmbeddingBag
+        ok, msg = fp32_close(out[:, t].numpy(), g[f"out{t}"])
+        assert ok, (t, msg)
+
+
+@pytest.mark.parametrize("D", [4, 16, 64, 128])
+def test_tbe_backward_sgd_golden(ops, golden, D):
+    g = golden(f"tbe_D{D}.npz")
+    off, idx, row_base, W, rows = _csr_from_golden(g)
+    T, B = len(rows), int(g["B"][0])
+    grad = torch.stack([torch.tensor(g[f"g{t}"]) for t in range(T)], 1)  # [B, T, D]
+    Wd = W.to(dev)
+    ops.tbe_backward("sgd", Wd, row_base.to(dev), T, B, idx.to(dev), off.to(dev), grad.to(dev),
+                     lr=0.1)
+    W1 = Wd.cpu().split(rows, 0)
+    for t in range(T):
+        ok, msg = fp32_close(W1[t].numpy(), g[f"w1_{t}"])
+        assert ok, (t, msg)
+
+
+def test_tbe_weighted_and_dense_grad(ops):
+    torch.manual_seed(0)
+    rows, D, B = [300, 7, 50], 32, 24
+    T = len(rows)
+    W = torch.randn(sum(rows), D)
+    lo, li = [], []
+    for n in rows:
+        lens = torch.randint(0, 9, (B,))
+        lo.append(torch.cat([torch.zeros(1, dtype=torch.int64), lens.cumsum(0)[:-1]]))
+        li.append(torch.randint(0, n, (int(lens.sum()),)))
+    off, idx = O.batched_csr(lo, li)
+    psw = torch.rand(idx.numel())
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64)
+    out = ops.tbe_forward(W.to(dev), row_base.to(dev), T, B, idx.to(dev), off.to(dev),
+                          per_sample_weights=psw.to(dev)).cpu()
+    Ws = W.split(rows, 0)
+    pw = psw.split([x.numel() for x in li])
+    for t in range(T):
+        ref = torch.nn.functional.embedding_bag(li[t], Ws[t], lo[t], mode="sum",
+                                                per_sample_weights=pw[t])
+        ok, msg = fp32_close(out[:, t].numpy(), ref.numpy())
+        assert ok, msg
+    # dense gradient accumulation == index_add of the expanded per-lookup grads
+    G = torch.randn(B, T, D)
+    gw = torch.zeros_like(W).to(dev)
+    ops.tbe_backward("dense", gw, row_base.to(dev), T, B, idx.to(dev), off.to(dev), G.to(dev),
+                     per_sample_weights=psw.to(dev))
+    ref = torch.zeros_like(W)
+    for t in range(T):
+        Wt = Ws[t].clone().requires_grad_(True)
+        y = torch.nn.functional.embedding_bag(li[t], Wt, lo[t], mode="sum",
+                                              per_sample_weights=pw[t])
+        (y * G[:, t]).sum().backward()
+        ref[row_base[t]:row_base[t + 1]] = Wt.grad
+    ok, msg = fp32_close(gw.cpu().numpy(), ref.numpy())
+    assert ok, msg
+    vals = ops.tbe_expand_grad(D, T, B, off.to(dev), idx.numel(), G.to(dev),
+                               per_sample_weights=psw.to(dev)).cpu()
+    bag = torch.repeat_interleave(torch.arange(T * B), off[1:] - off[:-1])
+    ref_vals = G.permute(1, 0, 2).reshape(T * B, D)[bag] * psw[:, None]
+    ok, msg = fp32_close(vals.numpy(), ref_vals.numpy())
+    assert ok, msg
+
+
+def test_tbe_out_of_range_flag(ops):
+    W = torch.randn(10, 8, device=dev)
+    row_base = torch.tensor([0, 10], dtype=torch.int64, device=dev)
+    off = torch.tensor([0, 2, 3], dtype=torch.int32, device=dev)
+    idx = torch.tensor([1, 12, 3], dtype=torch.int32, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = ops.tbe_forward(W, row_base, 1, 2, idx, off, error_flag=flag)
+    assert flag.item() == 1
+    assert torch.allclose(out[0, 0], W[1]) and torch.allclose(out[1, 0], W[3])
+
+
+def test_tbe_rowwise_adagrad_matches_oracle(ops):
+    torch.manual_seed(1)
+    rows, D, B = [40, 3], 16, 10
+    T = len(rows)
+    W = torch.randn(sum(rows), D)
+    lo, li = [], []
+    for n in rows:
+        lens = torch.randint(0, 6, (B,))
+        lo.append(torch.cat([torch.zeros(1, dtype=torch.int64), lens.cumsum(0)[:-1]]))
+        li.append(torch.randint(0, n, (int(lens.sum()),)))
+    off, idx = O.batched_csr(lo, li)
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64)
+    mom = torch.zeros(sum(rows))
+    Wd, md = W.to(dev), mom.to(dev)
+    ref_params = [torch.nn.Parameter(w.clone()) for w in W.split(rows, 0)]
+    opt = O.RWSAdagradOracle(ref_params, lr=0.05)
+    for step in range(3):
+        G = torch.randn(B, T, D)
+        ops.tbe_backward("rowwise_adagrad", Wd, row_base.to(dev), T, B, idx.to(dev), off.to(dev),
+                         G.to(dev), lr=0.05, eps=1e-10, momentum=md)
+        opt.zero_grad()
+        for t in range(T):
+            y = torch.nn.functional.embedding_bag(li[t], ref_params[t], lo[t], mode="sum",
+                                                  sparse=True)
+            (y * G[:, t]).sum().backward()
+        opt.step()
+        ok, msg = fp32_close(Wd.cpu().numpy(), torch.cat([p.data for p in ref_params]).numpy())
+        assert ok, (step, msg)
+
+
+@pytest.mark.parametrize("case", ["F4_D4_s0", "F9_D64_s0", "F27_D128_s0", "F27_D16_s0",
+                                  "F9_D64_s1", "F27_D128_s1"])
+def test_interaction_golden(ops, golden, case):
+    g = golden(f"interact_{case}.npz")
+    itself = bool(g["itself"][0])
+    x = torch.tensor(g["x"]).to(dev)
+    ly = torch.tensor(g["ly"]).to(dev)  # [B, T, D]
+    R = ops.interact_forward("dot", x, ly, itself).cpu()
+    ok, msg = fp32_close(R.numpy(), g["R"])
+    assert ok, msg
+    gx, gly = ops.interact_backward("dot", x, ly, torch.tensor(g["g"]).to(dev), itself)
+    ok, msg = fp32_close(gx.cpu().numpy(), g["gx"])
+    assert ok, msg
+    ok, msg = fp32_close(gly.cpu().numpy(), g["gly"])
+    assert ok, msg
+    # list-of-[B, D] layout (the reference's apply_emb output) through the same kernel
+    lyl = [ly[:, t].contiguous() for t in range(ly.shape[1])]
+    R2 = ops.interact_forward("dot", x, lyl, itself).cpu()
+    assert torch.equal(R2, R)
+
+
+def test_interaction_large_F_generic_path(ops):
+    torch.manual_seed(2)
+    B, T, D = 5, 40, 8  # F = 41 > 32 -> VALU path
+    x, ly = torch.randn(B, D), torch.randn(B, T, D)
+    ref_x, ref_ly = x.clone().requires_grad_(True), ly.clone().requires_grad_(True)
+    R_ref = O.interact(ref_x, list(ref_ly.unbind(1)), "dot", False)
+    R = ops.interact_forward("dot", x.to(dev), ly.to(dev)).cpu()
+    ok, msg = fp32_close(R.numpy(), R_ref.detach().numpy())
+    assert ok, msg
+    gR = torch.randn_like(R)
+    (R_ref * gR).sum().backward()
+    gx, gly = ops.interact_backward("dot", x.to(dev), ly.to(dev), gR.to(dev))
+    ok, msg = fp32_close(gly.cpu().numpy(), ref_ly.grad.numpy())
+    assert ok, msg
+    ok, msg = fp32_close(gx.cpu().numpy(), ref_x.grad.numpy())
+    assert ok, msg
+
+
+def test_interaction_cat(ops, golden):
+    g = golden("interact_cat.npz")
+    R = ops.interact_forward("cat", torch.tensor(g["x"]).to(dev), torch.tensor(g["ly"]).to(dev))
+    assert np.array_equal(R.cpu().numpy(), g["R"])
+
+
+def gemm_close(C, ref, absprod, K):
+    """fp32 GEMM error bound vs an fp64 reference: |C - ref| <= 1e-5*max(1,|ref|) +
+    2*K*u*(|A||B|), u = 2^-24 (the deterministic dot-product bound gamma_K)."""
+    C, ref, absprod = (np.asarray(x, dtype=np.float64) for x in (C, ref, absprod))
+    tol = 1e-5 * np.maximum(1.0, np.abs(ref)) + 2.0 * K * 2.0 ** -24 * absprod
+    bad = np.abs(C - ref) > tol
+    if bad.any():
+        i = np.unravel_index(np.argmax(np.abs(C - ref) - tol), C.shape)
+        return False, f"at {i}: got {C[i]!r} ref {ref[i]!r} tol {tol[i]!r} ({bad.sum()} bad)"
+    return True, ""
+
+
+GEMM_SHAPES = [(2048, 1024, 479), (64, 64, 64), (100, 37, 13), (2, 4, 10), (1000, 1, 256),
+               (256, 512, 2048), (33, 129, 67)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_vs_fp64(ops, M, N, K, ta, tb):
+    torch.manual_seed(M + N + K)
+    A = torch.randn(K, M) if ta else torch.randn(M, K)
+    Bm = torch.randn(N, K) if tb else torch.randn(K, N)
+    opA = A.double().t() if ta else A.double()
+    opB = Bm.double().t() if tb else Bm.double()
+    ref = opA @ opB
+    C = ops.gemm(A.to(dev), Bm.to(dev), bool(ta), bool(tb)).cpu()
+    ok, msg = gemm_close(C.numpy(), ref.numpy(), (opA.abs() @ opB.abs()).numpy(), K)
+    assert ok, msg
+
+
+def test_gemm_epilogues(ops):
+    torch.manual_seed(3)
+    M, N, K = 300, 200, 130
+    X, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
+    ref = X.double() @ W.double().t() + b.double()
+    Y = ops.gemm(X.to(dev), W.to(dev), False, True, epilogue=ops.EPI_BIAS_RELU, bias=b.to(dev))
+    ap = X.double().abs() @ W.double().abs().t() + b.double().abs()
+    ok, msg = gemm_close(Y.cpu().numpy(), ref.clamp_min(0).numpy(), ap.numpy(), K)
+    assert ok, msg
+    aux = torch.randn(M, N)
+    dY = torch.randn(M, K)
+    ref = (dY.double() @ W.double().t()) * (aux > 0)
+    Z = ops.gemm(dY.to(dev), W.to(dev), False, True, epilogue=ops.EPI_DRELU, aux=aux.to(dev))
+    ap = dY.double().abs() @ W.double().abs().t()
+    ok, msg = gemm_close(Z.cpu().numpy(), ref.numpy(), ap.numpy(), K)
+    assert ok, msg
+    P = torch.randn(N, K)
+    Pd = P.to(dev)
+    G = torch.randn(M, N)
+    ops.gemm(G.to(dev), X.to(dev), True, False, C=Pd, alpha=0.1, epilogue=ops.EPI_SGD)
+    ap = P.double().abs() + 0.1 * (G.double().abs().t() @ X.double().abs())
+    ok, msg = gemm_close(Pd.cpu().numpy(), (P.double() - 0.1 * (G.double().t() @ X.double())).numpy(),
+                         ap.numpy(), M)
+    assert ok, msg
+
+
+def test_colsum_head_outer(ops):
+    torch.manual_seed(4)
+    M, N = 2048, 300
+    Y, s = torch.randn(M, N), torch.randn(M)
+    out = torch.empty(N, device=dev)
+    ops.colsum(Y.to(dev), out=out)
+    ok, msg = gemm_close(out.cpu().numpy(), Y.double().sum(0).numpy(),
+                         Y.double().abs().sum(0).numpy(), M)
+    assert ok, msg
+    ops.colsum(Y.to(dev), scale=s.to(dev), out=out)
+    sy = s.double()[:, None] * Y.double()
+    ok, msg = gemm_close(out.cpu().numpy(), sy.sum(0).numpy(), sy.abs().sum(0).numpy(), M)
+    assert ok, msg
+    K = 256
+    X, w, b = torch.randn(M, K).relu(), torch.randn(K) * 0.1, torch.randn(1)
+    t = torch.rand(M)
+    for loss in ("mse", "bce"):
+        prob = torch.empty(M, device=dev)
+        dz = torch.empty(M, device=dev)
+        L = torch.empty(1, device=dev)
+        ops.head_forward_backward(X.to(dev), w.to(dev), b.to(dev), t.to(dev), loss, prob=prob,
+                                  dz=dz, loss_out=L)
+        Xr = X.clone()
+        wr = w.clone().requires_grad_(True)
+        z = Xr @ wr + b
+        z.retain_grad()
+        p = torch.sigmoid(z)
+        fn = torch.nn.MSELoss() if loss == "mse" else torch.nn.BCELoss()
+        E = fn(p, t)
+        E.backward()
+        ok, msg = fp32_close(prob.cpu().numpy(), p.detach().numpy())
+        assert ok, msg
+        ok, msg = fp32_close(L.cpu().numpy(), [E.item()])
+        assert ok, msg
+        ok, msg = fp32_close(dz.cpu().numpy(), z.grad.numpy())
+        assert ok, msg
+    dX = ops.outer_drelu(dz, w.to(dev), X.to(dev), True).cpu()
+    ref = dz.cpu()[:, None] * w[None, :] * (X > 0)
+    ok, msg = fp32_close(dX.numpy(), ref.numpy())
+    assert ok, msg
+
+
+def test_dense_optimizers(ops):
+    torch.manual_seed(5)
+    p, g = torch.randn(1000), torch.randn(1000)
+    pd = p.to(dev)
+    ops.sgd_update(pd, g.to(dev), 0.1)
+    ok, msg = fp32_close(pd.cpu().numpy(), (p - 0.1 * g).numpy())
+    assert ok, msg
+    s = torch.rand(1000)
+    pd, sd = p.to(dev), s.to(dev)
+    ops.adagrad_update(pd, g.to(dev), sd, 0.05, 1e-10)
+    s_ref = s + g * g
+    ok, msg = fp32_close(pd.cpu().numpy(), (p - 0.05 * g / (s_ref.sqrt() + 1e-10)).numpy())
+    assert ok, msg
+
+
+def test_qr_split_and_combine(ops, golden):
+    g = golden("qr.npz")
+    q, r = ops.qr_split_indices(torch.tensor(g["split_idx"]).to(dev), 3)
+    assert np.array_equal(q.cpu().numpy(), g["split_q3"])
+    assert np.array_equal(r.cpu().numpy(), g["split_r3"])
+    eq, er = torch.randn(6, 4, device=dev), torch.randn(6, 4, device=dev)
+    for op in ("mult", "add", "concat"):
+        y = ops.qr_combine_forward(op, eq, er)
+        ref = {"mult": eq * er, "add": eq + er, "concat": torch.cat([eq, er], 1)}[op]
+        assert torch.allclose(y, ref)
+
+
+def test_csr_builder_device(ops):
+    lo = [torch.tensor([0, 3, 5]), torch.tensor([0, 0, 2]), torch.tensor([0, 1, 4])]
+    li = [torch.arange(7), torch.arange(4), torch.arange(6)]
+    ref, _ = O.batched_csr(lo, li)
+    out = ops.csr_from_tables([o.to(dev) for o in lo], [7, 4, 6], 3)
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_uniform_fill(ops):
+    x = torch.empty(1 << 20, device=dev)
+    ops.uniform_fill_(x, -0.5, 0.25, 7)
+    assert x.min().item() >= -0.5 and x.max().item() < 0.25
+    assert abs(x.mean().item() + 0.125) < 2e-3
+    i = torch.empty(1 << 20, dtype=torch.int32, device=dev)
+    ops.uniform_int_fill_(i, 1000, 9)
+    assert i.min().item() >= 0 and i.max().item() == 999
