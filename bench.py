@@ -1,0 +1,304 @@
+#!/usr/bin/env python3
+"""DLRM training-step throughput on MI355X (samples/s, fwd + loss + bwd + update).
+
+Workload (BASELINE.json configs[3], the metric's headline config): MLPerf Terabyte-shaped
+synthetic DLRM — 26 tables with the terabyte row counts hashed to 1e7 (54,063,992 rows,
+27.7 GB fp32 resident in HBM), D=128, bottom 13-512-256-128, top 479-1024-1024-512-256-1,
+dot interaction, BCE, SGD lr 1.0, global batch 2048 (strong scaling over ranks, the
+reference methodology of bench/dlrm_s_benchmark.sh), one lookup per bag (Criteo one-hot).
+
+    python bench.py [--gpus N --steps K --warmup W]      # N>1 via torch.distributed.run
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dlrm-yx_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "DLRM samples/sec fwd+bwd at 1/2/4/8 MI355X; embedding HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: fp32 matrix peak (= vector peak)
+
+TERABYTE_ROWS = [10000000, 39043, 17289, 7420, 20263, 3, 7120, 1543, 63, 10000000, 2953546,
+                 403346, 10, 2208, 11938, 155, 4, 976, 14, 10000000, 10000000, 10000000, 585935,
+                 12972, 108, 36]
+KAGGLE_ROWS = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194,
+               27, 14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572]
+
+CONFIGS = {
+    "terabyte": dict(workload="mlperf_terabyte_synthetic", rows=TERABYTE_ROWS, D=128,
+                     bot=[13, 512, 256, 128], top=[1024, 1024, 512, 256, 1], B=2048, L=1,
+                     loss="bce", lr=1.0, optimizer="sgd"),
+    "terabyte_qr_rwsadagrad": dict(workload="mlperf_terabyte_synthetic+rwsadagrad",
+                                   rows=TERABYTE_ROWS, D=128, bot=[13, 512, 256, 128],
+                                   top=[1024, 1024, 512, 256, 1], B=2048, L=1, loss="bce",
+                                   lr=1.0, optimizer="rwsadagrad"),
+    "small": dict(workload="synthetic_small", rows=[100000] * 8, D=64, bot=[512, 512, 64],
+                  top=[1024, 1024, 1024, 1], B=2048, L=100, loss="mse", lr=0.1, optimizer="sgd"),
+    "kaggle": dict(workload="criteo_kaggle_synthetic", rows=KAGGLE_ROWS, D=16,
+                   bot=[13, 512, 256, 64, 16], top=[512, 256, 1], B=128, L=1, loss="bce", lr=0.1,
+                   optimizer="sgd"),
+}
+
+
+def num_int(T, D):
+    F = T + 1
+    return D + F * (F - 1) // 2
+
+
+def algorithmic_work(c, B_local, B_global, T_local, world):
+    """Per-step algorithmic FLOPs of the GEMM launches and bytes of the TBE kernels
+    (SURVEY.md §8d formulas)."""
+    D, L, T = c["D"], c["L"], len(c["rows"])
+    bot = c["bot"]
+    top = [num_int(T, D)] + c["top"]
+    layers = [(bot[i], bot[i + 1]) for i in range(len(bot) - 1)] + \
+             [(top[i], top[i + 1]) for i in range(len(top) - 2)]  # head (K->1) is not a GEMM
+    fl = 0
+    for li, (k, n) in enumerate(layers):
+        fl += 2 * B_local * n * k          # forward
+        fl += 2 * B_local * n * k          # wgrad
+        if li != 0:
+            fl += 2 * B_local * n * k      # dgrad (no dgrad for the bottom input layer)
+    # top first layer dgrad (into the interaction) is included (li != 0 for it)
+    s_idx = 4
+    lookups = T_local * B_global * L
+    fwd_bytes = lookups * (4 * D + s_idx) + 4 * (T_local * B_global + 1) + 4 * T_local * B_global * D
+    bwd_bytes = 4 * T_local * B_global * D + lookups * (s_idx + 8 * D)
+    return fl, fwd_bytes, bwd_bytes
+
+
+class KernelTimer:
+    """HIP-event brackets around kernel groups, on the stream the kernels run on."""
+
+    def __init__(self):
+        self.pending = []
+
+    def __call__(self, name):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self_inner):
+                self_inner.s = torch.cuda.Event(enable_timing=True)
+                self_inner.e = torch.cuda.Event(enable_timing=True)
+                self_inner.s.record()
+                return self_inner
+
+            def __exit__(self_inner, *a):
+                self_inner.e.record()
+                timer.pending.append((name, self_inner.s, self_inner.e))
+                return False
+        return _Ctx()
+
+    def totals(self):
+        torch.cuda.synchronize()
+        out, cnt = {}, {}
+        for name, s, e in self.pending:
+            out[name] = out.get(name, 0.0) + s.elapsed_time(e)
+            cnt[name] = cnt.get(name, 0) + 1
+        return out, cnt
+
+
+def cpu_baseline(c, seconds: float):
+    """The CPU oracle (a restatement of the reference step, pinned to its golden vectors)
+    timed on this host's cores: bounded sample of the same workload."""
+    sys.path.insert(0, ROOT)
+    import oracle as O
+    threads = torch.get_num_threads()
+    cap = 1_000_000
+    rows = [min(r, cap) for r in c["rows"]]
+    D = c["D"]
+    ln_top = [num_int(len(rows), D)] + c["top"]
+    B, L = c["B"], c["L"]
+    tables = []
+    g = torch.Generator().manual_seed(0)
+    for n in rows:
+        a = float(np.sqrt(1.0 / n))
+        tables.append(torch.empty(n, D).uniform_(-a, a, generator=g).numpy())
+    np.random.seed(0)
+    m = O.OracleDLRM(D, rows, c["bot"], ln_top, loss_function=c["loss"], tables=tables)
+    rng = np.random.RandomState(1)
+    batches = []
+    for _ in range(4):
+        X = torch.log1p(torch.tensor(rng.rand(B, c["bot"][0]).astype(np.float32)))
+        lS_o = torch.arange(B).mul(L).repeat(len(rows), 1)
+        lS_i = [torch.tensor(rng.randint(0, n, size=B * L)) for n in rows]
+        T = torch.tensor(np.round(rng.rand(B, 1)).astype(np.float32))
+        batches.append((X, lS_o, lS_i, T))
+    for i in range(2):
+        m.train_step(*batches[i % 4], c["lr"] * 0.01)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        m.train_step(*batches[n % 4], c["lr"] * 0.01)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 3) or n >= 2000:
+            break
+    return {"value": B * n / el, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (torch-CPU restatement of the reference step) on the "
+                      f"{c['workload']} shape with tables capped at {cap} rows, B={B}, "
+                      f"{n} timed steps ({el:.1f} s), {threads} threads",
+            "ms_per_step": 1000.0 * el / n}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="terabyte", choices=list(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="global batch (default: config's)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("error: --gpus N>1 must be launched with torch.distributed.run", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        pg = dist.group.WORLD
+
+    from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+
+    c = dict(CONFIGS[args.config])
+    B = args.batch or c["B"]
+    T = len(c["rows"])
+    ln_top = [num_int(T, c["D"])] + c["top"]
+    cfg = TrainerConfig(m_spa=c["D"], ln_emb=c["rows"], ln_bot=c["bot"], ln_top=ln_top,
+                        loss_function=c["loss"], learning_rate=c["lr"], optimizer=c["optimizer"],
+                        sharder="greedy")
+    tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, process_group=pg, seed=1)
+    nb = 10  # the reference cycles 10 pre-generated batches (dlrm_data_pytorch.py:631)
+    batches = [tr.synthetic_batch(B, c["L"], seed=100 + i) for i in range(nb)]
+    torch.cuda.synchronize()
+
+    use_graph = (world == 1) and not args.no_graph
+    graphs = None
+    if use_graph:
+        try:
+            for i in range(3):
+                tr.step(batches[i % nb])
+            torch.cuda.synchronize()
+            graphs = []
+            pool = torch.cuda.graph_pool_handle()
+            for i in range(nb):
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph, pool=pool):
+                    tr.step(batches[i])
+                graphs.append(gph)
+            torch.cuda.synchronize()
+        except Exception as e:  # capture unsupported -> eager
+            print(f"[bench] hipGraph capture failed ({e!r}); eager launches", file=sys.stderr)
+            graphs = None
+            use_graph = False
+
+    def run_step(k):
+        if graphs is not None:
+            graphs[k % nb].replay()
+        else:
+            tr.step(batches[k % nb])
+
+    for k in range(args.warmup):
+        run_step(k)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        run_step(k)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(el_t.item())
+    value = B * args.steps / elapsed
+    loss = float(tr._bufs[(B // world, B)]["loss"].item())
+
+    # ---- per-kernel HIP-event timing pass (same step, eager launches) for the roofline
+    roofline, emb_roof, groups = None, None, None
+    Bl = B // world
+    flops, fwd_bytes, bwd_bytes = algorithmic_work(c, Bl, B, tr.T_local, world)
+    if not args.no_kernel_timing:
+        timer = KernelTimer()
+        kt = max(5, min(args.steps, 20))
+        for k in range(kt):
+            tr.step(batches[k % nb], profile=timer)
+        tot, cnt = timer.totals()
+        groups = {k: round(v / kt * 1000.0, 2) for k, v in tot.items()}  # us per step
+        gemm_ms = tot.get("gemm", 0.0) / kt
+        if gemm_ms > 0:
+            ach = flops / (gemm_ms * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "kernel": "gemm_f32_mfma (all MLP GEMM launches)",
+                        "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS,
+                        "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFS, 4),
+                        "traffic": None, "launches_per_step": cnt.get("gemm", 0) // kt,
+                        "us_per_step": round(gemm_ms * 1000.0, 2),
+                        "algorithmic_flop_per_step": flops}
+        f_ms = tot.get("tbe_fwd", 0.0) / kt
+        b_ms = tot.get("tbe_bwd", 0.0) / kt
+        if f_ms > 0 and b_ms > 0:
+            emb_roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                        "fwd_achieved": round(fwd_bytes / (f_ms * 1e-3) / 1e9, 1),
+                        "fwd_frac": round(fwd_bytes / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "fwd_bytes": fwd_bytes, "fwd_us": round(f_ms * 1000.0, 2),
+                        "bwd_achieved_upper": round(bwd_bytes / (b_ms * 1e-3) / 1e9, 1),
+                        "bwd_bytes_upper": bwd_bytes, "bwd_us": round(b_ms * 1000.0, 2)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(c, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1000.0, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (device-generated, reference distributions; random init)",
+            "config": {"workload": c["workload"], "global_batch": B, "local_batch": Bl,
+                       "tables": T, "rows_total": int(sum(c["rows"])), "emb_dim": c["D"],
+                       "lookups_per_bag": c["L"], "bot": c["bot"], "top": ln_top,
+                       "optimizer": c["optimizer"], "parallelism": f"table-sharded emb x{world} + dp{world}",
+                       "hip_graph": use_graph},
+            "loss_last": loss,
+            "roofline": roofline,
+            "embedding_roofline": emb_roof,
+            "kernel_us_per_step": groups,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -318,9 +318,12 @@ def sigmoid_backward(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return dx
 
 
-def relu_backward(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+def relu_backward(dy: torch.Tensor, y: torch.Tensor,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     dy = dy.contiguous()
-    dx = torch.empty_like(dy)
+    if not y.is_contiguous():
+        raise ValueError("relu_backward needs a contiguous activation")
+    dx = torch.empty_like(dy) if out is None else out
     _lib.call("dlrm_relu_backward", dy.numel(), _p(dy), _p(y), _p(dx), _stream(dy.device))
     return dx
 

@@ -1,0 +1,537 @@
+"""Fused DLRM training step on MI355X: every FLOP and byte of the step goes through the
+HIP kernels of libdlrm_hip.so; torch provides device memory, streams and RCCL.
+
+One step = the reference iteration (dlrm_s_pytorch.py:1886-1934): forward
+(sequential_forward :732-770 or distributed_forward :686-730), loss, backward and the
+optimizer update.  Layout decisions (MI355X-first):
+
+* All local embedding tables live row-concatenated in ONE [sum rows, D] fp32 buffer with
+  64-bit row bases (C3 = 54 M rows x 128 = 27.7 GB, resident in HBM); the batch is the
+  reference's table-batched CSR (int32 offsets [T*B+1], int32 indices).
+* All MLP parameters live in ONE flat fp32 bucket (bottom then top, W then b per layer)
+  so the data-parallel gradient is one RCCL all-reduce and the dense update one kernel.
+  Every layer's input width is padded to a multiple of 4 floats (zero columns in both
+  the activation and the weight) so every GEMM operand row is 16-B aligned.
+* Single GPU: the optimizer is fused into the backward — wgrad GEMMs run with the SGD
+  epilogue (W -= lr * dY^T X after dX = dY W has consumed the old W), bias columns sums
+  apply their update, the embedding backward applies exact SGD per unique row.
+* Multi GPU (one process per GPU, RCCL over xGMI): tables are sharded table-wise with the
+  reference sharders; pooled embeddings go through one all_to_all_single per direction
+  (rank-major feature order, the W x embedding gradient of the reference is reproduced);
+  the bottom MLP overlaps the forward exchange, the backward exchange overlaps the bottom
+  MLP backward, and the dense all-reduce overlaps the embedding update.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+from .sharders import shard
+
+
+def _pad4(n: int) -> int:
+    return (int(n) + 3) // 4 * 4
+
+
+@dataclass
+class TrainerConfig:
+    m_spa: int
+    ln_emb: Sequence[int]
+    ln_bot: Sequence[int]
+    ln_top: Sequence[int]          # full top widths (first = number of interactions)
+    arch_interaction_op: str = "dot"
+    arch_interaction_itself: bool = False
+    loss_function: str = "mse"     # mse | bce
+    loss_threshold: float = 0.0
+    learning_rate: float = 0.01
+    emb_learning_rate: Optional[float] = None  # default: learning_rate
+    optimizer: str = "sgd"         # sgd | rwsadagrad
+    adagrad_eps: float = 1e-10
+    sharder: str = "greedy"
+    allocation: Optional[Sequence[int]] = None
+
+
+@dataclass
+class Batch:
+    X: torch.Tensor        # [B_local, Kp0] dense input (padded, zero pad columns)
+    offsets: torch.Tensor  # [T_local*B + 1] int32 CSR of the local tables, full batch
+    indices: torch.Tensor  # int32 table-local rows
+    target: torch.Tensor   # [B_local] fp32
+
+
+@dataclass
+class _Layer:
+    N: int
+    K: int
+    Kp: int
+    Np: int
+    W: torch.Tensor
+    b: torch.Tensor
+    gW: Optional[torch.Tensor] = None
+    gb: Optional[torch.Tensor] = None
+    sumW: Optional[torch.Tensor] = None  # Adagrad state views
+    sumb: Optional[torch.Tensor] = None
+
+
+class DLRMTrainer:
+    def __init__(self, cfg: TrainerConfig, device="cuda:0", rank: int = 0, world_size: int = 1,
+                 process_group=None, seed: int = 0, init: bool = True):
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        self.rank, self.world = rank, world_size
+        self.pg = process_group
+        D = int(cfg.m_spa)
+        if int(cfg.ln_bot[-1]) != D:
+            raise ValueError("trainer needs ln_bot[-1] == m_spa (the reference splits wider "
+                             "tables into D-sized features; not on this path)")
+        if D % 4:
+            raise ValueError("trainer needs the embedding dim to be a multiple of 4")
+        self.D = D
+        T = len(cfg.ln_emb)
+        self.T = T
+        if world_size > 1:
+            if T < world_size:
+                raise ValueError(f"only {T} tables for {world_size} ranks")
+            di = list(cfg.allocation) if cfg.allocation is not None else \
+                shard(list(cfg.ln_emb), world_size, cfg.sharder)
+        else:
+            di = [0] * T
+        self.device_indices = di
+        self.local_tables = [t for t in range(T) if di[t] == rank]
+        self.tables_per_rank = [sum(1 for t in range(T) if di[t] == r) for r in range(world_size)]
+        # rank-major global feature order after the all-to-all (extend_distributed.py:475-487)
+        self.feature_order = [t for r in range(world_size) for t in range(T) if di[t] == r]
+        self.T_local = len(self.local_tables)
+        rows = [int(cfg.ln_emb[t]) for t in self.local_tables]
+        self.rows_local = rows
+        self.row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64,
+                                     device=self.dev)
+        self.total_rows = int(sum(rows))
+        self.weights = torch.empty((max(self.total_rows, 1), D), dtype=torch.float32,
+                                   device=self.dev)
+        self.momentum = None
+        if cfg.optimizer == "rwsadagrad":
+            self.momentum = torch.zeros(max(self.total_rows, 1), dtype=torch.float32,
+                                        device=self.dev)
+        elif cfg.optimizer != "sgd":
+            raise ValueError(f"optimizer {cfg.optimizer!r} not supported")
+        # ---- dense parameters: one flat bucket
+        ln_bot, ln_top = [int(v) for v in cfg.ln_bot], [int(v) for v in cfg.ln_top]
+        if ln_top[-1] != 1:
+            raise ValueError("the fused head needs a single output (ln_top[-1] == 1)")
+        F = T + 1
+        if cfg.arch_interaction_op == "dot":
+            npairs = F * (F + 1) // 2 if cfg.arch_interaction_itself else F * (F - 1) // 2
+            self.num_int = D + npairs
+        else:
+            self.num_int = F * D
+        if ln_top[0] != self.num_int:
+            raise ValueError(f"ln_top[0]={ln_top[0]} != number of interactions {self.num_int}")
+        specs = [(ln_bot[i + 1], ln_bot[i]) for i in range(len(ln_bot) - 1)] + \
+                [(ln_top[i + 1], ln_top[i]) for i in range(len(ln_top) - 1)]
+        sizes = [n * _pad4(k) + n for n, k in specs]
+        self.n_params = int(sum(sizes))
+        self.params = torch.zeros(self.n_params, dtype=torch.float32, device=self.dev)
+        self.grads = torch.zeros_like(self.params) if (world_size > 1 or
+                                                      cfg.optimizer == "rwsadagrad") else None
+        self.adagrad_sum = torch.zeros_like(self.params) if cfg.optimizer == "rwsadagrad" else None
+        self.layers: List[_Layer] = []
+        o = 0
+        for n, k in specs:
+            kp = _pad4(k)
+            L = _Layer(N=n, K=k, Kp=kp, Np=_pad4(n),
+                       W=self.params[o:o + n * kp].view(n, kp),
+                       b=self.params[o + n * kp:o + n * kp + n])
+            if self.grads is not None:
+                L.gW = self.grads[o:o + n * kp].view(n, kp)
+                L.gb = self.grads[o + n * kp:o + n * kp + n]
+            o += n * kp + n
+            self.layers.append(L)
+        self.n_bot = len(ln_bot) - 1
+        self.bot = self.layers[:self.n_bot]
+        self.top = self.layers[self.n_bot:]
+        self._bufs = {}
+        self._tbe_ws: Optional[torch.Tensor] = None
+        self._colsum_ws: Optional[torch.Tensor] = None
+        self._head_ws: Optional[torch.Tensor] = None
+        self.step_count = 0
+        if init:
+            self.init_random(seed)
+
+    # ---------------------------------------------------------------- init --
+    def init_random(self, seed: int = 0):
+        """Reference-distribution random init on device: tables U(+-sqrt(1/n))
+        (dlrm_s_pytorch.py:304-308), W ~ N(0, sqrt(2/(m+n))), b ~ N(0, sqrt(1/m)) (:240-247)."""
+        for j, t in enumerate(self.local_tables):
+            n = int(self.cfg.ln_emb[t])
+            a = math.sqrt(1.0 / n)
+            view = self.weights[int(self.row_base[j].item()):int(self.row_base[j + 1].item())]
+            ops.uniform_fill_(view, -a, a, seed * 1000003 + t)
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(seed + 12345)
+        with torch.no_grad():
+            for L in self.layers:
+                L.W.zero_()
+                L.W[:, :L.K].normal_(0.0, math.sqrt(2.0 / (L.N + L.K)), generator=g)
+                L.b.normal_(0.0, math.sqrt(1.0 / L.N), generator=g)
+
+    def load_dense(self, mlp_params: Sequence[tuple], tables: Optional[Sequence] = None):
+        """Copy (W [N,K], b [N]) per layer (bottom then top) and optionally GLOBAL tables."""
+        with torch.no_grad():
+            for L, (W, b) in zip(self.layers, mlp_params):
+                L.W.zero_()
+                L.W[:, :L.K].copy_(torch.as_tensor(W))
+                L.b.copy_(torch.as_tensor(b))
+            if tables is not None:
+                for j, t in enumerate(self.local_tables):
+                    s, e = int(self.row_base[j].item()), int(self.row_base[j + 1].item())
+                    self.weights[s:e].copy_(torch.as_tensor(tables[t]))
+
+    @classmethod
+    def from_oracle(cls, cfg: TrainerConfig, ref, device="cuda:0", **kw):
+        """Build with the exact weights of an oracle.OracleDLRM (test/smoke helper)."""
+        tr = cls(cfg, device=device, init=False, **kw)
+        mlp = []
+        for seq in (ref.bot_l, ref.top_l):
+            for m in seq:
+                if isinstance(m, torch.nn.Linear):
+                    mlp.append((m.weight.detach(), m.bias.detach()))
+        tr.load_dense(mlp, [e.weight.detach() for e in ref.emb_l])
+        return tr
+
+    def dense_state(self):
+        return [(L.W[:, :L.K].detach().clone(), L.b.detach().clone()) for L in self.layers]
+
+    def table(self, t: int) -> torch.Tensor:
+        j = self.local_tables.index(t)
+        return self.weights[int(self.row_base[j].item()):int(self.row_base[j + 1].item())]
+
+    # ------------------------------------------------------------- batches --
+    @property
+    def lr(self) -> float:
+        return float(self.cfg.learning_rate)
+
+    @property
+    def emb_lr(self) -> float:
+        return float(self.cfg.emb_learning_rate if self.cfg.emb_learning_rate is not None
+                     else self.cfg.learning_rate)
+
+    def local_batch_size(self, B: int) -> int:
+        if B % self.world:
+            raise ValueError(f"batch {B} not divisible by {self.world} ranks "
+                             "(dlrm_s_pytorch.py:139-143)")
+        return B // self.world
+
+    def make_batch(self, X, lS_o, lS_i, target) -> Batch:
+        """From the reference's non-batched layout (X [B,m_den] GLOBAL batch, lS_o [T,B],
+        lS_i list of T index tensors) -> this rank's device Batch."""
+        B = X.shape[0]
+        Bl = self.local_batch_size(B)
+        sl = slice(self.rank * Bl, (self.rank + 1) * Bl)
+        L0 = self.bot[0]
+        Xp = torch.zeros((Bl, L0.Kp), dtype=torch.float32, device=self.dev)
+        Xp[:, :L0.K] = torch.as_tensor(X)[sl].to(self.dev)
+        offs, idxs, start = [], [], 0
+        for t in self.local_tables:
+            o = torch.as_tensor(lS_o[t]).to(torch.int64)
+            ii = torch.as_tensor(lS_i[t]).to(torch.int64)
+            offs.append(o + start)
+            idxs.append(ii)
+            start += ii.numel()
+        offsets = torch.cat(offs + [torch.tensor([start])]).to(torch.int32).to(self.dev)
+        indices = torch.cat(idxs).to(torch.int32).to(self.dev)
+        tg = torch.as_tensor(target).reshape(-1)[sl].to(torch.float32).to(self.dev)
+        return Batch(Xp, offsets, indices, tg)
+
+    def synthetic_batch(self, B: int, L: int, seed: int) -> Batch:
+        """Device-generated synthetic batch of the reference's shape: X ~ log(1+U[0,1))
+        (dlrm_data_pytorch.py:727), L uniform indices per bag per table, targets U[0,1)
+        (rounded for bce)."""
+        Bl = self.local_batch_size(B)
+        L0 = self.bot[0]
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(seed * 7919 + self.rank)
+        Xp = torch.zeros((Bl, L0.Kp), dtype=torch.float32, device=self.dev)
+        Xp[:, :L0.K] = torch.log1p(torch.rand((Bl, L0.K), generator=g, device=self.dev))
+        Tl = self.T_local
+        indices = torch.empty(Tl * B * L, dtype=torch.int32, device=self.dev)
+        for j, t in enumerate(self.local_tables):
+            ops.uniform_int_fill_(indices[j * B * L:(j + 1) * B * L], int(self.cfg.ln_emb[t]),
+                                  seed * 1000003 + t * 7 + 1)
+        offsets = torch.arange(0, Tl * B * L + 1, L, dtype=torch.int32, device=self.dev)
+        tg = torch.rand(Bl, generator=g, device=self.dev)
+        if self.cfg.loss_function == "bce":
+            tg = tg.round()
+        return Batch(Xp, offsets, indices, tg)
+
+    # ------------------------------------------------------------- buffers --
+    def _buffers(self, Bl: int, B: int):
+        key = (Bl, B)
+        if key in self._bufs:
+            return self._bufs[key]
+        dev, D = self.dev, self.D
+        f32 = dict(dtype=torch.float32, device=dev)
+        bufs = {}
+        bufs["bot_act"] = [torch.zeros((Bl, L.Np), **f32) for L in self.bot]
+        self.ldR = _pad4(self.num_int)
+        bufs["R"] = torch.zeros((Bl, self.ldR), **f32)
+        bufs["top_act"] = [torch.zeros((Bl, L.Np), **f32) for L in self.top[:-1]]
+        wmax = max([L.Kp for L in self.layers] + [self.ldR])
+        bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(2)]
+        bufs["dx"] = torch.zeros((Bl, D), **f32)
+        bufs["gx"] = torch.zeros((Bl, D), **f32)
+        bufs["E"] = torch.zeros((B, max(self.T_local, 1), D), **f32)
+        bufs["dE"] = torch.zeros_like(bufs["E"])
+        if self.world > 1:
+            bufs["recv"] = torch.zeros(self.T * Bl * D, **f32)
+            bufs["drecv"] = torch.zeros_like(bufs["recv"])
+        bufs["prob"] = torch.zeros(Bl, **f32)
+        bufs["dz"] = torch.zeros(Bl, **f32)
+        bufs["loss"] = torch.zeros(1, **f32)
+        self._bufs[key] = bufs
+        return bufs
+
+    def _features(self, bufs, Bl: int, grad: bool = False):
+        """(x, per-feature tensors) for the interaction: feature 0 = bottom-MLP output,
+        then the embedding features in rank-major order (single GPU: table order)."""
+        D = self.D
+        x = bufs["dx"] if grad else bufs["bot_act"][-1][:, :D]
+        if self.world == 1:
+            return x, bufs["dE" if grad else "E"]
+        flat = bufs["drecv" if grad else "recv"]
+        feats, o = [], 0
+        for r in range(self.world):
+            Tr = self.tables_per_rank[r]
+            chunk = flat[o:o + Bl * Tr * D].view(Bl, Tr, D)
+            feats.extend(chunk[:, j, :] for j in range(Tr))
+            o += Bl * Tr * D
+        return x, feats
+
+    # ---------------------------------------------------------------- step --
+    def step(self, batch: Batch, profile=None):
+        """One fwd + loss + bwd + update.  Returns (prob [B_local], loss [1]) device tensors.
+        ``profile``: optional callable(name) -> context manager around kernel groups."""
+        cfg = self.cfg
+        D = self.D
+        Bl = batch.X.shape[0]
+        B = Bl * self.world
+        bufs = self._buffers(Bl, B)
+        prof = profile or (lambda name: _NullCtx())
+        self._prof = prof
+        gemm = self._gemm
+        fused_opt = self.grads is None  # single GPU SGD: updates fused into backward
+        lr, elr = self.lr, self.emb_lr
+
+        # ---------------- forward: embeddings (full batch, local tables)
+        with prof("tbe_fwd"):
+            if self.T_local > 0:
+                ops.tbe_forward(self.weights, self.row_base, self.T_local, B, batch.indices,
+                                batch.offsets, out=bufs["E"])
+        work = None
+        if self.world > 1:
+            work = self._alltoall_fwd(bufs, Bl)
+        # ---------------- forward: bottom MLP (overlaps the exchange)
+        h = batch.X
+        for L, out in zip(self.bot, bufs["bot_act"]):
+            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_BIAS_RELU, bias=L.b)
+            h = out
+        if work is not None:
+            work.wait()
+        x, feats = self._features(bufs, Bl)
+        with prof("interaction_fwd"):
+            ops.interact_forward(cfg.arch_interaction_op, x, feats,
+                                 cfg.arch_interaction_itself, out=bufs["R"])
+        h = bufs["R"]
+        for L, out in zip(self.top[:-1], bufs["top_act"]):
+            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_BIAS_RELU, bias=L.b)
+            h = out
+        last = self.top[-1]
+        hin = h
+        with prof("head"):
+            ops.head_forward_backward(hin, last.W[0, :last.K], last.b, batch.target,
+                                      cfg.loss_function, cfg.loss_threshold, 1.0,
+                                      prob=bufs["prob"], dz=bufs["dz"], loss_out=bufs["loss"],
+                                      workspace=self._ws_head(Bl))
+        # ---------------- backward: head layer (K -> 1)
+        g_cur, g_nxt = bufs["g"]
+        dz = bufs["dz"]
+        gview = g_cur[:, :last.Kp]
+        prev_is_relu = len(self.top) > 1
+        with prof("head"):
+            ops.outer_drelu(dz, last.W[0, :last.Kp], hin if prev_is_relu else None, prev_is_relu,
+                            out=gview)
+        self._bias_and_w_head(last, hin, dz, fused_opt, lr)
+        g = gview
+        # top hidden layers, last to first
+        for li in range(len(self.top) - 2, -1, -1):
+            L = self.top[li]
+            inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
+            dinp = g_nxt[:, :L.Kp]
+            if li > 0:
+                gemm(g[:, :L.N], L.W, C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
+            else:
+                gemm(g[:, :L.N], L.W, C=dinp)
+            self._wgrad(L, g, inp, fused_opt, lr)
+            g = dinp
+            g_cur, g_nxt = g_nxt, g_cur
+        # ---------------- backward: interaction -> dR = g
+        xg, gfeats = self._features(bufs, Bl, grad=True)
+        with prof("interaction_bwd"):
+            ops.interact_backward(cfg.arch_interaction_op, x, feats, g[:, :self.num_int],
+                                  cfg.arch_interaction_itself, grad_x=xg, grad_ly=gfeats)
+        work = None
+        if self.world > 1:
+            work = self._alltoall_bwd(bufs, Bl)
+        # ---------------- backward: bottom MLP (overlaps the reverse exchange)
+        xin = bufs["bot_act"][-1]
+        with prof("relu_bwd"):
+            g = ops.relu_backward(bufs["dx"], xin, out=bufs["gx"])
+        for li in range(self.n_bot - 1, -1, -1):
+            L = self.bot[li]
+            inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
+            if li > 0:
+                dinp = g_nxt[:, :L.Kp]
+                gemm(g[:, :L.N], L.W, C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
+            self._wgrad(L, g, inp, fused_opt, lr)
+            if li > 0:
+                g = dinp
+                g_cur, g_nxt = g_nxt, g_cur
+        ar = None
+        if self.world > 1:
+            ar = self._allreduce_dense()
+        # ---------------- backward: embeddings + fused update
+        if work is not None:
+            work.wait()
+        with prof("tbe_bwd"):
+            if self.T_local > 0:
+                mode = "rowwise_adagrad" if cfg.optimizer == "rwsadagrad" else "sgd"
+                ops.tbe_backward(mode, self.weights, self.row_base, self.T_local, B,
+                                 batch.indices, batch.offsets, bufs["dE"], lr=elr,
+                                 eps=cfg.adagrad_eps, momentum=self.momentum,
+                                 workspace=self._ws_tbe(batch.indices.numel()))
+        if ar is not None:
+            ar.wait()
+        if not fused_opt:
+            with prof("dense_update"):
+                scale = 1.0 / self.world
+                if cfg.optimizer == "sgd":
+                    ops.sgd_update(self.params, self.grads, lr * scale)
+                else:
+                    if scale != 1.0:
+                        ops.scale_(self.grads, scale)
+                    ops.adagrad_update(self.params, self.grads, self.adagrad_sum, lr,
+                                       cfg.adagrad_eps)
+        self.step_count += 1
+        return bufs["prob"], bufs["loss"]
+
+    # -------------------------------------------------------------- pieces --
+    def _gemm(self, *args, **kw):
+        with self._prof("gemm"):
+            ops.gemm(*args, **kw)
+
+    def _colsum(self, *args, **kw):
+        with self._prof("colsum"):
+            ops.colsum(*args, **kw)
+
+    def _wgrad(self, L: _Layer, g, inp, fused_opt, lr):
+        if fused_opt:  # W -= lr * g^T inp ; b -= lr * colsum(g)
+            self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.W, alpha=lr,
+                       epilogue=ops.EPI_SGD)
+            self._colsum(g[:, :L.N], sgd_param=L.b, lr=lr,
+                         workspace=self._ws_colsum(g.shape[0], L.N))
+        else:
+            self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.gW)
+            self._colsum(g[:, :L.N], out=L.gb, workspace=self._ws_colsum(g.shape[0], L.N))
+
+    def _bias_and_w_head(self, last: _Layer, hin, dz, fused_opt, lr):
+        w = last.W[0]  # [Kp]
+        Bl = hin.shape[0]
+        if fused_opt:
+            self._colsum(hin[:, :last.Kp], scale=dz, sgd_param=w, lr=lr,
+                         workspace=self._ws_colsum(Bl, last.Kp))
+            self._colsum(dz.view(-1, 1), sgd_param=last.b, lr=lr,
+                         workspace=self._ws_colsum(Bl, 1))
+        else:
+            self._colsum(hin[:, :last.Kp], scale=dz, out=last.gW[0],
+                         workspace=self._ws_colsum(Bl, last.Kp))
+            self._colsum(dz.view(-1, 1), out=last.gb, workspace=self._ws_colsum(Bl, 1))
+
+    def _ws_tbe(self, n: int) -> torch.Tensor:
+        need = ops.tbe_backward_workspace_size(n, self.total_rows)
+        if self._tbe_ws is None or self._tbe_ws.numel() < need:
+            self._tbe_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        return self._tbe_ws
+
+    def _ws_colsum(self, M: int, N: int) -> torch.Tensor:
+        need = int(ops._lib.query("dlrm_colsum_workspace_size", M, max(N, 1024)))
+        if self._colsum_ws is None or self._colsum_ws.numel() < need:
+            self._colsum_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        return self._colsum_ws
+
+    def _ws_head(self, M: int) -> torch.Tensor:
+        need = int(ops._lib.query("dlrm_head_workspace_size", M))
+        if self._head_ws is None or self._head_ws.numel() < need:
+            self._head_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        return self._head_ws
+
+    # ------------------------------------------------------ communication --
+    def _split_sizes(self, Bl: int):
+        D = self.D
+        send = [Bl * self.T_local * D] * self.world
+        recv = [Bl * self.tables_per_rank[r] * D for r in range(self.world)]
+        return send, recv
+
+    def _alltoall_fwd(self, bufs, Bl):
+        """All2All_Req.forward (extend_distributed.py:405-444): [B, T_r*D] -> W chunks of
+        [B/W, T_s*D] in rank order."""
+        send, recv = self._split_sizes(Bl)
+        return _a2a(bufs["recv"], bufs["E"].view(-1), recv, send, self.pg)
+
+    def _alltoall_bwd(self, bufs, Bl):
+        """All2All_Wait.backward (extend_distributed.py:489-508): reverse exchange."""
+        send, recv = self._split_sizes(Bl)
+        return _a2a(bufs["dE"].view(-1), bufs["drecv"], send, recv, self.pg)
+
+    def _allreduce_dense(self):
+        """DDP gradient all-reduce (dlrm_s_pytorch.py:1626-1633) on the flat bucket; the
+        1/W average is folded into the update."""
+        return _allreduce(self.grads, self.pg)
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, pg):
+    import torch.distributed as dist
+    if out.is_cuda and dist.get_backend(pg) == "gloo":
+        # host-staged exchange (tests on a single GPU: several ranks, gloo)
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=pg)
+        out.copy_(o)
+        return _Done()
+    return dist.all_to_all_single(out, inp, out_splits, in_splits, group=pg, async_op=True)
+
+
+def _allreduce(t: torch.Tensor, pg):
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(pg) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, group=pg)
+        t.copy_(h)
+        return _Done()
+    return dist.all_reduce(t, group=pg, async_op=True)

@@ -1,0 +1,134 @@
+"""The fused HIP training step vs the reference (golden) and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import fp32_close
+
+pytestmark = pytest.mark.gpu
+dev = "cuda:0"
+
+
+def _trainer(**kw):
+    from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+    return DLRMTrainer, TrainerConfig
+
+
+def _num_int(T, D, itself=False):
+    F = T + 1
+    return D + (F * (F + 1) // 2 if itself else F * (F - 1) // 2)
+
+
+def _compare_state(tr, ref, tol_scale=1.0):
+    for k, e in enumerate(ref.emb_l):
+        ok, msg = fp32_close(tr.table(k).cpu().numpy(), e.weight.detach().numpy(),
+                             atol=1e-5 * tol_scale)
+        assert ok, ("emb", k, msg)
+    i = 0
+    for seq in (ref.bot_l, ref.top_l):
+        for m in seq:
+            if isinstance(m, torch.nn.Linear):
+                W, b = tr.dense_state()[i]
+                ok, msg = fp32_close(W.cpu().numpy(), m.weight.detach().numpy(),
+                                     atol=1e-5 * tol_scale)
+                assert ok, ("W", i, msg)
+                ok, msg = fp32_close(b.cpu().numpy(), m.bias.detach().numpy(),
+                                     atol=1e-5 * tol_scale)
+                assert ok, ("b", i, msg)
+                i += 1
+
+
+def test_c0_three_steps_vs_reference_golden(golden):
+    DLRMTrainer, TrainerConfig = _trainer()
+    g = golden("c0_train.npz")
+    np.random.seed(123)
+    ref = O.OracleDLRM(4, [1000] * 3, [13, 512, 4], [10, 4, 2, 1], loss_function="mse")
+    cfg = TrainerConfig(m_spa=4, ln_emb=[1000] * 3, ln_bot=[13, 512, 4], ln_top=[10, 4, 2, 1],
+                        loss_function="mse", learning_rate=0.01)
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    for s in range(3):
+        lS_i = [g[f"s{s}_lS_i{t}"] for t in range(3)]
+        b = tr.make_batch(g[f"s{s}_X"], g[f"s{s}_lS_o"], lS_i, g[f"s{s}_T"])
+        Z, E = tr.step(b)
+        ok, msg = fp32_close(Z.cpu().numpy(), g[f"s{s}_Z"].ravel())
+        assert ok, (s, msg)
+        ok, msg = fp32_close(E.cpu().numpy(), g[f"s{s}_loss"])
+        assert ok, (s, msg)
+    for k in range(3):
+        ok, msg = fp32_close(tr.table(k).cpu().numpy(), g[f"final_emb{k}"])
+        assert ok, msg
+    names = [f"bot.{i}" for i in (0, 2)] + [f"top.{i}" for i in (0, 2, 4)]
+    for (W, b), nm in zip(tr.dense_state(), names):
+        pre, idx = nm.split(".")
+        ok, msg = fp32_close(W.cpu().numpy(), g[f"final_{pre}.{idx}.weight"])
+        assert ok, (nm, msg)
+        ok, msg = fp32_close(b.cpu().numpy(), g[f"final_{pre}.{idx}.bias"])
+        assert ok, (nm, msg)
+
+
+CASES = {
+    # C3 shape with rows capped (bench/run_and_time.sh:17 widths), bce
+    "c3_small": dict(D=128, rows=[min(r, 2000) for r in O.TERABYTE_ROWS], bot=[13, 512, 256, 128],
+                     top=[1024, 1024, 512, 256, 1], B=256, L=1, loss="bce", lr=0.1),
+    # C1 shape (bench/dlrm_s_benchmark.sh:38-41) with fewer rows, L=100
+    "c1_small": dict(D=64, rows=[20000] * 8, bot=[512, 512, 64], top=[1024, 1024, 1024, 1],
+                     B=128, L=100, loss="mse", lr=0.1),
+    # C2 Kaggle shape (bench/dlrm_s_criteo_kaggle.sh:24), rows capped
+    "c2_small": dict(D=16, rows=[min(r, 5000) for r in O.KAGGLE_ROWS],
+                     bot=[13, 512, 256, 64, 16], top=[512, 256, 1], B=128, L=1, loss="bce",
+                     lr=0.1),
+}
+
+
+def _rand_batch(rng, rows, B, L, m_den, loss):
+    X = np.log1p(rng.rand(B, m_den).astype(np.float32))
+    lS_o = np.array([np.arange(B) * L for _ in rows], dtype=np.int64)
+    lS_i = [rng.randint(0, n, size=B * L).astype(np.int64) for n in rows]
+    T = rng.rand(B, 1).astype(np.float32)
+    if loss == "bce":
+        T = np.round(T)
+    return X, lS_o, lS_i, T
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_step_vs_oracle(name):
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    ln_top = [_num_int(len(rows), D)] + c["top"]
+    np.random.seed(7)
+    ref = O.OracleDLRM(D, rows, c["bot"], ln_top, loss_function=c["loss"])
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"], ln_top=ln_top,
+                        loss_function=c["loss"], learning_rate=c["lr"])
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    rng = np.random.RandomState(3)
+    for s in range(2):
+        X, lS_o, lS_i, T = _rand_batch(rng, rows, c["B"], c["L"], c["bot"][0], c["loss"])
+        Zr, Er = ref.train_step(torch.tensor(X), torch.tensor(lS_o),
+                                [torch.tensor(i) for i in lS_i], torch.tensor(T), c["lr"])
+        Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
+        assert ok, (s, msg)
+        ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
+        assert ok, (s, msg)
+    _compare_state(tr, ref)
+
+
+def test_synthetic_batch_and_determinism():
+    DLRMTrainer, TrainerConfig = _trainer()
+    rows, D = [5000] * 4, 32
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=[13, 64, 32], ln_top=[_num_int(4, D), 64, 1],
+                        loss_function="bce", learning_rate=0.1)
+    outs = []
+    for _ in range(2):
+        tr = DLRMTrainer(cfg, device=dev, seed=5)
+        b = tr.synthetic_batch(512, 3, seed=1)
+        assert b.indices.numel() == 4 * 512 * 3 and int(b.offsets[-1]) == 4 * 512 * 3
+        assert int(b.indices.max()) < 5000 and int(b.indices.min()) >= 0
+        for _ in range(3):
+            Z, E = tr.step(b)
+        outs.append((Z.cpu().clone(), tr.weights.cpu().clone(), tr.params.cpu().clone()))
+    # the whole step is bitwise reproducible (sorted embedding backward, no float atomics)
+    for a, b2 in zip(outs[0], outs[1]):
+        assert torch.equal(a, b2)
