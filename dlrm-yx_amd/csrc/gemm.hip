@@ -17,12 +17,20 @@
 // under 64-cycle MFMAs) and written after them, one barrier per K-tile.  Workgroups
 // are remapped bijectively so that each XCD (private 4 MiB L2) receives a contiguous
 // run of output tiles that share operand panels.
+//
+// DLRM's GEMMs are small for 256 CUs (M = batch <= 2048, N,K <= 1024) and the weight
+// gradients have a long K (= the batch) over a small M x N: the planner splits K
+// until there are >= 2 workgroups per CU; split partials go to a caller workspace and
+// a reduce kernel sums them IN SPLIT ORDER (deterministic) and applies the epilogue.
 #include "common.hpp"
 
 namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 constexpr int BK = 32;
+constexpr int kTargetWG = 512;  // 2 workgroups per CU
+constexpr int kMaxSplit = 32;
+constexpr int kMinSplitK = 128;
 
 struct GemmParams {
   int64_t M, N, K;
@@ -38,6 +46,8 @@ struct GemmParams {
   const float* aux;
   int64_t ldaux;
   int tiles_m, tiles_n;
+  int64_t kchunk;  // K range per split (multiple of BK)
+  float* ws;       // split partials [splits][M][N] (splits > 1 only)
 };
 
 // Stages an (MN x BK) panel of X into LDS rows [BK][MN + PAD].
@@ -118,6 +128,35 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// C = epilogue(v) where v = alpha * acc (already scaled).
+__device__ __forceinline__ void apply_epilogue(const GemmParams& p, int64_t row, int64_t col,
+                                               float v) {
+  float* cp = p.C + row * p.ldc + col;
+  switch (p.epi) {
+    case DLRM_EPI_BIAS:
+      v += p.bias[col];
+      break;
+    case DLRM_EPI_BIAS_RELU:
+      v = fmaxf(v + p.bias[col], 0.f);
+      break;
+    case DLRM_EPI_RELU:
+      v = fmaxf(v, 0.f);
+      break;
+    case DLRM_EPI_DRELU:
+      v = p.aux[row * p.ldaux + col] > 0.f ? v : 0.f;
+      break;
+    case DLRM_EPI_SGD:
+      v = *cp - v;
+      break;
+    case DLRM_EPI_ACCUM:
+      v = *cp + v;
+      break;
+    default:
+      break;
+  }
+  *cp = v;
+}
+
 template <int BM, int BN, bool A_KC, bool B_KC, bool VA, bool VB>
 __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -136,6 +175,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
   const int tn = wg - tm * p.tiles_n;
   const int64_t m0 = (int64_t)tm * BM;
   const int64_t n0 = (int64_t)tn * BN;
+  const int split = blockIdx.y;
+  const int64_t kbeg = (int64_t)split * p.kchunk;
+  const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -155,11 +197,13 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
 
   LA la;
   LB lb;
-  const int64_t nk = (p.K + BK - 1) / BK;
-  la.load(p.A, p.lda, m0, p.M, 0, p.K, tid);
-  lb.load(p.B, p.ldb, n0, p.N, 0, p.K, tid);
-  la.store(As0, tid);
-  lb.store(Bs0, tid);
+  const int64_t nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    la.load(p.A, p.lda, m0, p.M, kbeg, kend, tid);
+    lb.load(p.B, p.ldb, n0, p.N, kbeg, kend, tid);
+    la.store(As0, tid);
+    lb.store(Bs0, tid);
+  }
   __syncthreads();
 
   for (int64_t kt = 0; kt < nk; ++kt) {
@@ -168,8 +212,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
     const float* Bs = odd ? Bs1 : Bs0;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(p.A, p.lda, m0, p.M, (kt + 1) * BK, p.K, tid);
-      lb.load(p.B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, tid);
+      la.load(p.A, p.lda, m0, p.M, kbeg + (kt + 1) * BK, kend, tid);
+      lb.load(p.B, p.ldb, n0, p.N, kbeg + (kt + 1) * BK, kend, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
@@ -193,61 +237,77 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
 
   // Epilogue: accumulator register r of a 32x32 tile holds
   //   row (r&3) + 8*(r>>2) + 4*(lane>>5), column lane&31.
+  const bool partial = gridDim.y > 1;
+  float* wsp = partial ? p.ws + (int64_t)split * p.M * p.N : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int64_t col = n0 + wn0 + j * 32 + l32;
       if (col >= p.N) continue;
-      float bias_v = 0.f;
-      if (p.epi == DLRM_EPI_BIAS || p.epi == DLRM_EPI_BIAS_RELU) bias_v = p.bias[col];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row >= p.M) continue;
-        float v = p.alpha * acc[i][j][r];
-        float* cp = p.C + row * p.ldc + col;
-        switch (p.epi) {
-          case DLRM_EPI_BIAS:
-            v += bias_v;
-            break;
-          case DLRM_EPI_BIAS_RELU:
-            v = fmaxf(v + bias_v, 0.f);
-            break;
-          case DLRM_EPI_DRELU:
-            v = p.aux[row * p.ldaux + col] > 0.f ? v : 0.f;
-            break;
-          case DLRM_EPI_SGD:
-            v = *cp - v;
-            break;
-          case DLRM_EPI_ACCUM:
-            v = *cp + v;
-            break;
-          default:
-            break;
-        }
-        *cp = v;
+        if (partial)
+          wsp[row * p.N + col] = acc[i][j][r];
+        else
+          apply_epilogue(p, row, col, p.alpha * acc[i][j][r]);
       }
     }
   }
 }
 
+// Sum the split partials in split order, scale, apply the epilogue.
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmParams p, int splits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t MN = p.M * p.N;
+  if (i >= MN) return;
+  float s = p.ws[i];
+  for (int k = 1; k < splits; ++k) s += p.ws[(int64_t)k * MN + i];
+  const int64_t row = i / p.N;
+  apply_epilogue(p, row, i - row * p.N, p.alpha * s);
+}
+
+struct Plan {
+  int bm, bn, splits;
+  int64_t kchunk;
+};
+
+Plan plan_gemm(int64_t M, int64_t N, int64_t K) {
+  const int64_t t128 = dlrm::ceil_div(M, 128) * dlrm::ceil_div(N, 128);
+  if (t128 >= kTargetWG) return {128, 128, 1, K};
+  const int64_t t64x128 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 128);
+  if (t64x128 >= kTargetWG) return {64, 128, 1, K};
+  const int64_t t64 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 64);
+  int64_t s = dlrm::ceil_div(kTargetWG, t64);
+  int64_t smax = K / kMinSplitK;
+  if (s > smax) s = smax;
+  if (s > kMaxSplit) s = kMaxSplit;
+  if (s < 1) s = 1;
+  int64_t kchunk = dlrm::ceil_div(dlrm::ceil_div(K, s), BK) * BK;
+  if (kchunk < BK) kchunk = BK;
+  s = dlrm::ceil_div(K, kchunk);
+  if (s < 1) s = 1;
+  return {64, 64, (int)s, kchunk};
+}
+
 template <int BM, int BN>
-int launch_tiles(const GemmParams& p0, bool a_kc, bool b_kc, bool va, bool vb, hipStream_t st) {
-  GemmParams p = p0;
+int launch_tiles(GemmParams p, int splits, bool a_kc, bool b_kc, bool va, bool vb,
+                 hipStream_t st) {
   p.tiles_m = (int)dlrm::ceil_div(p.M, BM);
   p.tiles_n = (int)dlrm::ceil_div(p.N, BN);
-  const dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  const dim3 grid(p.tiles_m * p.tiles_n, splits), block(256);
 #define G(AK, BK_, VA_, VB_) \
   hipLaunchKernelGGL((gemm_f32_mfma_kernel<BM, BN, AK, BK_, VA_, VB_>), grid, block, 0, st, p)
-#define G_V(AK, BK_)      \
-  if (va && vb)           \
+#define G_V(AK, BK_)          \
+  if (va && vb)               \
     G(AK, BK_, true, true);   \
-  else if (va)            \
+  else if (va)                \
     G(AK, BK_, true, false);  \
-  else if (vb)            \
+  else if (vb)                \
     G(AK, BK_, false, true);  \
-  else                    \
+  else                        \
     G(AK, BK_, false, false);
   if (a_kc && b_kc) {
     G_V(true, true)
@@ -261,6 +321,11 @@ int launch_tiles(const GemmParams& p0, bool a_kc, bool b_kc, bool va, bool vb, h
 #undef G_V
 #undef G
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32");
+  if (splits > 1) {
+    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(dlrm::ceil_div(p.M * p.N, 256)), dim3(256),
+                       0, st, p, splits);
+    DLRM_LAUNCH_CHECK("dlrm_gemm_f32 (split-K reduce)");
+  }
   return DLRM_OK;
 }
 
@@ -268,16 +333,22 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 }  // namespace
 
+extern "C" size_t dlrm_gemm_f32_workspace_size(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const Plan pl = plan_gemm(M, N, K);
+  return pl.splits > 1 ? (size_t)pl.splits * M * N * sizeof(float) : 0;
+}
+
 extern "C" int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                              float alpha, const float* A, int64_t lda, const float* B,
                              int64_t ldb, float* C, int64_t ldc, int32_t epilogue,
                              const float* bias, const float* aux, int64_t ld_aux,
-                             dlrm_stream_t stream) {
+                             void* workspace, size_t workspace_bytes, dlrm_stream_t stream) {
   DLRM_ARG(M >= 0 && N >= 0 && K >= 0, "dlrm_gemm_f32: negative size");
   if (M == 0 || N == 0) return DLRM_OK;
   DLRM_ARG(C, "dlrm_gemm_f32: null C");
   DLRM_ARG(K == 0 || (A && B), "dlrm_gemm_f32: null A/B");
-  DLRM_ARG(epilogue >= DLRM_EPI_STORE && epilogue <= DLRM_EPI_ACCUM, "dlrm_gemm_f32: bad epilogue");
+  DLRM_ARG(epilogue >= DLRM_EPI_STORE && epilogue <= DLRM_EPI_RELU, "dlrm_gemm_f32: bad epilogue");
   DLRM_ARG(!(epilogue == DLRM_EPI_BIAS || epilogue == DLRM_EPI_BIAS_RELU) || bias,
            "dlrm_gemm_f32: epilogue needs bias");
   DLRM_ARG(epilogue != DLRM_EPI_DRELU || (aux && ld_aux >= N), "dlrm_gemm_f32: DRELU needs aux");
@@ -302,15 +373,23 @@ extern "C" int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_
   p.bias = bias;
   p.aux = aux;
   p.ldaux = ld_aux;
+  Plan pl = plan_gemm(M, N, K);
+  if (pl.splits > 1) {
+    const size_t need = (size_t)pl.splits * M * N * sizeof(float);
+    if (!workspace || workspace_bytes < need) {  // no workspace: single pass
+      pl.splits = 1;
+      pl.kchunk = K;
+    } else {
+      p.ws = static_cast<float*>(workspace);
+    }
+  }
+  p.kchunk = pl.kchunk > 0 ? pl.kchunk : 1;
   const bool a_kc = !trans_a;
   const bool b_kc = trans_b != 0;
   const bool va = aligned16(A) && (lda % 4 == 0);
   const bool vb = aligned16(B) && (ldb % 4 == 0);
   hipStream_t st = dlrm::as_stream(stream);
-  // Tile choice: the largest tile that still gives >= ~one workgroup per CU.
-  const int64_t t128 = dlrm::ceil_div(M, 128) * dlrm::ceil_div(N, 128);
-  const int64_t t64x128 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 128);
-  if (t128 >= 240) return launch_tiles<128, 128>(p, a_kc, b_kc, va, vb, st);
-  if (t64x128 >= 240) return launch_tiles<64, 128>(p, a_kc, b_kc, va, vb, st);
-  return launch_tiles<64, 64>(p, a_kc, b_kc, va, vb, st);
+  if (pl.bm == 128) return launch_tiles<128, 128>(p, pl.splits, a_kc, b_kc, va, vb, st);
+  if (pl.bn == 128) return launch_tiles<64, 128>(p, pl.splits, a_kc, b_kc, va, vb, st);
+  return launch_tiles<64, 64>(p, pl.splits, a_kc, b_kc, va, vb, st);
 }

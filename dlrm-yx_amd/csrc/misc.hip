@@ -174,12 +174,16 @@ __global__ __launch_bounds__(256) void sigmoid_bwd_kernel(int64_t n, const float
   for (int64_t j = i; j < n; j += stride) dx[j] = dy[j] * (1.f - y[j]) * y[j];
 }
 
-__global__ __launch_bounds__(256) void relu_bwd_kernel(int64_t n, const float* __restrict__ dy,
-                                                       const float* __restrict__ y,
-                                                       float* __restrict__ dx) {
+__global__ __launch_bounds__(256) void relu_bwd_kernel(int64_t M, int64_t K,
+                                                       const float* __restrict__ dy, int64_t lddy,
+                                                       const float* __restrict__ y, int64_t ldy,
+                                                       float* __restrict__ dx, int64_t lddx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t j = i; j < n; j += stride) dx[j] = y[j] > 0.f ? dy[j] : 0.f;
+  for (int64_t j = i; j < M * K; j += stride) {
+    const int64_t m = j / K, k = j - m * K;
+    dx[m * lddx + k] = y[m * ldy + k] > 0.f ? dy[m * lddy + k] : 0.f;
+  }
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -379,13 +383,15 @@ extern "C" int dlrm_sigmoid_backward(int64_t n, const float* dy, const float* y,
   return DLRM_OK;
 }
 
-extern "C" int dlrm_relu_backward(int64_t n, const float* dy, const float* y, float* dx,
+extern "C" int dlrm_relu_backward(int64_t M, int64_t K, const float* dy, int64_t lddy,
+                                  const float* y, int64_t ldy, float* dx, int64_t lddx,
                                   dlrm_stream_t stream) {
-  DLRM_ARG(n >= 0, "dlrm_relu_backward: bad n");
-  if (n == 0) return DLRM_OK;
+  DLRM_ARG(M >= 0 && K >= 0, "dlrm_relu_backward: bad sizes");
+  if (M == 0 || K == 0) return DLRM_OK;
   DLRM_ARG(dy && y && dx, "dlrm_relu_backward: null pointer");
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
-                     dlrm::as_stream(stream), n, dy, y, dx);
+  DLRM_ARG(lddy >= K && ldy >= K && lddx >= K, "dlrm_relu_backward: bad leading dims");
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_stride_blocks(M * K)), dim3(256), 0,
+                     dlrm::as_stream(stream), M, K, dy, lddy, y, ldy, dx, lddx);
   DLRM_LAUNCH_CHECK("dlrm_relu_backward");
   return DLRM_OK;
 }

@@ -12,55 +12,12 @@
 //  * the group loads up to LPB indices of its bag in one coalesced load and broadcasts
 //    them with wave shuffles (ds_bpermute), four row fetches in flight per lane;
 //  * 64-bit row bases (a 54 M x 128 table set is 6.9e9 elements);
-//  * backward: stable LSD radix sort of (global row, lookup) pairs, run-length encode,
-//    then one lane-group per unique row reads the row once, applies its lookups'
-//    gradient in lookup order, and writes it once — bitwise reproducible.
-#include <hipcub/hipcub.hpp>
-
-#include "common.hpp"
+//  * backward (tbe_bwd.hip): stable radix sort of (global row, lookup) pairs, fixed
+//    64-lookup blocks summed per run of equal rows, partials combined in block order;
+//    every weight row read and written once — bitwise reproducible.
+#include "tbe_common.hpp"
 
 namespace {
-
-using dlrm::kWave;
-
-template <int VW>
-struct VecT;
-template <>
-struct VecT<4> {
-  using T = float4;
-};
-template <>
-struct VecT<1> {
-  using T = float;
-};
-
-__device__ __forceinline__ void vzero(float4& a) { a = make_float4(0.f, 0.f, 0.f, 0.f); }
-__device__ __forceinline__ void vzero(float& a) { a = 0.f; }
-__device__ __forceinline__ void vadd(float4& a, const float4& b) {
-  a.x += b.x;
-  a.y += b.y;
-  a.z += b.z;
-  a.w += b.w;
-}
-__device__ __forceinline__ void vadd(float& a, const float& b) { a += b; }
-__device__ __forceinline__ void vfma(float4& a, float w, const float4& b) {
-  a.x = fmaf(w, b.x, a.x);
-  a.y = fmaf(w, b.y, a.y);
-  a.z = fmaf(w, b.z, a.z);
-  a.w = fmaf(w, b.w, a.w);
-}
-__device__ __forceinline__ void vfma(float& a, float w, const float& b) { a = fmaf(w, b, a); }
-__device__ __forceinline__ void vscale(float4& a, float w) {
-  a.x *= w;
-  a.y *= w;
-  a.z *= w;
-  a.w *= w;
-}
-__device__ __forceinline__ void vscale(float& a, float w) { a *= w; }
-__device__ __forceinline__ float vdot(const float4& a) {
-  return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
-}
-__device__ __forceinline__ float vdot(const float& a) { return a * a; }
 
 // ----------------------------------------------------------------- forward --
 template <int LPB, int VW, int MAXV, typename IdxT, typename OffT>
@@ -151,172 +108,6 @@ __global__ __launch_bounds__(256) void tbe_fwd_kernel(
       for (int c = 0; c < MAXV; ++c) {
         const int chunk = gl + c * LPB;
         if (chunk < nchunks) o[chunk] = acc[c];
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------- backward --
-// Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags).
-template <typename IdxT, typename OffT, typename KeyT>
-__global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
-    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
-    int T, int B, int64_t N, KeyT sentinel, KeyT* __restrict__ keys, int32_t* __restrict__ pos,
-    int32_t* __restrict__ bag_of) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
-  const int64_t nb = (int64_t)T * B;
-  KeyT key = sentinel;
-  int32_t bag = -1;
-  if (p >= (int64_t)off[0] && p < (int64_t)off[nb]) {
-    int64_t lo = 0, hi = nb;  // invariant off[lo] <= p < off[hi]
-    while (hi - lo > 1) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)off[mid] <= p)
-        lo = mid;
-      else
-        hi = mid;
-    }
-    const int t = (int)(lo / B);
-    const int64_t r = (int64_t)idx[p];
-    const int64_t nrows = row_base[t + 1] - row_base[t];
-    if (r >= 0 && r < nrows) {
-      key = (KeyT)(row_base[t] + r);
-      bag = (int32_t)lo;
-    }
-  }
-  keys[p] = key;
-  pos[p] = (int32_t)p;
-  bag_of[p] = bag;
-}
-
-enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2 };
-
-template <int LPB, int VW, int MAXV, typename KeyT, int MODE>
-__global__ __launch_bounds__(256) void tbe_bwd_update_kernel(
-    float* __restrict__ W, float* __restrict__ mom, int64_t D, int B,
-    const KeyT* __restrict__ uniq, const int32_t* __restrict__ counts,
-    const int32_t* __restrict__ starts, const int32_t* __restrict__ num_runs,
-    const int32_t* __restrict__ pos_sorted, const int32_t* __restrict__ bag_of,
-    const float* __restrict__ psw, const float* __restrict__ gout, int64_t gbs, float lr,
-    float eps, KeyT sentinel) {
-  using V = typename VecT<VW>::T;
-  constexpr int GPW = kWave / LPB;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane / LPB;
-  const int gl = lane - g * LPB;
-  const int nchunks = (int)(D / VW);
-  const int64_t nruns = (int64_t)(*num_runs);
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
-
-  for (int64_t run0 = wave_id * GPW; run0 < nruns; run0 += nwaves * GPW) {
-    const int64_t run = run0 + g;
-    if (run >= nruns) continue;
-    const KeyT row = uniq[run];
-    if (row == sentinel) continue;
-    const int64_t s0 = starts[run];
-    const int cnt = counts[run];
-    float* wrow = W + (int64_t)row * D;
-
-    V acc[MAXV];  // SGD: the weights being updated; others: gradient sum
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int chunk = gl + c * LPB;
-      if (MODE == MODE_SGD && chunk < nchunks)
-        acc[c] = reinterpret_cast<const V*>(wrow)[chunk];
-      else
-        vzero(acc[c]);
-    }
-    for (int i = 0; i < cnt; i += 4) {
-      int32_t bags[4];
-      float ws[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        bags[u] = -1;
-        ws[u] = 1.f;
-        if (i + u < cnt) {
-          const int32_t p = pos_sorted[s0 + i + u];
-          bags[u] = bag_of[p];
-          if (psw) ws[u] = psw[p];
-        }
-      }
-      V gv[4][MAXV];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int t = bags[u] >= 0 ? bags[u] / B : 0;
-        const int b = bags[u] >= 0 ? bags[u] - t * B : 0;
-        const V* grow = reinterpret_cast<const V*>(gout + (int64_t)b * gbs + (int64_t)t * D);
-#pragma unroll
-        for (int c = 0; c < MAXV; ++c) {
-          const int chunk = gl + c * LPB;
-          if (bags[u] >= 0 && chunk < nchunks) {
-            gv[u][c] = grow[chunk];
-            if (psw) vscale(gv[u][c], ws[u]);
-          } else {
-            vzero(gv[u][c]);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (i + u < cnt) {
-#pragma unroll
-          for (int c = 0; c < MAXV; ++c) {
-            if (MODE == MODE_SGD)
-              vfma(acc[c], -lr, gv[u][c]);
-            else
-              vadd(acc[c], gv[u][c]);
-          }
-        }
-      }
-    }
-
-    if (MODE == MODE_SGD) {
-#pragma unroll
-      for (int c = 0; c < MAXV; ++c) {
-        const int chunk = gl + c * LPB;
-        if (chunk < nchunks) reinterpret_cast<V*>(wrow)[chunk] = acc[c];
-      }
-    } else if (MODE == MODE_DENSE) {
-#pragma unroll
-      for (int c = 0; c < MAXV; ++c) {
-        const int chunk = gl + c * LPB;
-        if (chunk < nchunks) {
-          V cur = reinterpret_cast<const V*>(wrow)[chunk];
-          vadd(cur, acc[c]);
-          reinterpret_cast<V*>(wrow)[chunk] = cur;
-        }
-      }
-    } else {  // row-wise Adagrad on the coalesced gradient
-      float sq = 0.f;
-#pragma unroll
-      for (int c = 0; c < MAXV; ++c) {
-        const int chunk = gl + c * LPB;
-        if (chunk < nchunks) sq += vdot(acc[c]);
-      }
-#pragma unroll
-      for (int m = LPB / 2; m >= 1; m >>= 1) sq += __shfl_xor(sq, m, kWave);
-      const float mnew = mom[row] + sq / (float)D;
-      if (gl == 0) mom[row] = mnew;
-      const float denom = sqrtf(mnew) + eps;
-#pragma unroll
-      for (int c = 0; c < MAXV; ++c) {
-        const int chunk = gl + c * LPB;
-        if (chunk < nchunks) {
-          V cur = reinterpret_cast<const V*>(wrow)[chunk];
-          V upd = acc[c];
-          if constexpr (VW == 4) {
-            upd.x /= denom;
-            upd.y /= denom;
-            upd.z /= denom;
-            upd.w /= denom;
-          } else {
-            upd /= denom;
-          }
-          vfma(cur, -lr, upd);
-          reinterpret_cast<V*>(wrow)[chunk] = cur;
-        }
       }
     }
   }
@@ -482,166 +273,6 @@ int launch_fwd(const float* W, int64_t D, const int64_t* row_base, int T, int B,
   return DLRM_OK;
 }
 
-inline int bit_width_u64(uint64_t v) {
-  int b = 0;
-  while (v) {
-    ++b;
-    v >>= 1;
-  }
-  return b < 1 ? 1 : b;
-}
-
-template <typename KeyT>
-struct BwdWs {
-  KeyT* keys_in;
-  KeyT* keys_out;
-  int32_t* pos_in;
-  int32_t* pos_out;
-  int32_t* bag_of;
-  KeyT* uniq;
-  int32_t* counts;
-  int32_t* starts;
-  int32_t* num_runs;
-  void* temp;
-  size_t temp_bytes;
-  size_t total;
-};
-
-template <typename KeyT>
-BwdWs<KeyT> carve_bwd_ws(void* base, int64_t N, int end_bit) {
-  BwdWs<KeyT> w{};
-  WsCarver c(base);
-  w.keys_in = c.take<KeyT>(N);
-  w.keys_out = c.take<KeyT>(N);
-  w.pos_in = c.take<int32_t>(N);
-  w.pos_out = c.take<int32_t>(N);
-  w.bag_of = c.take<int32_t>(N);
-  w.uniq = c.take<KeyT>(N);
-  w.counts = c.take<int32_t>(N);
-  w.starts = c.take<int32_t>(N);
-  w.num_runs = c.take<int32_t>(1);
-  size_t s1 = 0, s2 = 0, s3 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s1, (KeyT*)nullptr, (KeyT*)nullptr,
-                                     (int32_t*)nullptr, (int32_t*)nullptr, (int)N, 0, end_bit);
-  (void)hipcub::DeviceRunLengthEncode::Encode(nullptr, s2, (KeyT*)nullptr, (KeyT*)nullptr,
-                                        (int32_t*)nullptr, (int32_t*)nullptr, (int)N);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s3, (int32_t*)nullptr, (int32_t*)nullptr, (int)N);
-  size_t s = s1 > s2 ? s1 : s2;
-  s = s > s3 ? s : s3;
-  w.temp_bytes = s + 256;
-  w.temp = c.take<char>(w.temp_bytes);
-  w.total = c.used + 256;
-  return w;
-}
-
-template <typename KeyT, typename IdxT, typename OffT>
-int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
-               const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
-               const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
-               hipStream_t st, const char* name) {
-  if (N == 0) return DLRM_OK;
-  const KeyT sentinel = (KeyT)total_rows;
-  const int end_bit = bit_width_u64((uint64_t)total_rows);
-  BwdWs<KeyT> w = carve_bwd_ws<KeyT>(ws, N, end_bit);
-  DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
-               name, ws_bytes, w.total);
-  const int64_t kblocks = dlrm::ceil_div(N, 256);
-  hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(kblocks), dim3(256), 0, st,
-                     static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base, T,
-                     B, N, sentinel, w.keys_in, w.pos_in, w.bag_of);
-  DLRM_LAUNCH_CHECK(name);
-  size_t tb = w.temp_bytes;
-  DLRM_HIP_CALL(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in,
-                                                   w.pos_out, (int)N, 0, end_bit, st),
-                name);
-  DLRM_HIP_CALL(hipMemsetAsync(w.counts, 0, sizeof(int32_t) * N, st), name);
-  tb = w.temp_bytes;
-  DLRM_HIP_CALL(hipcub::DeviceRunLengthEncode::Encode(w.temp, tb, w.keys_out, w.uniq, w.counts,
-                                                      w.num_runs, (int)N, st),
-                name);
-  tb = w.temp_bytes;
-  DLRM_HIP_CALL(hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.counts, w.starts, (int)N, st),
-                name);
-
-  const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
-                    ((reinterpret_cast<uintptr_t>(gout) & 15) == 0) && (gbs % 4 == 0);
-  const int64_t nchunks = vec4 ? D / 4 : D;
-  int lpb = 1;
-  while (lpb < nchunks && lpb < 64) lpb <<= 1;
-  const int64_t maxv = dlrm::ceil_div(nchunks, lpb);
-  DLRM_REQUIRE(maxv <= 8, DLRM_ERR_UNSUPPORTED, "%s: D=%lld too large", name, (long long)D);
-  const int gpw = 64 / lpb;
-  int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(N, gpw), 4);
-  if (blocks > 8192) blocks = 8192;
-  if (blocks < 1) blocks = 1;
-#define UPD(LPB, VW, MV, MODE)                                                              \
-  hipLaunchKernelGGL((tbe_bwd_update_kernel<LPB, VW, MV, KeyT, MODE>), dim3(blocks),        \
-                     dim3(256), 0, st, W, mom, D, B, w.uniq, w.counts, w.starts, w.num_runs, \
-                     w.pos_out, w.bag_of, psw, gout, gbs, lr, eps, sentinel)
-#define UPD_LPB(VW, MODE)                        \
-  switch (lpb) {                                 \
-    case 1: UPD(1, VW, 1, MODE); break;          \
-    case 2: UPD(2, VW, 1, MODE); break;          \
-    case 4: UPD(4, VW, 1, MODE); break;          \
-    case 8: UPD(8, VW, 1, MODE); break;          \
-    case 16: UPD(16, VW, 1, MODE); break;        \
-    case 32: UPD(32, VW, 1, MODE); break;        \
-    default:                                     \
-      if (maxv == 1) UPD(64, VW, 1, MODE);       \
-      else if (maxv == 2) UPD(64, VW, 2, MODE);  \
-      else if (maxv <= 4) UPD(64, VW, 4, MODE);  \
-      else UPD(64, VW, 8, MODE);                 \
-  }
-#define UPD_MODE(VW)                                 \
-  if (mode == MODE_SGD) {                            \
-    UPD_LPB(VW, MODE_SGD)                            \
-  } else if (mode == MODE_ADAGRAD) {                 \
-    UPD_LPB(VW, MODE_ADAGRAD)                        \
-  } else {                                           \
-    UPD_LPB(VW, MODE_DENSE)                          \
-  }
-  if (vec4) {
-    UPD_MODE(4)
-  } else {
-    UPD_MODE(1)
-  }
-#undef UPD_MODE
-#undef UPD_LPB
-#undef UPD
-  DLRM_LAUNCH_CHECK(name);
-  return DLRM_OK;
-}
-
-int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T,
-                 int B, const void* idx, int ib, const void* off, int ob, int64_t N,
-                 int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
-                 float eps, void* ws, size_t ws_bytes, dlrm_stream_t stream, const char* name) {
-  DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
-  DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
-  DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
-  DLRM_ARG(ob == 32 || ob == 64, "%s: offset_bits must be 32 or 64", name);
-  DLRM_REQUIRE(N < (int64_t)INT32_MAX && (int64_t)T * B < (int64_t)INT32_MAX,
-               DLRM_ERR_UNSUPPORTED, "%s: more than 2^31 lookups/bags per call", name);
-  DLRM_ARG(gbs >= (int64_t)T * D, "%s: grad_batch_stride < T*D", name);
-  hipStream_t st = dlrm::as_stream(stream);
-  const bool k32 = (uint64_t)total_rows < 0xFFFFFFFFull;
-#define BWD(K, I, O)                                                                     \
-  return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
-                             gout, gbs, lr, eps, ws, ws_bytes, st, name)
-  if (k32) {
-    if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
-    if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
-    if (ib == 64 && ob == 32) BWD(uint32_t, int64_t, int32_t);
-    BWD(uint32_t, int64_t, int64_t);
-  } else {
-    if (ib == 32 && ob == 32) BWD(uint64_t, int32_t, int32_t);
-    if (ib == 32 && ob == 64) BWD(uint64_t, int32_t, int64_t);
-    if (ib == 64 && ob == 32) BWD(uint64_t, int64_t, int32_t);
-    BWD(uint64_t, int64_t, int64_t);
-  }
-#undef BWD
-}
-
 }  // namespace
 
 extern "C" int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base,
@@ -669,55 +300,6 @@ extern "C" int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* 
                                         per_sample_weights, out, out_batch_stride, error_flag, st);
   return launch_fwd<int64_t, int64_t>(weights, D, row_base, T, B, indices, offsets,
                                       per_sample_weights, out, out_batch_stride, error_flag, st);
-}
-
-extern "C" size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows) {
-  if (num_lookups <= 0) return 256;
-  const int end_bit = bit_width_u64((uint64_t)(total_rows > 0 ? total_rows : 1));
-  if ((uint64_t)total_rows < 0xFFFFFFFFull)
-    return carve_bwd_ws<uint32_t>(nullptr, num_lookups, end_bit).total;
-  return carve_bwd_ws<uint64_t>(nullptr, num_lookups, end_bit).total;
-}
-
-extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base,
-                                     int32_t T, int32_t B, const void* indices,
-                                     int32_t index_bits, const void* offsets,
-                                     int32_t offset_bits, int64_t num_lookups,
-                                     int64_t total_rows, const float* per_sample_weights,
-                                     const float* grad_out, int64_t grad_batch_stride, float lr,
-                                     void* workspace, size_t workspace_bytes,
-                                     dlrm_stream_t stream) {
-  return bwd_dispatch(MODE_SGD, weights, nullptr, D, row_base, T, B, indices, index_bits,
-                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
-                      grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes, stream,
-                      "dlrm_tbe_backward_sgd");
-}
-
-extern "C" int dlrm_tbe_backward_rowwise_adagrad(
-    float* weights, float* momentum, int64_t D, const int64_t* row_base, int32_t T, int32_t B,
-    const void* indices, int32_t index_bits, const void* offsets, int32_t offset_bits,
-    int64_t num_lookups, int64_t total_rows, const float* per_sample_weights,
-    const float* grad_out, int64_t grad_batch_stride, float lr, float eps, void* workspace,
-    size_t workspace_bytes, dlrm_stream_t stream) {
-  DLRM_ARG(momentum, "dlrm_tbe_backward_rowwise_adagrad: null momentum");
-  return bwd_dispatch(MODE_ADAGRAD, weights, momentum, D, row_base, T, B, indices, index_bits,
-                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
-                      grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes, stream,
-                      "dlrm_tbe_backward_rowwise_adagrad");
-}
-
-extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_base,
-                                       int32_t T, int32_t B, const void* indices,
-                                       int32_t index_bits, const void* offsets,
-                                       int32_t offset_bits, int64_t num_lookups,
-                                       int64_t total_rows, const float* per_sample_weights,
-                                       const float* grad_out, int64_t grad_batch_stride,
-                                       void* workspace, size_t workspace_bytes,
-                                       dlrm_stream_t stream) {
-  return bwd_dispatch(MODE_DENSE, grad_weights, nullptr, D, row_base, T, B, indices, index_bits,
-                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
-                      grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes, stream,
-                      "dlrm_tbe_backward_dense");
 }
 
 extern "C" int dlrm_qr_split_indices(const void* indices, int32_t index_bits, int64_t n,

@@ -1,0 +1,494 @@
+// Table-batched EmbeddingBag backward with the optimizer fused in — deterministic.
+//
+// Replaces the EmbeddingBag sparse backward + torch.optim.SGD sparse add_ of the
+// reference step (dlrm_s_pytorch.py:1923-1934; exact-SGD TBE of create_emb_batched
+// :321-334) and the sparse branch of RWSAdagrad.step (optim/rwsadagrad.py:92-115).
+//
+// Pipeline (all on the caller's stream, no host sync, graph-capturable):
+//  1. keys:    per lookup l, global row row_base[t] + idx[l] (or a sentinel) and its bag;
+//  2. sort:    stable LSD radix sort of (row, l) pairs on ceil(log2 rows) bits (hipCUB);
+//  3. blocks:  the sorted lookups are cut into fixed blocks of 64.  One lane-group per
+//              block walks them in order (row ids / grad-row offsets loaded coalesced and
+//              broadcast by wave shuffles, four gradient rows in flight), summing the
+//              gradient of each run of equal rows.  A run that starts and ends inside
+//              the block is applied at once (one read + one write of the weight row);
+//              a run crossing a block edge leaves its partial sum in slot
+//              2*block + (segment starts at the block edge ? 0 : 1) — unique because a
+//              block holds at most one continuing and one starting multi-block run;
+//  4. combine: the block where a multi-block run starts sums its partials in block
+//              order and applies the update.
+// Skewed rows (the 3- and 4-row Terabyte tables receive ~700 lookups per row per
+// batch) are thus split over many lane-groups instead of serialising one of them, and
+// the summation order is fixed by the sort: bitwise reproducible run to run.
+#include <hipcub/hipcub.hpp>
+
+#include "tbe_common.hpp"
+
+namespace {
+
+constexpr int CH = 64;  // sorted lookups per block
+
+// ---------------------------------------------------------------- backward --
+// Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags).
+template <typename IdxT, typename OffT, typename KeyT>
+__global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
+    int T, int B, int64_t N, KeyT sentinel, KeyT* __restrict__ keys, int32_t* __restrict__ pos,
+    int32_t* __restrict__ bag_of) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= N) return;
+  const int64_t nb = (int64_t)T * B;
+  KeyT key = sentinel;
+  int32_t bag = -1;
+  if (p >= (int64_t)off[0] && p < (int64_t)off[nb]) {
+    int64_t lo = 0, hi = nb;  // invariant off[lo] <= p < off[hi]
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)off[mid] <= p)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const int t = (int)(lo / B);
+    const int64_t r = (int64_t)idx[p];
+    const int64_t nrows = row_base[t + 1] - row_base[t];
+    if (r >= 0 && r < nrows) {
+      key = (KeyT)(row_base[t] + r);
+      bag = (int32_t)lo;
+    }
+  }
+  keys[p] = key;
+  pos[p] = (int32_t)p;
+  bag_of[p] = bag;
+}
+
+enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2 };
+
+// Apply the coalesced gradient g of one row (group-uniform control flow).
+template <int LPB, int VW, int MAXV, int MODE>
+__device__ __forceinline__ void finalize_row(float* __restrict__ W, float* __restrict__ mom,
+                                             int64_t D, int64_t row,
+                                             typename VecT<VW>::T (&g)[MAXV], int gl,
+                                             int nchunks, float lr, float eps) {
+  using V = typename VecT<VW>::T;
+  V* wrow = reinterpret_cast<V*>(W + row * D);
+  if (MODE == MODE_SGD) {
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int chunk = gl + c * LPB;
+      if (chunk < nchunks) {
+        V w = wrow[chunk];
+        vfma(w, -lr, g[c]);
+        wrow[chunk] = w;
+      }
+    }
+  } else if (MODE == MODE_DENSE) {
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int chunk = gl + c * LPB;
+      if (chunk < nchunks) {
+        V w = wrow[chunk];
+        vadd(w, g[c]);
+        wrow[chunk] = w;
+      }
+    }
+  } else {  // RWSAdagrad: momentum += mean(g^2); w -= lr * g / (sqrt(momentum) + eps)
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c)
+      if (gl + c * LPB < nchunks) sq += vdot(g[c]);
+#pragma unroll
+    for (int m = LPB / 2; m >= 1; m >>= 1) sq += __shfl_xor(sq, m, kWave);
+    const float mnew = mom[row] + sq / (float)D;
+    if (gl == 0) mom[row] = mnew;
+    const float denom = sqrtf(mnew) + eps;
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int chunk = gl + c * LPB;
+      if (chunk < nchunks) {
+        V w = wrow[chunk];
+        V u = g[c];
+        if constexpr (VW == 4) {
+          u.x /= denom;
+          u.y /= denom;
+          u.z /= denom;
+          u.w /= denom;
+        } else {
+          u /= denom;
+        }
+        vfma(w, -lr, u);
+        wrow[chunk] = w;
+      }
+    }
+  }
+}
+
+template <int LPB, int VW, int MAXV, typename KeyT, int MODE>
+__global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
+    float* __restrict__ W, float* __restrict__ mom, int64_t D, int B,
+    const KeyT* __restrict__ keys, const int32_t* __restrict__ pos,
+    const int32_t* __restrict__ bag_of, const float* __restrict__ psw,
+    const float* __restrict__ gout, int64_t gbs, int64_t N, float lr, float eps,
+    KeyT sentinel, float* __restrict__ partial) {
+  using V = typename VecT<VW>::T;
+  constexpr int GPW = kWave / LPB;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPB;
+  const int gl = lane - g * LPB;
+  const int nchunks = (int)(D / VW);
+  const int64_t nblocks = (N + CH - 1) / CH;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
+
+  for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {
+    const int64_t k = k0 + g;
+    if (k >= nblocks) continue;
+    const int64_t i0 = k * CH;
+    const int64_t i1 = (i0 + CH < N) ? i0 + CH : N;
+    const bool has_prev = i0 > 0;
+    const bool has_next = i1 < N;
+    const KeyT prev_key = has_prev ? keys[i0 - 1] : sentinel;
+    const KeyT next_key = has_next ? keys[i1] : sentinel;
+
+    V acc[MAXV];
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) vzero(acc[c]);
+    KeyT cur = sentinel;
+    int64_t seg_a = i0;
+    bool have = false;
+
+    auto flush = [&](int64_t b_end) {
+      if (cur == sentinel) return;
+      const bool starts = (seg_a > i0) || !has_prev || (prev_key != cur);
+      const bool ends = (b_end < i1) || !has_next || (next_key != cur);
+      if (starts && ends) {
+        finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)cur, acc, gl, nchunks, lr, eps);
+      } else {
+        V* dst = reinterpret_cast<V*>(partial + (2 * k + (seg_a == i0 ? 0 : 1)) * D);
+#pragma unroll
+        for (int c = 0; c < MAXV; ++c)
+          if (gl + c * LPB < nchunks) dst[gl + c * LPB] = acc[c];
+      }
+    };
+
+    for (int64_t base = i0; base < i1; base += LPB) {
+      const int n = (int)((i1 - base) < LPB ? (i1 - base) : LPB);
+      KeyT my_key = sentinel;
+      int64_t my_off = -1;
+      float my_w = 1.f;
+      if (gl < n) {
+        my_key = keys[base + gl];
+        const int32_t p = pos[base + gl];
+        const int32_t bag = bag_of[p];
+        if (bag >= 0) {
+          const int t = bag / B;
+          const int b = bag - t * B;
+          my_off = (int64_t)b * gbs + (int64_t)t * D;
+        }
+        if (psw) my_w = psw[p];
+      }
+      for (int j = 0; j < n; j += 4) {
+        KeyT ku[4];
+        int64_t ou[4];
+        float wu[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = g * LPB + ((j + u) < LPB ? (j + u) : 0);
+          if constexpr (sizeof(KeyT) == 8)
+            ku[u] = (KeyT)__shfl((long long)my_key, src, kWave);
+          else
+            ku[u] = (KeyT)__shfl((int)my_key, src, kWave);
+          ou[u] = __shfl(my_off, src, kWave);
+          wu[u] = __shfl(my_w, src, kWave);
+          if (j + u >= n) ou[u] = -1;
+        }
+        V gv[4][MAXV];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int c = 0; c < MAXV; ++c) {
+            const int chunk = gl + c * LPB;
+            if (ou[u] >= 0 && chunk < nchunks) {
+              gv[u][c] = reinterpret_cast<const V*>(gout + ou[u])[chunk];
+              if (psw) vscale(gv[u][c], wu[u]);
+            } else {
+              vzero(gv[u][c]);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j + u < n) {
+            if (!have || ku[u] != cur) {
+              if (have) flush(base + j + u);
+              have = true;
+              cur = ku[u];
+              seg_a = base + j + u;
+#pragma unroll
+              for (int c = 0; c < MAXV; ++c) vzero(acc[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < MAXV; ++c) vadd(acc[c], gv[u][c]);
+          }
+        }
+      }
+    }
+    if (have) flush(i1);
+  }
+}
+
+template <int LPB, int VW, int MAXV, typename KeyT, int MODE>
+__global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
+    float* __restrict__ W, float* __restrict__ mom, int64_t D, const KeyT* __restrict__ keys,
+    int64_t N, float lr, float eps, KeyT sentinel, const float* __restrict__ partial) {
+  using V = typename VecT<VW>::T;
+  constexpr int GPW = kWave / LPB;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPB;
+  const int gl = lane - g * LPB;
+  const int nchunks = (int)(D / VW);
+  const int64_t nblocks = (N + CH - 1) / CH;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
+
+  for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {
+    const int64_t k = k0 + g;
+    if (k >= nblocks) continue;
+    const int64_t i0 = k * CH;
+    const int64_t i1 = (i0 + CH < N) ? i0 + CH : N;
+    if (i1 >= N) continue;
+    const KeyT last = keys[i1 - 1];
+    if (last == sentinel || keys[i1] != last) continue;  // run ends inside this block
+    // start of the last segment: first index of the block holding `last` (keys sorted)
+    int64_t a = i1;
+    for (int64_t i = i0 + gl; i < i1; i += LPB)
+      if (keys[i] == last && i < a) a = i;
+#pragma unroll
+    for (int m = LPB / 2; m >= 1; m >>= 1) {
+      const int64_t o = __shfl_xor(a, m, kWave);
+      a = o < a ? o : a;
+    }
+    const bool starts = (a > i0) || (i0 == 0) || (keys[i0 - 1] != last);
+    if (!starts) continue;  // the block where the run starts combines it
+    V acc[MAXV];
+    const V* src = reinterpret_cast<const V*>(partial + (2 * k + (a == i0 ? 0 : 1)) * D);
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      if (gl + c * LPB < nchunks)
+        acc[c] = src[gl + c * LPB];
+      else
+        vzero(acc[c]);
+    }
+    for (int64_t kk = k + 1; kk < nblocks; ++kk) {
+      const V* s2 = reinterpret_cast<const V*>(partial + (2 * kk) * D);
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c)
+        if (gl + c * LPB < nchunks) vadd(acc[c], s2[gl + c * LPB]);
+      const int64_t e = (kk + 1) * CH;
+      if (e >= N || keys[e] != last) break;
+    }
+    finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)last, acc, gl, nchunks, lr, eps);
+  }
+}
+
+inline int bit_width_u64(uint64_t v) {
+  int b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b < 1 ? 1 : b;
+}
+
+template <typename KeyT>
+struct BwdWs {
+  KeyT* keys_in;
+  KeyT* keys_out;
+  int32_t* pos_in;
+  int32_t* pos_out;
+  int32_t* bag_of;
+  float* partial;
+  void* temp;
+  size_t temp_bytes;
+  size_t total;
+};
+
+template <typename KeyT>
+BwdWs<KeyT> carve_bwd_ws(void* base, int64_t N, int64_t D, int end_bit) {
+  BwdWs<KeyT> w{};
+  WsCarver c(base);
+  w.keys_in = c.take<KeyT>(N);
+  w.keys_out = c.take<KeyT>(N);
+  w.pos_in = c.take<int32_t>(N);
+  w.pos_out = c.take<int32_t>(N);
+  w.bag_of = c.take<int32_t>(N);
+  w.partial = c.take<float>((size_t)2 * ((N + CH - 1) / CH) * D);
+  size_t s1 = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s1, (KeyT*)nullptr, (KeyT*)nullptr,
+                                           (int32_t*)nullptr, (int32_t*)nullptr, (int)N, 0,
+                                           end_bit);
+  w.temp_bytes = s1 + 256;
+  w.temp = c.take<char>(w.temp_bytes);
+  w.total = c.used + 256;
+  return w;
+}
+
+template <typename KeyT, typename IdxT, typename OffT>
+int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
+               const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
+               const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
+               hipStream_t st, const char* name) {
+  if (N == 0) return DLRM_OK;
+  const KeyT sentinel = (KeyT)total_rows;
+  const int end_bit = bit_width_u64((uint64_t)total_rows);
+  BwdWs<KeyT> w = carve_bwd_ws<KeyT>(ws, N, D, end_bit);
+  DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
+               name, ws_bytes, w.total);
+  hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(dlrm::ceil_div(N, 256)),
+                     dim3(256), 0, st, static_cast<const IdxT*>(idx),
+                     static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_in,
+                     w.pos_in, w.bag_of);
+  DLRM_LAUNCH_CHECK(name);
+  size_t tb = w.temp_bytes;
+  DLRM_HIP_CALL(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in,
+                                                   w.pos_out, (int)N, 0, end_bit, st),
+                name);
+
+  const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
+                    ((reinterpret_cast<uintptr_t>(gout) & 15) == 0) && (gbs % 4 == 0);
+  const int64_t nchunks = vec4 ? D / 4 : D;
+  int lpb = 1;
+  while (lpb < nchunks && lpb < 64) lpb <<= 1;
+  const int64_t maxv = dlrm::ceil_div(nchunks, lpb);
+  DLRM_REQUIRE(maxv <= 8, DLRM_ERR_UNSUPPORTED, "%s: D=%lld too large", name, (long long)D);
+  const int gpw = 64 / lpb;
+  const int64_t nblocks = dlrm::ceil_div(N, CH);
+  int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(nblocks, gpw), 4);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+#define LAUNCH2(LPB, VW, MV, MODE)                                                             \
+  do {                                                                                         \
+    hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE>), dim3(blocks),          \
+                       dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw,   \
+                       gout, gbs, N, lr, eps, sentinel, w.partial);                            \
+    hipLaunchKernelGGL((tbe_bwd_combine_kernel<LPB, VW, MV, KeyT, MODE>), dim3(blocks),        \
+                       dim3(256), 0, st, W, mom, D, w.keys_out, N, lr, eps, sentinel,          \
+                       w.partial);                                                             \
+  } while (0)
+#define BY_LPB(VW, MODE)                             \
+  switch (lpb) {                                     \
+    case 1: LAUNCH2(1, VW, 1, MODE); break;          \
+    case 2: LAUNCH2(2, VW, 1, MODE); break;          \
+    case 4: LAUNCH2(4, VW, 1, MODE); break;          \
+    case 8: LAUNCH2(8, VW, 1, MODE); break;          \
+    case 16: LAUNCH2(16, VW, 1, MODE); break;        \
+    case 32: LAUNCH2(32, VW, 1, MODE); break;        \
+    default:                                         \
+      if (maxv == 1) LAUNCH2(64, VW, 1, MODE);       \
+      else if (maxv == 2) LAUNCH2(64, VW, 2, MODE);  \
+      else if (maxv <= 4) LAUNCH2(64, VW, 4, MODE);  \
+      else LAUNCH2(64, VW, 8, MODE);                 \
+  }
+#define BY_MODE(VW)                    \
+  if (mode == MODE_SGD) {              \
+    BY_LPB(VW, MODE_SGD)               \
+  } else if (mode == MODE_ADAGRAD) {   \
+    BY_LPB(VW, MODE_ADAGRAD)           \
+  } else {                             \
+    BY_LPB(VW, MODE_DENSE)             \
+  }
+  if (vec4) {
+    BY_MODE(4)
+  } else {
+    BY_MODE(1)
+  }
+#undef BY_MODE
+#undef BY_LPB
+#undef LAUNCH2
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T,
+                 int B, const void* idx, int ib, const void* off, int ob, int64_t N,
+                 int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
+                 float eps, void* ws, size_t ws_bytes, dlrm_stream_t stream, const char* name) {
+  DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
+  DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
+  DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
+  DLRM_ARG(ob == 32 || ob == 64, "%s: offset_bits must be 32 or 64", name);
+  DLRM_REQUIRE(N < (int64_t)INT32_MAX && (int64_t)T * B < (int64_t)INT32_MAX,
+               DLRM_ERR_UNSUPPORTED, "%s: more than 2^31 lookups/bags per call", name);
+  DLRM_ARG(gbs >= (int64_t)T * D, "%s: grad_batch_stride < T*D", name);
+  DLRM_ARG(ws || N == 0, "%s: null workspace", name);
+  hipStream_t st = dlrm::as_stream(stream);
+  const bool k32 = (uint64_t)total_rows < 0xFFFFFFFFull;
+#define BWD(K, I, O)                                                                     \
+  return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
+                             gout, gbs, lr, eps, ws, ws_bytes, st, name)
+  if (k32) {
+    if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
+    if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
+    if (ib == 64 && ob == 32) BWD(uint32_t, int64_t, int32_t);
+    BWD(uint32_t, int64_t, int64_t);
+  } else {
+    if (ib == 32 && ob == 32) BWD(uint64_t, int32_t, int32_t);
+    if (ib == 32 && ob == 64) BWD(uint64_t, int32_t, int64_t);
+    if (ib == 64 && ob == 32) BWD(uint64_t, int64_t, int32_t);
+    BWD(uint64_t, int64_t, int64_t);
+  }
+#undef BWD
+}
+
+}  // namespace
+
+extern "C" size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows,
+                                                   int64_t D) {
+  if (num_lookups <= 0) return 256;
+  if (D < 1) D = 1;
+  const int end_bit = bit_width_u64((uint64_t)(total_rows > 0 ? total_rows : 1));
+  if ((uint64_t)total_rows < 0xFFFFFFFFull)
+    return carve_bwd_ws<uint32_t>(nullptr, num_lookups, D, end_bit).total;
+  return carve_bwd_ws<uint64_t>(nullptr, num_lookups, D, end_bit).total;
+}
+
+extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base,
+                                     int32_t T, int32_t B, const void* indices,
+                                     int32_t index_bits, const void* offsets,
+                                     int32_t offset_bits, int64_t num_lookups,
+                                     int64_t total_rows, const float* per_sample_weights,
+                                     const float* grad_out, int64_t grad_batch_stride, float lr,
+                                     void* workspace, size_t workspace_bytes,
+                                     dlrm_stream_t stream) {
+  return bwd_dispatch(MODE_SGD, weights, nullptr, D, row_base, T, B, indices, index_bits,
+                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
+                      grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes, stream,
+                      "dlrm_tbe_backward_sgd");
+}
+
+extern "C" int dlrm_tbe_backward_rowwise_adagrad(
+    float* weights, float* momentum, int64_t D, const int64_t* row_base, int32_t T, int32_t B,
+    const void* indices, int32_t index_bits, const void* offsets, int32_t offset_bits,
+    int64_t num_lookups, int64_t total_rows, const float* per_sample_weights,
+    const float* grad_out, int64_t grad_batch_stride, float lr, float eps, void* workspace,
+    size_t workspace_bytes, dlrm_stream_t stream) {
+  DLRM_ARG(momentum, "dlrm_tbe_backward_rowwise_adagrad: null momentum");
+  return bwd_dispatch(MODE_ADAGRAD, weights, momentum, D, row_base, T, B, indices, index_bits,
+                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
+                      grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes, stream,
+                      "dlrm_tbe_backward_rowwise_adagrad");
+}
+
+extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_base,
+                                       int32_t T, int32_t B, const void* indices,
+                                       int32_t index_bits, const void* offsets,
+                                       int32_t offset_bits, int64_t num_lookups,
+                                       int64_t total_rows, const float* per_sample_weights,
+                                       const float* grad_out, int64_t grad_batch_stride,
+                                       void* workspace, size_t workspace_bytes,
+                                       dlrm_stream_t stream) {
+  return bwd_dispatch(MODE_DENSE, grad_weights, nullptr, D, row_base, T, B, indices, index_bits,
+                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
+                      grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes, stream,
+                      "dlrm_tbe_backward_dense");
+}

@@ -33,7 +33,7 @@ SIGNATURES = {
     "dlrm_last_error": (ctypes.c_char_p, []),
     "dlrm_tbe_forward": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32, P, P,
                                    c_int64, P, P]),
-    "dlrm_tbe_backward_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "dlrm_tbe_backward_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
     "dlrm_tbe_backward_sgd": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32,
                                         c_int64, c_int64, P, P, c_int64, c_float, P, c_size_t,
                                         P]),
@@ -54,8 +54,9 @@ SIGNATURES = {
                                              c_int64, P, P, P]),
     "dlrm_interact_cat_forward": (c_int32, [c_int32, c_int32, c_int32, P, P, P, c_int64, P]),
     "dlrm_interact_cat_backward": (c_int32, [c_int32, c_int32, c_int32, P, c_int64, P, P, P]),
+    "dlrm_gemm_f32_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
     "dlrm_gemm_f32": (c_int32, [c_int32, c_int32, c_int64, c_int64, c_int64, c_float, P, c_int64,
-                                P, c_int64, P, c_int64, c_int32, P, P, c_int64, P]),
+                                P, c_int64, P, c_int64, c_int32, P, P, c_int64, P, c_size_t, P]),
     "dlrm_colsum_workspace_size": (c_size_t, [c_int64, c_int64]),
     "dlrm_colsum_f32": (c_int32, [c_int64, c_int64, P, c_int64, P, c_float, P, c_int32, P,
                                   c_float, P, c_size_t, P]),
@@ -68,7 +69,7 @@ SIGNATURES = {
     "dlrm_scale_f32": (c_int32, [P, c_int64, c_float, P]),
     "dlrm_sigmoid_forward": (c_int32, [c_int64, P, P, P]),
     "dlrm_sigmoid_backward": (c_int32, [c_int64, P, P, P, P]),
-    "dlrm_relu_backward": (c_int32, [c_int64, P, P, P, P]),
+    "dlrm_relu_backward": (c_int32, [c_int64, c_int64, P, c_int64, P, c_int64, P, c_int64, P]),
     "dlrm_uniform_fill": (c_int32, [P, c_int64, c_float, c_float, c_uint64, P]),
     "dlrm_uniform_int_fill": (c_int32, [P, c_int32, c_int64, c_int64, c_uint64, P]),
     "dlrm_csr_from_tables": (c_int32, [c_int32, c_int32, P, P, P, c_int32, P]),

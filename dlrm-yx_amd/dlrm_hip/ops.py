@@ -13,7 +13,7 @@ import torch
 
 from . import _lib
 
-EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_DRELU, EPI_SGD, EPI_ACCUM = range(6)
+EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_DRELU, EPI_SGD, EPI_ACCUM, EPI_RELU = range(7)
 LOSS_MSE, LOSS_BCE = 0, 1
 QR_OPS = {"mult": 0, "add": 1, "concat": 2}
 
@@ -83,8 +83,8 @@ def tbe_forward(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
     return out
 
 
-def tbe_backward_workspace_size(num_lookups: int, total_rows: int) -> int:
-    return _lib.query("dlrm_tbe_backward_workspace_size", num_lookups, total_rows)
+def tbe_backward_workspace_size(num_lookups: int, total_rows: int, D: int) -> int:
+    return _lib.query("dlrm_tbe_backward_workspace_size", num_lookups, total_rows, D)
 
 
 def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
@@ -101,7 +101,7 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
     total_rows = weights.shape[0]
     if grad_batch_stride is None:
         grad_batch_stride = T * D
-    need = tbe_backward_workspace_size(N, total_rows)
+    need = tbe_backward_workspace_size(N, total_rows, D)
     if workspace is None:
         workspace = _ws("tbe_bwd", need, weights.device)
     args_common = (D, _p(row_base), T, B, _p(indices), _bits(indices), _p(offsets),
@@ -242,10 +242,16 @@ def interact_backward(op: str, x: torch.Tensor, ly, grad_out: torch.Tensor,
 
 
 # ------------------------------------------------------------------ MLP ----
+def gemm_workspace_size(M: int, N: int, K: int) -> int:
+    return _lib.query("dlrm_gemm_f32_workspace_size", M, N, K)
+
+
 def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
          C: Optional[torch.Tensor] = None, alpha: float = 1.0, epilogue: int = EPI_STORE,
-         bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D operands (unit inner stride)."""
+         bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
+         workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D operands (unit inner stride).
+    Split-K uses ``workspace`` (or a cached one) when the planner asks for it."""
     _check_cuda(A, B, C, bias, aux)
     if A.stride(1) != 1 or B.stride(1) != 1:
         raise ValueError("gemm operands need unit inner stride")
@@ -257,9 +263,13 @@ def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool 
         raise ValueError(f"gemm inner dims differ: {K} vs {Kb}")
     if C is None:
         C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    need = gemm_workspace_size(M, N, K)
+    if need and (workspace is None or workspace.numel() < need):
+        workspace = _ws("gemm", need, A.device)
     _lib.call("dlrm_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), _p(A),
               A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0), epilogue, _p(bias), _p(aux),
-              aux.stride(0) if aux is not None else 0, _stream(A.device))
+              aux.stride(0) if aux is not None else 0, _p(workspace) if need else None,
+              workspace.numel() if (need and workspace is not None) else 0, _stream(A.device))
     return C
 
 
@@ -320,11 +330,16 @@ def sigmoid_backward(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
 
 def relu_backward(dy: torch.Tensor, y: torch.Tensor,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    dy = dy.contiguous()
-    if not y.is_contiguous():
-        raise ValueError("relu_backward needs a contiguous activation")
-    dx = torch.empty_like(dy) if out is None else out
-    _lib.call("dlrm_relu_backward", dy.numel(), _p(dy), _p(y), _p(dx), _stream(dy.device))
+    """dx = dy * (y > 0) for 2-D row-strided operands (unit inner stride)."""
+    if dy.dim() == 1:
+        dy, y = dy.view(1, -1), y.reshape(1, -1)
+        out = None if out is None else out.view(1, -1)
+    if dy.stride(1) != 1 or y.stride(1) != 1:
+        raise ValueError("relu_backward needs unit inner strides")
+    M, K = dy.shape
+    dx = torch.empty((M, K), dtype=torch.float32, device=dy.device) if out is None else out
+    _lib.call("dlrm_relu_backward", M, K, _p(dy), dy.stride(0), _p(y), y.stride(0), _p(dx),
+              dx.stride(0), _stream(dy.device))
     return dx
 
 

@@ -134,7 +134,10 @@ class DLRMTrainer:
             raise ValueError(f"ln_top[0]={ln_top[0]} != number of interactions {self.num_int}")
         specs = [(ln_bot[i + 1], ln_bot[i]) for i in range(len(ln_bot) - 1)] + \
                 [(ln_top[i + 1], ln_top[i]) for i in range(len(ln_top) - 1)]
-        sizes = [n * _pad4(k) + n for n, k in specs]
+        # Bias folding: layer l stores [W | b | 0-pad] as one [N, Kp] block with
+        # Kp = pad4(K + 1); every layer input carries a constant-1 column at index K, so
+        # the forward GEMM adds the bias as its last k-term and the wgrad GEMM yields db.
+        sizes = [n * _pad4(k + 1) for n, k in specs]
         self.n_params = int(sum(sizes))
         self.params = torch.zeros(self.n_params, dtype=torch.float32, device=self.dev)
         self.grads = torch.zeros_like(self.params) if (world_size > 1 or
@@ -143,14 +146,13 @@ class DLRMTrainer:
         self.layers: List[_Layer] = []
         o = 0
         for n, k in specs:
-            kp = _pad4(k)
-            L = _Layer(N=n, K=k, Kp=kp, Np=_pad4(n),
-                       W=self.params[o:o + n * kp].view(n, kp),
-                       b=self.params[o + n * kp:o + n * kp + n])
+            kp = _pad4(k + 1)
+            W = self.params[o:o + n * kp].view(n, kp)
+            L = _Layer(N=n, K=k, Kp=kp, Np=_pad4(n + 1), W=W, b=W[:, k])
             if self.grads is not None:
                 L.gW = self.grads[o:o + n * kp].view(n, kp)
-                L.gb = self.grads[o + n * kp:o + n * kp + n]
-            o += n * kp + n
+                L.gb = L.gW[:, k]
+            o += n * kp
             self.layers.append(L)
         self.n_bot = len(ln_bot) - 1
         self.bot = self.layers[:self.n_bot]
@@ -236,6 +238,7 @@ class DLRMTrainer:
         L0 = self.bot[0]
         Xp = torch.zeros((Bl, L0.Kp), dtype=torch.float32, device=self.dev)
         Xp[:, :L0.K] = torch.as_tensor(X)[sl].to(self.dev)
+        Xp[:, L0.K] = 1.0  # bias column
         offs, idxs, start = [], [], 0
         for t in self.local_tables:
             o = torch.as_tensor(lS_o[t]).to(torch.int64)
@@ -258,6 +261,7 @@ class DLRMTrainer:
         g.manual_seed(seed * 7919 + self.rank)
         Xp = torch.zeros((Bl, L0.Kp), dtype=torch.float32, device=self.dev)
         Xp[:, :L0.K] = torch.log1p(torch.rand((Bl, L0.K), generator=g, device=self.dev))
+        Xp[:, L0.K] = 1.0  # bias column
         Tl = self.T_local
         indices = torch.empty(Tl * B * L, dtype=torch.int32, device=self.dev)
         for j, t in enumerate(self.local_tables):
@@ -277,11 +281,21 @@ class DLRMTrainer:
         dev, D = self.dev, self.D
         f32 = dict(dtype=torch.float32, device=dev)
         bufs = {}
+        # activations carry the constant-1 bias column right after their N real columns
         bufs["bot_act"] = [torch.zeros((Bl, L.Np), **f32) for L in self.bot]
-        self.ldR = _pad4(self.num_int)
+        self.ldR = _pad4(self.num_int + 1)
         bufs["R"] = torch.zeros((Bl, self.ldR), **f32)
         bufs["top_act"] = [torch.zeros((Bl, L.Np), **f32) for L in self.top[:-1]]
+        for L, a in zip(self.bot + self.top[:-1], bufs["bot_act"] + bufs["top_act"]):
+            a[:, L.N] = 1.0
+        bufs["R"][:, self.num_int] = 1.0
         wmax = max([L.Kp for L in self.layers] + [self.ldR])
+        # one split-K workspace sized for the largest GEMM of the step
+        shapes = []
+        for L in self.layers[:-1]:
+            shapes += [(Bl, L.N, L.Kp), (Bl, L.Kp, L.N), (L.N, L.Kp, Bl)]
+        gws = max([ops.gemm_workspace_size(*s) for s in shapes] + [256])
+        self._gemm_ws = torch.empty(gws, dtype=torch.uint8, device=dev)
         bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(2)]
         bufs["dx"] = torch.zeros((Bl, D), **f32)
         bufs["gx"] = torch.zeros((Bl, D), **f32)
@@ -338,7 +352,7 @@ class DLRMTrainer:
         # ---------------- forward: bottom MLP (overlaps the exchange)
         h = batch.X
         for L, out in zip(self.bot, bufs["bot_act"]):
-            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_BIAS_RELU, bias=L.b)
+            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)
             h = out
         if work is not None:
             work.wait()
@@ -348,12 +362,13 @@ class DLRMTrainer:
                                  cfg.arch_interaction_itself, out=bufs["R"])
         h = bufs["R"]
         for L, out in zip(self.top[:-1], bufs["top_act"]):
-            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_BIAS_RELU, bias=L.b)
+            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)
             h = out
         last = self.top[-1]
         hin = h
         with prof("head"):
-            ops.head_forward_backward(hin, last.W[0, :last.K], last.b, batch.target,
+            # bias folded: [hin | 1] . [w | b]
+            ops.head_forward_backward(hin, last.W[0, :last.Kp], None, batch.target,
                                       cfg.loss_function, cfg.loss_threshold, 1.0,
                                       prob=bufs["prob"], dz=bufs["dz"], loss_out=bufs["loss"],
                                       workspace=self._ws_head(Bl))
@@ -388,7 +403,7 @@ class DLRMTrainer:
         if self.world > 1:
             work = self._alltoall_bwd(bufs, Bl)
         # ---------------- backward: bottom MLP (overlaps the reverse exchange)
-        xin = bufs["bot_act"][-1]
+        xin = bufs["bot_act"][-1][:, :D]
         with prof("relu_bwd"):
             g = ops.relu_backward(bufs["dx"], xin, out=bufs["gx"])
         for li in range(self.n_bot - 1, -1, -1):
@@ -432,37 +447,32 @@ class DLRMTrainer:
     # -------------------------------------------------------------- pieces --
     def _gemm(self, *args, **kw):
         with self._prof("gemm"):
-            ops.gemm(*args, **kw)
+            ops.gemm(*args, workspace=self._gemm_ws, **kw)
 
     def _colsum(self, *args, **kw):
         with self._prof("colsum"):
             ops.colsum(*args, **kw)
 
     def _wgrad(self, L: _Layer, g, inp, fused_opt, lr):
-        if fused_opt:  # W -= lr * g^T inp ; b -= lr * colsum(g)
+        """[dW | db] = g^T [inp | 1] in one GEMM (bias folded); fused SGD on one GPU."""
+        if fused_opt:
             self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.W, alpha=lr,
                        epilogue=ops.EPI_SGD)
-            self._colsum(g[:, :L.N], sgd_param=L.b, lr=lr,
-                         workspace=self._ws_colsum(g.shape[0], L.N))
         else:
             self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.gW)
-            self._colsum(g[:, :L.N], out=L.gb, workspace=self._ws_colsum(g.shape[0], L.N))
 
     def _bias_and_w_head(self, last: _Layer, hin, dz, fused_opt, lr):
-        w = last.W[0]  # [Kp]
+        """Head layer (K -> 1): [dw | db] = sum_m dz[m] [hin[m] | 1] as one column sum."""
         Bl = hin.shape[0]
         if fused_opt:
-            self._colsum(hin[:, :last.Kp], scale=dz, sgd_param=w, lr=lr,
+            self._colsum(hin[:, :last.Kp], scale=dz, sgd_param=last.W[0], lr=lr,
                          workspace=self._ws_colsum(Bl, last.Kp))
-            self._colsum(dz.view(-1, 1), sgd_param=last.b, lr=lr,
-                         workspace=self._ws_colsum(Bl, 1))
         else:
             self._colsum(hin[:, :last.Kp], scale=dz, out=last.gW[0],
                          workspace=self._ws_colsum(Bl, last.Kp))
-            self._colsum(dz.view(-1, 1), out=last.gb, workspace=self._ws_colsum(Bl, 1))
 
     def _ws_tbe(self, n: int) -> torch.Tensor:
-        need = ops.tbe_backward_workspace_size(n, self.total_rows)
+        need = ops.tbe_backward_workspace_size(n, self.total_rows, self.D)
         if self._tbe_ws is None or self._tbe_ws.numel() < need:
             self._tbe_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
         return self._tbe_ws

@@ -71,7 +71,8 @@ enum dlrm_epilogue {
   DLRM_EPI_BIAS_RELU = 2, /* C = max(alpha*acc + bias[n], 0)      (Linear+ReLU) */
   DLRM_EPI_DRELU = 3,     /* C = alpha*acc * (aux[m][n] > 0)      (ReLU bwd)    */
   DLRM_EPI_SGD = 4,       /* C = C - alpha*acc                    (fused SGD)   */
-  DLRM_EPI_ACCUM = 5      /* C = C + alpha*acc                                  */
+  DLRM_EPI_ACCUM = 5,     /* C = C + alpha*acc                                  */
+  DLRM_EPI_RELU = 6       /* C = max(alpha*acc, 0)   (Linear+ReLU, bias folded) */
 };
 
 enum dlrm_loss { DLRM_LOSS_MSE = 0, DLRM_LOSS_BCE = 1 };
@@ -101,14 +102,15 @@ int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base, i
                      int64_t out_batch_stride, int32_t* error_flag, dlrm_stream_t stream);
 
 /* Workspace for the deterministic (sorted, segment-reduced) backward. */
-size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows);
+size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows, int64_t D);
 
 /*
  * Exact-SGD backward fused with the update: for every lookup l of bag (t,b),
  *   W[row_base[t]+indices[l]] -= lr * w_l * grad_out[b*grad_batch_stride + t*D + :]
  * Duplicate rows are combined deterministically: lookups are radix-sorted by
- * global row (stable), and each unique row is read once, updated in lookup order
- * and written once.  num_lookups = length of indices.
+ * global row (stable), the gradient of each unique row is summed in sorted order
+ * (long runs in fixed 64-lookup blocks whose partials are added in block order),
+ * and the row is read once and written once.  num_lookups = length of indices.
  */
 int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, int32_t T,
                           int32_t B, const void* indices, int32_t index_bits,
@@ -204,11 +206,19 @@ int dlrm_interact_cat_backward(int32_t B, int32_t F, int32_t D, const float* gra
  * Linear forward  Y = X W^T + b : trans_a=0, trans_b=1, EPI_BIAS[_RELU]
  * Linear dgrad    dX = dY W     : trans_a=0, trans_b=0, EPI_STORE / EPI_DRELU
  * Linear wgrad    dW = dY^T X   : trans_a=1, trans_b=0, EPI_STORE / EPI_SGD
+ * Bias folding: with a constant-1 column appended to X and the bias stored as the
+ * matching extra column of W, the forward needs no bias epilogue (EPI_RELU) and the
+ * wgrad GEMM produces the bias gradient in that column.
+ * Small-M*N / long-K shapes are split along K into >= 2 workgroups per CU when a
+ * workspace of dlrm_gemm_f32_workspace_size() bytes is given (partials summed in
+ * split order: deterministic); with workspace == NULL the GEMM runs unsplit.
  */
+size_t dlrm_gemm_f32_workspace_size(int64_t M, int64_t N, int64_t K);
 int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
                   float* C, int64_t ldc, int32_t epilogue, const float* bias,
-                  const float* aux, int64_t ld_aux, dlrm_stream_t stream);
+                  const float* aux, int64_t ld_aux, void* workspace, size_t workspace_bytes,
+                  dlrm_stream_t stream);
 
 /* Workspace for dlrm_colsum_f32 (deterministic two-pass column reduction). */
 size_t dlrm_colsum_workspace_size(int64_t M, int64_t N);
@@ -253,9 +263,9 @@ int dlrm_sigmoid_forward(int64_t n, const float* x, float* y, dlrm_stream_t stre
 /* dx = dy * (1 - y) * y */
 int dlrm_sigmoid_backward(int64_t n, const float* dy, const float* y, float* dx,
                           dlrm_stream_t stream);
-/* dx = dy * (y > 0) */
-int dlrm_relu_backward(int64_t n, const float* dy, const float* y, float* dx,
-                       dlrm_stream_t stream);
+/* dx[m][k] = dy[m][k] * (y[m][k] > 0) over an M x K block of row-strided matrices */
+int dlrm_relu_backward(int64_t M, int64_t K, const float* dy, int64_t lddy, const float* y,
+                       int64_t ldy, float* dx, int64_t lddx, dlrm_stream_t stream);
 
 /* ------------------------------------------------------------- utilities --- */
 /* out[i] = lo + (hi - lo) * u_i, u_i uniform in [0,1) from a counter hash of (seed, i). */
