@@ -22,6 +22,8 @@
 // gradients have a long K (= the batch) over a small M x N: the planner splits K
 // until there are >= 2 workgroups per CU; split partials go to a caller workspace and
 // a reduce kernel sums them IN SPLIT ORDER (deterministic) and applies the epilogue.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
@@ -63,6 +65,20 @@ struct TileLoader {
 
   __device__ __forceinline__ void load(const float* __restrict__ X, int64_t ld, int64_t mn0,
                                        int64_t mnlim, int64_t k0, int64_t klim, int tid) {
+    // Workgroup-uniform fast path: the whole panel is in range -> plain float4 loads.
+    if (VEC && mn0 + MN <= mnlim && k0 + BK <= klim) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int q = tid + v * 256;
+        const float* ptr;
+        if constexpr (KCONTIG)
+          ptr = X + (mn0 + q / (BK / 4)) * ld + k0 + 4 * (q % (BK / 4));
+        else
+          ptr = X + (k0 + q / (MN / 4)) * ld + mn0 + 4 * (q % (MN / 4));
+        regs[v] = *reinterpret_cast<const float4*>(ptr);
+      }
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int q = tid + v * 256;
@@ -215,19 +231,24 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
       la.load(p.A, p.lda, m0, p.M, kbeg + (kt + 1) * BK, kend, tid);
       lb.load(p.B, p.ldb, n0, p.N, kbeg + (kt + 1) * BK, kend, tid);
     }
+    // All operands of the K-tile are fetched into registers first (the LDS reads are
+    // independent, so they stay in flight under the MFMA chain instead of exposing
+    // their latency once per k-step), then the MFMAs consume them.
+    float a[BK / 2][TM], b[BK / 2][TN];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      float a[TM], b[TN];
+    for (int s = 0; s < BK / 2; ++s) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[(kk + h) * LA::STRIDE + wm0 + i * 32 + l32];
+      for (int i = 0; i < TM; ++i) a[s][i] = As[(2 * s + h) * LA::STRIDE + wm0 + i * 32 + l32];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[(kk + h) * LB::STRIDE + wn0 + j * 32 + l32];
+      for (int j = 0; j < TN; ++j) b[s][j] = Bs[(2 * s + h) * LB::STRIDE + wn0 + j * 32 + l32];
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][i], b[s][j], acc[i][j], 0, 0, 0);
     if (more) {
       la.store(odd ? As0 : As1, tid);
       lb.store(odd ? Bs0 : Bs1, tid);
@@ -274,13 +295,14 @@ struct Plan {
   int64_t kchunk;
 };
 
-Plan plan_gemm(int64_t M, int64_t N, int64_t K) {
-  const int64_t t128 = dlrm::ceil_div(M, 128) * dlrm::ceil_div(N, 128);
-  if (t128 >= kTargetWG) return {128, 128, 1, K};
-  const int64_t t64x128 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 128);
-  if (t64x128 >= kTargetWG) return {64, 128, 1, K};
-  const int64_t t64 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 64);
-  int64_t s = dlrm::ceil_div(kTargetWG, t64);
+// Tuning overrides (read per call, for sweeps): DLRM_GEMM_TILE=128x128|128x64|64x128|64x64,
+// DLRM_GEMM_SPLIT=<n>, DLRM_GEMM_TARGET=<workgroups>.
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+Plan finish_plan(int bm, int bn, int64_t s, int64_t K) {
   int64_t smax = K / kMinSplitK;
   if (s > smax) s = smax;
   if (s > kMaxSplit) s = kMaxSplit;
@@ -289,7 +311,30 @@ Plan plan_gemm(int64_t M, int64_t N, int64_t K) {
   if (kchunk < BK) kchunk = BK;
   s = dlrm::ceil_div(K, kchunk);
   if (s < 1) s = 1;
-  return {64, 64, (int)s, kchunk};
+  return {bm, bn, (int)s, kchunk};
+}
+
+// Workgroup target: measured on MI355X over the C3 step shapes (tools/gemm_sweep.py) —
+// forward (X W^T, both operands k-contiguous) peaks at ~2 WGs/CU with no split, the
+// dgrad / wgrad forms (one mn-contiguous operand) keep gaining up to ~6 WGs/CU.
+Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc) {
+  const int target = env_int("DLRM_GEMM_TARGET", (a_kc && b_kc) ? kTargetWG : 3 * kTargetWG);
+  const int force_split = env_int("DLRM_GEMM_SPLIT", 0);
+  const char* tile = getenv("DLRM_GEMM_TILE");
+  if (tile && *tile) {
+    int bm = 64, bn = 64;
+    if (sscanf(tile, "%dx%d", &bm, &bn) != 2) bm = bn = 64;
+    const int64_t t = dlrm::ceil_div(M, bm) * dlrm::ceil_div(N, bn);
+    const int64_t s = force_split > 0 ? force_split : dlrm::ceil_div(target, t);
+    return finish_plan(bm, bn, s, K);
+  }
+  const int64_t t128 = dlrm::ceil_div(M, 128) * dlrm::ceil_div(N, 128);
+  if (t128 >= target) return {128, 128, 1, K};
+  const int64_t t64x128 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 128);
+  if (t64x128 >= target) return {64, 128, 1, K};
+  const int64_t t64 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 64);
+  const int64_t s = force_split > 0 ? force_split : dlrm::ceil_div(target, t64);
+  return finish_plan(64, 64, s, K);
 }
 
 template <int BM, int BN>
@@ -333,9 +378,10 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 }  // namespace
 
-extern "C" size_t dlrm_gemm_f32_workspace_size(int64_t M, int64_t N, int64_t K) {
+extern "C" size_t dlrm_gemm_f32_workspace_size(int32_t trans_a, int32_t trans_b, int64_t M,
+                                               int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  const Plan pl = plan_gemm(M, N, K);
+  const Plan pl = plan_gemm(M, N, K, !trans_a, trans_b != 0);
   return pl.splits > 1 ? (size_t)pl.splits * M * N * sizeof(float) : 0;
 }
 
@@ -373,7 +419,7 @@ extern "C" int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_
   p.bias = bias;
   p.aux = aux;
   p.ldaux = ld_aux;
-  Plan pl = plan_gemm(M, N, K);
+  Plan pl = plan_gemm(M, N, K, !trans_a, trans_b != 0);
   if (pl.splits > 1) {
     const size_t need = (size_t)pl.splits * M * N * sizeof(float);
     if (!workspace || workspace_bytes < need) {  // no workspace: single pass
@@ -389,7 +435,9 @@ extern "C" int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_
   const bool va = aligned16(A) && (lda % 4 == 0);
   const bool vb = aligned16(B) && (ldb % 4 == 0);
   hipStream_t st = dlrm::as_stream(stream);
-  if (pl.bm == 128) return launch_tiles<128, 128>(p, pl.splits, a_kc, b_kc, va, vb, st);
+  if (pl.bm == 128 && pl.bn == 128)
+    return launch_tiles<128, 128>(p, pl.splits, a_kc, b_kc, va, vb, st);
+  if (pl.bm == 128) return launch_tiles<128, 64>(p, pl.splits, a_kc, b_kc, va, vb, st);
   if (pl.bn == 128) return launch_tiles<64, 128>(p, pl.splits, a_kc, b_kc, va, vb, st);
   return launch_tiles<64, 64>(p, pl.splits, a_kc, b_kc, va, vb, st);
 }

@@ -54,7 +54,7 @@ SIGNATURES = {
                                              c_int64, P, P, P]),
     "dlrm_interact_cat_forward": (c_int32, [c_int32, c_int32, c_int32, P, P, P, c_int64, P]),
     "dlrm_interact_cat_backward": (c_int32, [c_int32, c_int32, c_int32, P, c_int64, P, P, P]),
-    "dlrm_gemm_f32_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
+    "dlrm_gemm_f32_workspace_size": (c_size_t, [c_int32, c_int32, c_int64, c_int64, c_int64]),
     "dlrm_gemm_f32": (c_int32, [c_int32, c_int32, c_int64, c_int64, c_int64, c_float, P, c_int64,
                                 P, c_int64, P, c_int64, c_int32, P, P, c_int64, P, c_size_t, P]),
     "dlrm_colsum_workspace_size": (c_size_t, [c_int64, c_int64]),

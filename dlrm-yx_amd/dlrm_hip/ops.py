@@ -242,8 +242,9 @@ def interact_backward(op: str, x: torch.Tensor, ly, grad_out: torch.Tensor,
 
 
 # ------------------------------------------------------------------ MLP ----
-def gemm_workspace_size(M: int, N: int, K: int) -> int:
-    return _lib.query("dlrm_gemm_f32_workspace_size", M, N, K)
+def gemm_workspace_size(M: int, N: int, K: int, trans_a: bool = False,
+                        trans_b: bool = False) -> int:
+    return _lib.query("dlrm_gemm_f32_workspace_size", int(trans_a), int(trans_b), M, N, K)
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
@@ -263,7 +264,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool 
         raise ValueError(f"gemm inner dims differ: {K} vs {Kb}")
     if C is None:
         C = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    need = gemm_workspace_size(M, N, K)
+    need = gemm_workspace_size(M, N, K, trans_a, trans_b)
     if need and (workspace is None or workspace.numel() < need):
         workspace = _ws("gemm", need, A.device)
     _lib.call("dlrm_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), _p(A),

@@ -293,7 +293,8 @@ class DLRMTrainer:
         # one split-K workspace sized for the largest GEMM of the step
         shapes = []
         for L in self.layers[:-1]:
-            shapes += [(Bl, L.N, L.Kp), (Bl, L.Kp, L.N), (L.N, L.Kp, Bl)]
+            shapes += [(Bl, L.N, L.Kp, False, True), (Bl, L.K, L.N, False, False),
+                       (L.N, L.Kp, Bl, True, False)]
         gws = max([ops.gemm_workspace_size(*s) for s in shapes] + [256])
         self._gemm_ws = torch.empty(gws, dtype=torch.uint8, device=dev)
         bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(2)]
@@ -386,11 +387,11 @@ class DLRMTrainer:
         for li in range(len(self.top) - 2, -1, -1):
             L = self.top[li]
             inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
-            dinp = g_nxt[:, :L.Kp]
+            dinp = g_nxt[:, :L.K]
             if li > 0:
-                gemm(g[:, :L.N], L.W, C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
+                gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
             else:
-                gemm(g[:, :L.N], L.W, C=dinp)
+                gemm(g[:, :L.N], L.W[:, :L.K], C=dinp)
             self._wgrad(L, g, inp, fused_opt, lr)
             g = dinp
             g_cur, g_nxt = g_nxt, g_cur
@@ -410,8 +411,8 @@ class DLRMTrainer:
             L = self.bot[li]
             inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
             if li > 0:
-                dinp = g_nxt[:, :L.Kp]
-                gemm(g[:, :L.N], L.W, C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
+                dinp = g_nxt[:, :L.K]
+                gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
             self._wgrad(L, g, inp, fused_opt, lr)
             if li > 0:
                 g = dinp

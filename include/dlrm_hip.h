@@ -213,7 +213,8 @@ int dlrm_interact_cat_backward(int32_t B, int32_t F, int32_t D, const float* gra
  * workspace of dlrm_gemm_f32_workspace_size() bytes is given (partials summed in
  * split order: deterministic); with workspace == NULL the GEMM runs unsplit.
  */
-size_t dlrm_gemm_f32_workspace_size(int64_t M, int64_t N, int64_t K);
+size_t dlrm_gemm_f32_workspace_size(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
+                                    int64_t K);
 int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
                   float* C, int64_t ldc, int32_t epilogue, const float* bias,
