@@ -109,6 +109,34 @@ class KernelTimer:
         return out, cnt
 
 
+def _sleep_cycles_for(ms: float) -> int:
+    """Cycles of torch.cuda._sleep that park the stream for about ``ms`` milliseconds."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 1_000_000
+    s.record()
+    torch.cuda._sleep(n)
+    e.record()
+    torch.cuda.synchronize()
+    per_ms = n / max(s.elapsed_time(e), 1e-3)
+    return int(per_ms * ms)
+
+
+def pmc_traffic():
+    """HBM bytes per step of the GEMM group from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, made by tools/pmc_summary.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench); None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    g = d.get("gemm")
+    if not g:
+        return None, None
+    return (int(g["hbm_bytes_per_launch"] * g["launches_per_step_approx"]),
+            os.path.relpath(files[-1], ROOT))
+
+
 def cpu_baseline(c, seconds: float):
     """The CPU oracle (a restatement of the reference step, pinned to its golden vectors)
     timed on this host's cores: bounded sample of the same workload."""
@@ -154,7 +182,7 @@ def cpu_baseline(c, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="terabyte", choices=list(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="global batch (default: config's)")
@@ -228,11 +256,17 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    evs[0].record()
     for k in range(args.steps):
         run_step(k)
+        evs[k + 1].record()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    per_step = sorted(evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps))
+    pct = {q: round(per_step[min(len(per_step) - 1, int(q / 100 * len(per_step)))], 4)
+           for q in (10, 50, 90)}
     barrier()
     el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -248,17 +282,27 @@ def main():
     if not args.no_kernel_timing:
         timer = KernelTimer()
         kt = max(5, min(args.steps, 20))
+        sleep_cycles = _sleep_cycles_for(3.0)
         for k in range(kt):
+            # park the stream so the whole step is enqueued before any of it runs: the
+            # event pairs then bracket back-to-back kernels, not host launch latency
+            torch.cuda._sleep(sleep_cycles)
             tr.step(batches[k % nb], profile=timer)
+            torch.cuda.synchronize()
         tot, cnt = timer.totals()
         groups = {k: round(v / kt * 1000.0, 2) for k, v in tot.items()}  # us per step
         gemm_ms = tot.get("gemm", 0.0) / kt
         if gemm_ms > 0:
             ach = flops / (gemm_ms * 1e-3) / 1e12
+            traffic, tsrc = pmc_traffic() if world == 1 else (None, None)
             roofline = {"bound": "mfma", "kernel": "gemm_f32_mfma (all MLP GEMM launches)",
                         "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS,
                         "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFS, 4),
-                        "traffic": None, "launches_per_step": cnt.get("gemm", 0) // kt,
+                        "traffic": traffic,
+                        "traffic_unit": "HBM bytes per step, GEMM group (FETCH_SIZE x2 + "
+                                        "WRITE_SIZE)" if traffic else None,
+                        "traffic_source": tsrc,
+                        "launches_per_step": cnt.get("gemm", 0) // kt,
                         "us_per_step": round(gemm_ms * 1000.0, 2),
                         "algorithmic_flop_per_step": flops}
         f_ms = tot.get("tbe_fwd", 0.0) / kt
@@ -280,6 +324,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1000.0, 4),
+            "ms_per_step_p10_p50_p90": [pct[10], pct[50], pct[90]],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (device-generated, reference distributions; random init)",
             "config": {"workload": c["workload"], "global_batch": B, "local_batch": Bl,
