@@ -1,5 +1,5 @@
 // Exact-fp32 GEMM with fused epilogues on the gfx950 fp32 matrix core
-// (v_mfma_f32_32x32x2_f32: 64 FLOP/clk/SIMD, bit-exact k-ordered fmaf chain, no xf32).
+// (v_mfma_f32_32x32x2_f32: 64 FLOP/clk/SIMD, k-ordered fmaf chain, no xf32).
 //
 // Serves the DLRM MLPs (DLRM_Net.create_mlp / apply_mlp, dlrm_s_pytorch.py:227-265,
 // 518-524): Linear forward with bias(+ReLU) fused, dgrad with the ReLU mask of the
@@ -7,30 +7,33 @@
 // into the flat gradient bucket (multi GPU, all-reduced before the update).
 //
 // Structure: 256-thread workgroups = 4 waves in a 2x2 arrangement, each wave owning a
-// (BM/2)x(BN/2) sub-tile built from 32x32 MFMA accumulators (16 AGPRs each).  K is
-// staged BK=32 deep through double-buffered LDS in k-major rows ([k][m], [k][n]) so
-// each MFMA operand fetch is one conflict-free ds_read_b32 per lane (32 consecutive
-// floats per half-wave).  Operands that are k-contiguous in HBM (X rows, W rows of
-// nn.Linear) are transposed on the LDS write with an odd row pitch (conflict-free
-// ds_write_b32); mn-contiguous operands go in with ds_write_b128.  The next K-tile is
-// fetched into registers before the MFMAs of the current one (global latency hidden
-// under 64-cycle MFMAs) and written after them, one barrier per K-tile.  Workgroups
-// are remapped bijectively so that each XCD (private 4 MiB L2) receives a contiguous
-// run of output tiles that share operand panels.
+// (BM/2)x(BN/2) sub-tile of 32x32 MFMA accumulators (16 AGPRs each).  K is staged
+// BK deep through double-buffered LDS.  The k-order inside a K-tile is permuted so
+// that a lane's operands are CONTIGUOUS: lane (l, h) (l = lane & 31, h = lane >> 5)
+// feeds k = h*BK/2 + s at MFMA step s, for both operands, so
+//   * an operand that is k-contiguous in HBM (X rows, nn.Linear W rows) is staged
+//     [mn][k] with float4 loads + ds_write_b128 and its fragments are ds_read_b128
+//     (16 k-values in 4 instructions);
+//   * an mn-contiguous operand is staged [k][mn] (float4 along mn, ds_write_b128) and
+//     read with conflict-free ds_read_b32 (32 consecutive floats per half-wave).
+// The next K-tile is fetched into registers before the MFMAs of the current one and
+// written after them (one barrier per K-tile).  Workgroups are remapped bijectively
+// so each XCD (private 4 MiB L2) receives a contiguous run of output tiles.
 //
 // DLRM's GEMMs are small for 256 CUs (M = batch <= 2048, N,K <= 1024) and the weight
-// gradients have a long K (= the batch) over a small M x N: the planner splits K
-// until there are >= 2 workgroups per CU; split partials go to a caller workspace and
-// a reduce kernel sums them IN SPLIT ORDER (deterministic) and applies the epilogue.
+// gradients have a long K (= the batch) over a small M x N: the planner may split K;
+// split partials go to a caller workspace and a reduce kernel sums them IN SPLIT ORDER
+// (deterministic) and applies the epilogue.  Tile / BK / split per shape come from
+// on-device sweeps (tools/gemm_sweep.py), with a heuristic for other shapes.
 #include <cstdlib>
+#include <cstring>
 
 #include "common.hpp"
 
 namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
-constexpr int BK = 32;
-constexpr int kTargetWG = 512;  // 2 workgroups per CU
+constexpr int kThreads = 256;
 constexpr int kMaxSplit = 32;
 constexpr int kMinSplitK = 128;
 
@@ -52,64 +55,53 @@ struct GemmParams {
   float* ws;       // split partials [splits][M][N] (splits > 1 only)
 };
 
-// Stages an (MN x BK) panel of X into LDS rows [BK][MN + PAD].
-//   KCONTIG: X(mn, k) = X[mn*ld + k]     (float4 along k, transposed on the LDS write)
-//   else   : X(mn, k) = X[k*ld + mn]     (float4 along mn, direct ds_write_b128)
-template <int MN, bool KCONTIG, bool VEC>
-struct TileLoader {
-  static constexpr int NV = MN * BK / 4 / 256;  // float4 per thread
-  static constexpr int PAD = KCONTIG ? 1 : 4;
-  static constexpr int STRIDE = MN + PAD;
-  static constexpr int SIZE = BK * STRIDE;  // floats per LDS stage
+// One operand's (MN x BKT) panel, staged global -> registers -> LDS.
+//   KC  : X(mn, k) = X[mn*ld + k]  -> LDS [mn][BKT + 4]   (fragments: ds_read_b128)
+//   !KC : X(mn, k) = X[k*ld + mn]  -> LDS [BKT][MN + 4]   (fragments: ds_read_b32)
+template <int MN, int BKT, bool KC, bool VEC>
+struct Stage {
+  static constexpr int PITCH = KC ? BKT + 4 : MN + 4;
+  static constexpr int SIZE = KC ? MN * PITCH : BKT * PITCH;  // floats per LDS buffer
+  static constexpr int NV = MN * BKT / 4 / kThreads;         // float4 per thread
+  static_assert(NV >= 1 && MN * BKT % (4 * kThreads) == 0, "panel / thread mismatch");
   float4 regs[NV];
+
+  __device__ __forceinline__ void coords(int q, int& mn, int& k) const {
+    if constexpr (KC) {
+      mn = q / (BKT / 4);
+      k = 4 * (q % (BKT / 4));
+    } else {
+      k = q / (MN / 4);
+      mn = 4 * (q % (MN / 4));
+    }
+  }
 
   __device__ __forceinline__ void load(const float* __restrict__ X, int64_t ld, int64_t mn0,
                                        int64_t mnlim, int64_t k0, int64_t klim, int tid) {
-    // Workgroup-uniform fast path: the whole panel is in range -> plain float4 loads.
-    if (VEC && mn0 + MN <= mnlim && k0 + BK <= klim) {
+    if (VEC && mn0 + MN <= mnlim && k0 + BKT <= klim) {  // workgroup-uniform fast path
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
-        const int q = tid + v * 256;
-        const float* ptr;
-        if constexpr (KCONTIG)
-          ptr = X + (mn0 + q / (BK / 4)) * ld + k0 + 4 * (q % (BK / 4));
-        else
-          ptr = X + (k0 + q / (MN / 4)) * ld + mn0 + 4 * (q % (MN / 4));
+        int mn, k;
+        coords(tid + v * kThreads, mn, k);
+        const float* ptr = KC ? X + (mn0 + mn) * ld + k0 + k : X + (k0 + k) * ld + mn0 + mn;
         regs[v] = *reinterpret_cast<const float4*>(ptr);
       }
       return;
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int q = tid + v * 256;
-      int64_t gmn, gk;
-      if constexpr (KCONTIG) {
-        gmn = mn0 + q / (BK / 4);
-        gk = k0 + 4 * (q % (BK / 4));
-      } else {
-        gk = k0 + q / (MN / 4);
-        gmn = mn0 + 4 * (q % (MN / 4));
-      }
-      float e[4];
-      bool full;
-      const float* ptr;
-      if constexpr (KCONTIG) {
-        full = (gmn < mnlim) && (gk + 3 < klim);
-        ptr = X + gmn * ld + gk;
-      } else {
-        full = (gk < klim) && (gmn + 3 < mnlim);
-        ptr = X + gk * ld + gmn;
-      }
+      int mn, k;
+      coords(tid + v * kThreads, mn, k);
+      const int64_t gmn = mn0 + mn, gk = k0 + k;
+      const float* ptr = KC ? X + gmn * ld + gk : X + gk * ld + gmn;
+      const bool full = KC ? (gmn < mnlim && gk + 3 < klim) : (gk < klim && gmn + 3 < mnlim);
       if (VEC && full) {
         regs[v] = *reinterpret_cast<const float4*>(ptr);
       } else {
+        float e[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          bool ok;
-          if constexpr (KCONTIG)
-            ok = (gmn < mnlim) && (gk + c < klim);
-          else
-            ok = (gk < klim) && (gmn + c < mnlim);
+          const bool ok = KC ? (gmn < mnlim && gk + c < klim) : (gk < klim && gmn + c < mnlim);
           e[c] = ok ? ptr[c] : 0.f;
         }
         regs[v] = make_float4(e[0], e[1], e[2], e[3]);
@@ -120,19 +112,30 @@ struct TileLoader {
   __device__ __forceinline__ void store(float* __restrict__ lds, int tid) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int q = tid + v * 256;
-      if constexpr (KCONTIG) {
-        const int mn = q / (BK / 4);
-        const int kq = q % (BK / 4);
-        lds[(4 * kq + 0) * STRIDE + mn] = regs[v].x;
-        lds[(4 * kq + 1) * STRIDE + mn] = regs[v].y;
-        lds[(4 * kq + 2) * STRIDE + mn] = regs[v].z;
-        lds[(4 * kq + 3) * STRIDE + mn] = regs[v].w;
-      } else {
-        const int k = q / (MN / 4);
-        const int mq = q % (MN / 4);
-        *reinterpret_cast<float4*>(lds + k * STRIDE + 4 * mq) = regs[v];
+      int mn, k;
+      coords(tid + v * kThreads, mn, k);
+      float* dst = KC ? lds + mn * PITCH + k : lds + k * PITCH + mn;
+      *reinterpret_cast<float4*>(dst) = regs[v];
+    }
+  }
+
+  // 16 consecutive k-steps (k = kbase .. kbase+15) of the 32-wide sub-tile at `off`
+  // for this lane (row/col off + l32).
+  __device__ __forceinline__ void frag(const float* __restrict__ lds, int off, int l32, int kbase,
+                                       float (&f)[16]) const {
+    if constexpr (KC) {
+      const float* p = lds + (off + l32) * PITCH + kbase;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 v = *reinterpret_cast<const float4*>(p + 4 * c);
+        f[4 * c + 0] = v.x;
+        f[4 * c + 1] = v.y;
+        f[4 * c + 2] = v.z;
+        f[4 * c + 3] = v.w;
       }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) f[s] = lds[(kbase + s) * PITCH + off + l32];
     }
   }
 };
@@ -173,17 +176,18 @@ __device__ __forceinline__ void apply_epilogue(const GemmParams& p, int64_t row,
   *cp = v;
 }
 
-template <int BM, int BN, bool A_KC, bool B_KC, bool VA, bool VB>
-__global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
+template <int BM, int BN, int BKT, bool A_KC, bool B_KC, bool VEC>
+__global__ __launch_bounds__(kThreads, (BM * BN >= 128 * 128 && BKT >= 64) ? 1 : 2)
+void gemm_f32_mfma_kernel(GemmParams p) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
-  using LA = TileLoader<BM, A_KC, VA>;
-  using LB = TileLoader<BN, B_KC, VB>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (LA::SIZE + LB::SIZE)];
+  using SA = Stage<BM, BKT, A_KC, VEC>;
+  using SB = Stage<BN, BKT, B_KC, VEC>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (SA::SIZE + SB::SIZE)];
   float* As0 = smem;
-  float* Bs0 = smem + LA::SIZE;
-  float* As1 = smem + LA::SIZE + LB::SIZE;
-  float* Bs1 = As1 + LA::SIZE;
+  float* Bs0 = smem + SA::SIZE;
+  float* As1 = smem + SA::SIZE + SB::SIZE;
+  float* Bs1 = As1 + SA::SIZE;
 
   const int nwg = p.tiles_m * p.tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -211,14 +215,14 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  LA la;
-  LB lb;
-  const int64_t nk = (kend - kbeg + BK - 1) / BK;
+  SA sa;
+  SB sb;
+  const int64_t nk = (kend - kbeg + BKT - 1) / BKT;
   if (nk > 0) {
-    la.load(p.A, p.lda, m0, p.M, kbeg, kend, tid);
-    lb.load(p.B, p.ldb, n0, p.N, kbeg, kend, tid);
-    la.store(As0, tid);
-    lb.store(Bs0, tid);
+    sa.load(p.A, p.lda, m0, p.M, kbeg, kend, tid);
+    sb.load(p.B, p.ldb, n0, p.N, kbeg, kend, tid);
+    sa.store(As0, tid);
+    sb.store(Bs0, tid);
   }
   __syncthreads();
 
@@ -228,30 +232,28 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma_kernel(GemmParams p) {
     const float* Bs = odd ? Bs1 : Bs0;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(p.A, p.lda, m0, p.M, kbeg + (kt + 1) * BK, kend, tid);
-      lb.load(p.B, p.ldb, n0, p.N, kbeg + (kt + 1) * BK, kend, tid);
-    }
-    // All operands of the K-tile are fetched into registers first (the LDS reads are
-    // independent, so they stay in flight under the MFMA chain instead of exposing
-    // their latency once per k-step), then the MFMAs consume them.
-    float a[BK / 2][TM], b[BK / 2][TN];
-#pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[s][i] = As[(2 * s + h) * LA::STRIDE + wm0 + i * 32 + l32];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[s][j] = Bs[(2 * s + h) * LB::STRIDE + wn0 + j * 32 + l32];
+      sa.load(p.A, p.lda, m0, p.M, kbeg + (kt + 1) * BKT, kend, tid);
+      sb.load(p.B, p.ldb, n0, p.N, kbeg + (kt + 1) * BKT, kend, tid);
     }
 #pragma unroll
-    for (int s = 0; s < BK / 2; ++s)
+    for (int sub = 0; sub < BKT / 32; ++sub) {
+      const int kbase = h * (BKT / 2) + sub * 16;
+      float a[TM][16], b[TN][16];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) sa.frag(As, wm0 + i * 32, l32, kbase, a[i]);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][i], b[s][j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) sb.frag(Bs, wn0 + j * 32, l32, kbase, b[j]);
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+    }
     if (more) {
-      la.store(odd ? As0 : As1, tid);
-      lb.store(odd ? Bs0 : Bs1, tid);
+      sa.store(odd ? As0 : As1, tid);
+      sb.store(odd ? Bs0 : Bs1, tid);
     }
     __syncthreads();
   }
@@ -291,69 +293,83 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmParams p, i
 }
 
 struct Plan {
-  int bm, bn, splits;
+  int bm, bn, bk, splits;
   int64_t kchunk;
 };
 
-// Tuning overrides (read per call, for sweeps): DLRM_GEMM_TILE=128x128|128x64|64x128|64x64,
-// DLRM_GEMM_SPLIT=<n>, DLRM_GEMM_TARGET=<workgroups>.
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
 }
 
-Plan finish_plan(int bm, int bn, int64_t s, int64_t K) {
+Plan finish_plan(int bm, int bn, int bk, int64_t s, int64_t K) {
   int64_t smax = K / kMinSplitK;
   if (s > smax) s = smax;
   if (s > kMaxSplit) s = kMaxSplit;
   if (s < 1) s = 1;
-  int64_t kchunk = dlrm::ceil_div(dlrm::ceil_div(K, s), BK) * BK;
-  if (kchunk < BK) kchunk = BK;
+  int64_t kchunk = dlrm::ceil_div(dlrm::ceil_div(K, s), bk) * bk;
+  if (kchunk < bk) kchunk = bk;
   s = dlrm::ceil_div(K, kchunk);
   if (s < 1) s = 1;
-  return {bm, bn, (int)s, kchunk};
+  return {bm, bn, bk, (int)s, kchunk};
 }
 
-// Workgroup target: measured on MI355X over the C3 step shapes (tools/gemm_sweep.py) —
-// forward (X W^T, both operands k-contiguous) peaks at ~2 WGs/CU with no split, the
-// dgrad / wgrad forms (one mn-contiguous operand) keep gaining up to ~6 WGs/CU.
+bool valid_cfg(int bm, int bn, int bk) {
+  const bool tile = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
+  return tile && (bk == 32 || bk == 64);
+}
+
+struct PlanEntry {
+  int64_t M, N, K;
+  int ta, tb, bm, bn, bk, split;
+};
+
+// Measured plans for the DLRM step shapes (exact match), from tools/gemm_sweep.py.
+constexpr PlanEntry kPlans[] = {
+#include "gemm_plans.inc"
+};
+
+// Tuning overrides (read per call, for sweeps): DLRM_GEMM_CFG=<BM>x<BN>x<BK>,
+// DLRM_GEMM_SPLIT=<n>, DLRM_GEMM_TARGET=<workgroups>.
 Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc) {
-  const int target = env_int("DLRM_GEMM_TARGET", (a_kc && b_kc) ? kTargetWG : 3 * kTargetWG);
   const int force_split = env_int("DLRM_GEMM_SPLIT", 0);
-  const char* tile = getenv("DLRM_GEMM_TILE");
-  if (tile && *tile) {
-    int bm = 64, bn = 64;
-    if (sscanf(tile, "%dx%d", &bm, &bn) != 2) bm = bn = 64;
+  const char* cfg = getenv("DLRM_GEMM_CFG");
+  if (cfg && *cfg) {
+    int bm = 64, bn = 64, bk = 32;
+    if (sscanf(cfg, "%dx%dx%d", &bm, &bn, &bk) != 3 || !valid_cfg(bm, bn, bk)) bm = bn = 64, bk = 32;
     const int64_t t = dlrm::ceil_div(M, bm) * dlrm::ceil_div(N, bn);
-    const int64_t s = force_split > 0 ? force_split : dlrm::ceil_div(target, t);
-    return finish_plan(bm, bn, s, K);
+    const int64_t s = force_split > 0 ? force_split : 1;
+    (void)t;
+    return finish_plan(bm, bn, bk, s, K);
   }
+  const int ta = a_kc ? 0 : 1, tb = b_kc ? 1 : 0;
+  for (const PlanEntry& e : kPlans)
+    if (e.M == M && e.N == N && e.K == K && e.ta == ta && e.tb == tb && !getenv("DLRM_GEMM_NOTABLE"))
+      return finish_plan(e.bm, e.bn, e.bk, e.split, K);
+  // Heuristic: the largest tile that still gives >= target workgroups; split K of the
+  // 64x64 tiling up to the target otherwise.
+  const int target = env_int("DLRM_GEMM_TARGET", (a_kc && b_kc) ? 512 : 1536);
   const int64_t t128 = dlrm::ceil_div(M, 128) * dlrm::ceil_div(N, 128);
-  if (t128 >= target) return {128, 128, 1, K};
+  if (t128 >= target) return {128, 128, 32, 1, K};
   const int64_t t64x128 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 128);
-  if (t64x128 >= target) return {64, 128, 1, K};
+  if (t64x128 >= target) return {64, 128, 32, 1, K};
   const int64_t t64 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 64);
   const int64_t s = force_split > 0 ? force_split : dlrm::ceil_div(target, t64);
-  return finish_plan(64, 64, s, K);
+  return finish_plan(64, 64, 32, s, K);
 }
 
-template <int BM, int BN>
-int launch_tiles(GemmParams p, int splits, bool a_kc, bool b_kc, bool va, bool vb,
-                 hipStream_t st) {
+template <int BM, int BN, int BKT>
+int launch_cfg(GemmParams p, int splits, bool a_kc, bool b_kc, bool vec, hipStream_t st) {
   p.tiles_m = (int)dlrm::ceil_div(p.M, BM);
   p.tiles_n = (int)dlrm::ceil_div(p.N, BN);
-  const dim3 grid(p.tiles_m * p.tiles_n, splits), block(256);
-#define G(AK, BK_, VA_, VB_) \
-  hipLaunchKernelGGL((gemm_f32_mfma_kernel<BM, BN, AK, BK_, VA_, VB_>), grid, block, 0, st, p)
-#define G_V(AK, BK_)          \
-  if (va && vb)               \
-    G(AK, BK_, true, true);   \
-  else if (va)                \
-    G(AK, BK_, true, false);  \
-  else if (vb)                \
-    G(AK, BK_, false, true);  \
-  else                        \
-    G(AK, BK_, false, false);
+  const dim3 grid(p.tiles_m * p.tiles_n, splits), block(kThreads);
+#define G(AK, BK_, V_) \
+  hipLaunchKernelGGL((gemm_f32_mfma_kernel<BM, BN, BKT, AK, BK_, V_>), grid, block, 0, st, p)
+#define G_V(AK, BK_)  \
+  if (vec)            \
+    G(AK, BK_, true); \
+  else                \
+    G(AK, BK_, false);
   if (a_kc && b_kc) {
     G_V(true, true)
   } else if (a_kc) {
@@ -432,12 +448,20 @@ extern "C" int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_
   p.kchunk = pl.kchunk > 0 ? pl.kchunk : 1;
   const bool a_kc = !trans_a;
   const bool b_kc = trans_b != 0;
-  const bool va = aligned16(A) && (lda % 4 == 0);
-  const bool vb = aligned16(B) && (ldb % 4 == 0);
+  const bool vec = aligned16(A) && (lda % 4 == 0) && aligned16(B) && (ldb % 4 == 0);
   hipStream_t st = dlrm::as_stream(stream);
-  if (pl.bm == 128 && pl.bn == 128)
-    return launch_tiles<128, 128>(p, pl.splits, a_kc, b_kc, va, vb, st);
-  if (pl.bm == 128) return launch_tiles<128, 64>(p, pl.splits, a_kc, b_kc, va, vb, st);
-  if (pl.bn == 128) return launch_tiles<64, 128>(p, pl.splits, a_kc, b_kc, va, vb, st);
-  return launch_tiles<64, 64>(p, pl.splits, a_kc, b_kc, va, vb, st);
+#define CFG(BM_, BN_, BK_)                       \
+  if (pl.bm == BM_ && pl.bn == BN_ && pl.bk == BK_) \
+    return launch_cfg<BM_, BN_, BK_>(p, pl.splits, a_kc, b_kc, vec, st);
+  CFG(64, 64, 32)
+  CFG(128, 64, 32)
+  CFG(64, 128, 32)
+  CFG(128, 128, 32)
+  CFG(64, 64, 64)
+  CFG(128, 64, 64)
+  CFG(64, 128, 64)
+  CFG(128, 128, 64)
+#undef CFG
+  dlrm::set_error("dlrm_gemm_f32: no kernel for plan %dx%dx%d", pl.bm, pl.bn, pl.bk);
+  return DLRM_ERR_UNSUPPORTED;
 }
