@@ -216,6 +216,33 @@ def test_gemm_vs_fp64(ops, M, N, K, ta, tb):
     assert ok, msg
 
 
+GEMM_CFGS = ["64x64x32", "128x64x32", "64x128x32", "128x128x32", "64x64x64", "128x64x64",
+             "64x128x64", "128x128x64", "64x64x32x2", "128x64x32x2", "64x128x32x2",
+             "128x128x32x2", "64x64x64x2", "64x64x32x16", "128x64x32x16", "64x128x32x16",
+             "128x128x32x16", "64x64x32x32", "128x64x32x32", "64x128x32x32"]
+
+
+@pytest.mark.parametrize("cfg", GEMM_CFGS)
+def test_gemm_every_kernel_config(ops, cfg, monkeypatch):
+    """Every tile/BK/k-group/MFMA-shape instantiation the planner can pick, forced via the
+    tuning override, on ragged shapes in all four operand layouts, with and without split-K."""
+    monkeypatch.setenv("DLRM_GEMM_CFG", cfg)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+    for (M, N, K) in [(130, 70, 300), (64, 128, 256), (3, 5, 1030)]:
+        for ta, tb in [(0, 1), (0, 0), (1, 0), (1, 1)]:
+            for split in ("1", "3"):
+                monkeypatch.setenv("DLRM_GEMM_SPLIT", split)
+                torch.manual_seed(M * 7 + N + K + ta * 3 + tb)
+                A = torch.randn(K, M) if ta else torch.randn(M, K)
+                Bm = torch.randn(N, K) if tb else torch.randn(K, N)
+                opA = A.double().t() if ta else A.double()
+                opB = Bm.double().t() if tb else Bm.double()
+                C = ops.gemm(A.to(dev), Bm.to(dev), bool(ta), bool(tb), workspace=ws).cpu()
+                ok, msg = gemm_close(C.numpy(), (opA @ opB).numpy(),
+                                     (opA.abs() @ opB.abs()).numpy(), K)
+                assert ok, (cfg, M, N, K, ta, tb, split, msg)
+
+
 def test_gemm_epilogues(ops):
     torch.manual_seed(3)
     M, N, K = 300, 200, 130

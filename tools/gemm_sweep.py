@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from dlrm_hip import ops  # noqa: E402
 
 CFGS = ["64x64x32", "128x64x32", "64x128x32", "128x128x32", "64x64x64", "128x64x64",
-        "64x128x64", "128x128x64"]
+        "64x128x64", "128x128x64", "64x64x32x2", "128x64x32x2", "64x128x32x2", "128x128x32x2",
+        "64x64x64x2", "64x64x32x16", "128x64x32x16", "64x128x32x16", "128x128x32x16", "64x64x32x32", "128x64x32x32", "64x128x32x32"]
 SPLITS = [1, 2, 3, 4, 6, 8, 12, 16]
 # (K, N) of the C3 (terabyte) layers and the C1/C2 widths
 LAYER_SETS = {
@@ -103,9 +104,11 @@ def main():
                 os.environ.pop("DLRM_GEMM_SPLIT", None)
                 tot_best += res[0][0]
                 tot_default += t0
-                bm, bn, bk = (int(v) for v in res[0][1].split("x"))
+                parts = [int(v) for v in res[0][1].split("x")]
+                bm, bn, bk = parts[:3]
+                ks = parts[3] if len(parts) > 3 else 1
                 plans.append({"M": M_, "N": N_, "K": K_, "trans_a": ta, "trans_b": tb,
-                              "bm": bm, "bn": bn, "bk": bk, "split": res[0][2],
+                              "bm": bm, "bn": bn, "bk": bk, "ks": ks, "split": res[0][2],
                               "us": round(res[0][0] * 1e6, 2)})
                 top = " ".join(f"{c}/{s}:{tt * 1e6:.1f}" for tt, c, s in res[:4])
                 print(f"B{B} L{li} {K:5d}->{N:5d} {name:6s} blas {tb_ * 1e6:6.1f}us "
