@@ -24,6 +24,7 @@ optimizer update.  Layout decisions (MI355X-first):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -158,6 +159,14 @@ class DLRMTrainer:
         self.bot = self.layers[:self.n_bot]
         self.top = self.layers[self.n_bot:]
         self._bufs = {}
+        # independent kernels of a step run on a side stream (see step())
+        self.concurrent = True
+        # which overlaps to use: "fwd" (bottom MLP || lookup), "top" (wgrad || next dgrad),
+        # "bot" (bottom-MLP backward || embedding backward).  Off by default: measured on
+        # MI355X, each cross-queue dependency in a replayed hipGraph costs ~10 us, more than
+        # the overlap recovers at C3 (profiles/r01_overlap_ab.txt).
+        self.overlaps = set(os.environ.get("DLRM_OVERLAPS", "").split(","))
+        self._side = torch.cuda.Stream(device=self.dev)
         self._tbe_ws: Optional[torch.Tensor] = None
         self._colsum_ws: Optional[torch.Tensor] = None
         self._head_ws: Optional[torch.Tensor] = None
@@ -297,7 +306,12 @@ class DLRMTrainer:
                        (L.N, L.Kp, Bl, True, False)]
         gws = max([ops.gemm_workspace_size(*s) for s in shapes] + [256])
         self._gemm_ws = torch.empty(gws, dtype=torch.uint8, device=dev)
-        bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(2)]
+        self._gemm_ws_side = torch.empty(gws, dtype=torch.uint8, device=dev)
+        # three gradient buffers: a weight-gradient GEMM on the side stream may still read
+        # g_l while the main stream's next two data-gradient GEMMs produce g_{l-1}, g_{l-2}
+        bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(3)]
+        wbot = max(L.Kp for L in self.bot)
+        bufs["gb"] = [torch.zeros((Bl, wbot), **f32) for _ in range(2)]
         bufs["dx"] = torch.zeros((Bl, D), **f32)
         bufs["gx"] = torch.zeros((Bl, D), **f32)
         bufs["E"] = torch.zeros((B, max(self.T_local, 1), D), **f32)
@@ -330,7 +344,13 @@ class DLRMTrainer:
     # ---------------------------------------------------------------- step --
     def step(self, batch: Batch, profile=None):
         """One fwd + loss + bwd + update.  Returns (prob [B_local], loss [1]) device tensors.
-        ``profile``: optional callable(name) -> context manager around kernel groups."""
+        ``profile``: optional callable(name) -> context manager around kernel groups (the
+        step then runs on one stream so each group's events bracket only its kernels).
+
+        Independent work runs on a side stream (joined before return; hipGraph capture keeps
+        the fork/join): the bottom MLP forward beside the embedding lookup, each top-layer
+        weight-gradient GEMM (+ fused SGD) beside the next data-gradient GEMM, and the whole
+        bottom-MLP backward beside the embedding backward."""
         cfg = self.cfg
         D = self.D
         Bl = batch.X.shape[0]
@@ -338,11 +358,30 @@ class DLRMTrainer:
         bufs = self._buffers(Bl, B)
         prof = profile or (lambda name: _NullCtx())
         self._prof = prof
-        gemm = self._gemm
         fused_opt = self.grads is None  # single GPU SGD: updates fused into backward
         lr, elr = self.lr, self.emb_lr
+        conc = self.concurrent and profile is None
+        s0 = torch.cuda.current_stream(self.dev)
+        s1 = self._side if conc else s0
 
-        # ---------------- forward: embeddings (full batch, local tables)
+        def fork():
+            if conc:
+                s1.wait_stream(s0)
+
+        def join():
+            if conc:
+                s0.wait_stream(s1)
+
+        c_fwd = conc and "fwd" in self.overlaps
+        c_top = conc and "top" in self.overlaps
+        c_bot = conc and "bot" in self.overlaps
+
+        def side_if(flag):
+            return torch.cuda.stream(s1) if flag else _NullCtx()
+
+        # ---------------- forward: embeddings (full batch, local tables) || bottom MLP
+        if c_fwd:
+            fork()
         with prof("tbe_fwd"):
             if self.T_local > 0:
                 ops.tbe_forward(self.weights, self.row_base, self.T_local, B, batch.indices,
@@ -350,11 +389,13 @@ class DLRMTrainer:
         work = None
         if self.world > 1:
             work = self._alltoall_fwd(bufs, Bl)
-        # ---------------- forward: bottom MLP (overlaps the exchange)
-        h = batch.X
-        for L, out in zip(self.bot, bufs["bot_act"]):
-            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)
-            h = out
+        with side_if(c_fwd):
+            h = batch.X
+            for L, out in zip(self.bot, bufs["bot_act"]):
+                self._gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU, side=c_fwd)
+                h = out
+        if c_fwd:
+            join()
         if work is not None:
             work.wait()
         x, feats = self._features(bufs, Bl)
@@ -363,7 +404,7 @@ class DLRMTrainer:
                                  cfg.arch_interaction_itself, out=bufs["R"])
         h = bufs["R"]
         for L, out in zip(self.top[:-1], bufs["top_act"]):
-            gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)
+            self._gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)
             h = out
         last = self.top[-1]
         hin = h
@@ -374,27 +415,43 @@ class DLRMTrainer:
                                       prob=bufs["prob"], dz=bufs["dz"], loss_out=bufs["loss"],
                                       workspace=self._ws_head(Bl))
         # ---------------- backward: head layer (K -> 1)
-        g_cur, g_nxt = bufs["g"]
+        G = bufs["g"]
+        gi = 0
         dz = bufs["dz"]
-        gview = g_cur[:, :last.Kp]
+        gview = G[gi][:, :last.Kp]
         prev_is_relu = len(self.top) > 1
         with prof("head"):
             ops.outer_drelu(dz, last.W[0, :last.Kp], hin if prev_is_relu else None, prev_is_relu,
                             out=gview)
-        self._bias_and_w_head(last, hin, dz, fused_opt, lr)
+        if c_top:
+            fork()
+        with side_if(c_top):
+            self._bias_and_w_head(last, hin, dz, fused_opt, lr)
         g = gview
-        # top hidden layers, last to first
+        # top hidden layers, last to first: dgrad on the main stream, wgrad beside it.
+        # G rotates over three buffers; the dgrad that overwrites a buffer first waits for
+        # the side-stream wgrad that read it (issued two layers earlier).
+        readers = {}  # buffer index -> event recorded on s1 after its last reader
         for li in range(len(self.top) - 2, -1, -1):
             L = self.top[li]
             inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
-            dinp = g_nxt[:, :L.K]
+            gn = (gi + 1) % 3
+            if c_top and gn in readers:
+                s0.wait_event(readers.pop(gn))
+            dinp = G[gn][:, :L.K]
             if li > 0:
-                gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
+                self._gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
             else:
-                gemm(g[:, :L.N], L.W[:, :L.K], C=dinp)
-            self._wgrad(L, g, inp, fused_opt, lr)
-            g = dinp
-            g_cur, g_nxt = g_nxt, g_cur
+                self._gemm(g[:, :L.N], L.W[:, :L.K], C=dinp)
+            if c_top:
+                fork()  # the weight update may run once W has been read by the dgrad
+            with side_if(c_top):
+                self._wgrad(L, g, inp, fused_opt, lr, side=c_top)
+            if c_top:
+                ev = torch.cuda.Event()
+                ev.record(s1)
+                readers[gi] = ev
+            g, gi = dinp, gn
         # ---------------- backward: interaction -> dR = g
         xg, gfeats = self._features(bufs, Bl, grad=True)
         with prof("interaction_bwd"):
@@ -403,22 +460,28 @@ class DLRMTrainer:
         work = None
         if self.world > 1:
             work = self._alltoall_bwd(bufs, Bl)
-        # ---------------- backward: bottom MLP (overlaps the reverse exchange)
-        xin = bufs["bot_act"][-1][:, :D]
-        with prof("relu_bwd"):
-            g = ops.relu_backward(bufs["dx"], xin, out=bufs["gx"])
-        for li in range(self.n_bot - 1, -1, -1):
-            L = self.bot[li]
-            inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
-            if li > 0:
-                dinp = g_nxt[:, :L.K]
-                gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
-            self._wgrad(L, g, inp, fused_opt, lr)
-            if li > 0:
-                g = dinp
-                g_cur, g_nxt = g_nxt, g_cur
+        # ---------------- backward: bottom MLP on the side stream || embeddings
+        if c_bot:
+            fork()
+        with side_if(c_bot):
+            xin = bufs["bot_act"][-1][:, :D]
+            with prof("relu_bwd"):
+                g = ops.relu_backward(bufs["dx"], xin, out=bufs["gx"])
+            bg = [bufs["gb"][0], bufs["gb"][1]]
+            for li in range(self.n_bot - 1, -1, -1):
+                L = self.bot[li]
+                inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
+                if li > 0:
+                    dinp = bg[li % 2][:, :L.K]
+                    self._gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp,
+                               side=c_bot)
+                self._wgrad(L, g, inp, fused_opt, lr, side=c_bot)
+                if li > 0:
+                    g = dinp
         ar = None
         if self.world > 1:
+            if conc:
+                join()
             ar = self._allreduce_dense()
         # ---------------- backward: embeddings + fused update
         if work is not None:
@@ -430,6 +493,8 @@ class DLRMTrainer:
                                  batch.indices, batch.offsets, bufs["dE"], lr=elr,
                                  eps=cfg.adagrad_eps, momentum=self.momentum,
                                  workspace=self._ws_tbe(batch.indices.numel()))
+        if conc:
+            join()
         if ar is not None:
             ar.wait()
         if not fused_opt:
@@ -446,21 +511,21 @@ class DLRMTrainer:
         return bufs["prob"], bufs["loss"]
 
     # -------------------------------------------------------------- pieces --
-    def _gemm(self, *args, **kw):
+    def _gemm(self, *args, side=False, **kw):
         with self._prof("gemm"):
-            ops.gemm(*args, workspace=self._gemm_ws, **kw)
+            ops.gemm(*args, workspace=self._gemm_ws_side if side else self._gemm_ws, **kw)
 
     def _colsum(self, *args, **kw):
         with self._prof("colsum"):
             ops.colsum(*args, **kw)
 
-    def _wgrad(self, L: _Layer, g, inp, fused_opt, lr):
+    def _wgrad(self, L: _Layer, g, inp, fused_opt, lr, side=False):
         """[dW | db] = g^T [inp | 1] in one GEMM (bias folded); fused SGD on one GPU."""
         if fused_opt:
             self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.W, alpha=lr,
-                       epilogue=ops.EPI_SGD)
+                       epilogue=ops.EPI_SGD, side=side)
         else:
-            self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.gW)
+            self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.gW, side=side)
 
     def _bias_and_w_head(self, last: _Layer, hin, dz, fused_opt, lr):
         """Head layer (K -> 1): [dw | db] = sum_m dz[m] [hin[m] | 1] as one column sum."""

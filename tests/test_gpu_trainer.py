@@ -132,3 +132,44 @@ def test_synthetic_batch_and_determinism():
     # the whole step is bitwise reproducible (sorted embedding backward, no float atomics)
     for a, b2 in zip(outs[0], outs[1]):
         assert torch.equal(a, b2)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_side_stream_schedule_matches_serial(graph):
+    """The two-stream schedule (bottom MLP || lookup, wgrad || next dgrad, bottom backward ||
+    embedding backward), eager and captured in a hipGraph, gives bitwise the serial result."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES["c3_small"]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function="bce",
+                        learning_rate=0.1)
+    res = []
+    for conc in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.concurrent = conc
+        tr.overlaps = {"fwd", "top", "bot"}
+        batches = [tr.synthetic_batch(512, 1, seed=s) for s in range(3)]
+        if graph and conc:
+            tr.step(batches[0])  # allocate buffers outside capture
+            torch.cuda.synchronize()
+            gs = []
+            for b in batches[1:]:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    tr.step(b)
+                gs.append(g)
+            for g in gs:
+                g.replay()
+            for g in gs:
+                g.replay()
+        else:
+            tr.step(batches[0])
+            for _ in range(2):
+                for b in batches[1:]:
+                    tr.step(b)
+        torch.cuda.synchronize()
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
+                    tr._bufs[(512, 512)]["prob"].cpu().clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
