@@ -103,6 +103,131 @@ __global__ __launch_bounds__(256) void head_rows_kernel(int64_t M, int64_t K,
   }
 }
 
+// ---------------------------------------------------------------- fused head --
+// Per-row loss math shared by the head kernels: returns (prob, dz, row loss).
+__device__ __forceinline__ void head_row_math(float z, float t, int loss_kind, float lo,
+                                              float gscale, float invM, float& pc, float& dzv,
+                                              float& l) {
+  const float p = 1.f / (1.f + expf(-z));
+  pc = p;
+  bool pass = true;
+  if (lo > 0.f && lo < 0.5f) {
+    const float hi = 1.f - lo;
+    pass = (p >= lo) && (p <= hi);
+    pc = fminf(fmaxf(p, lo), hi);
+  }
+  float dp;
+  if (loss_kind == DLRM_LOSS_BCE) {
+    const float lp = fmaxf(logf(pc), -100.f);
+    const float l1p = fmaxf(logf(1.f - pc), -100.f);
+    l = -(t * lp + (1.f - t) * l1p);
+    dp = (pc - t) / fmaxf((1.f - pc) * pc, 1e-12f) * invM;
+  } else {
+    const float d = pc - t;
+    l = d * d;
+    dp = 2.f * d * invM;
+  }
+  dp *= gscale;
+  if (!pass) dp = 0.f;
+  dzv = dp * (1.f - p) * p;
+}
+
+constexpr int kHeadRows = 4;  // rows per workgroup (one per wave)
+constexpr int kHeadMaxK = 2048;
+
+// One pass over the rows of the last layer's input X [M, K] (K includes the folded bias
+// column): z = X w, sigmoid, loss term, dz, the ReLU-masked input gradient
+// dX = dz w^T (.) (X > 0), and this workgroup's column partial sum of dz X (the weight
+// gradient) in fixed row order.
+template <int NC>
+__global__ __launch_bounds__(256) void head_fused_rows_kernel(
+    int64_t M, int64_t K, const float* __restrict__ X, int64_t ldx, const float* __restrict__ w,
+    const float* __restrict__ target, int loss_kind, float lo, float gscale,
+    float* __restrict__ prob, float* __restrict__ dz, float* __restrict__ row_loss,
+    float* __restrict__ dX, int64_t lddx, int mask, float* __restrict__ part) {
+  __shared__ float red[4][NC * 64];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const float invM = 1.f / (float)M;
+  float wr[NC], cp[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int64_t k = lane + 64 * c;
+    wr[c] = k < K ? w[k] : 0.f;
+    cp[c] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * kHeadRows + wave * (kHeadRows / 4);
+  for (int q = 0; q < kHeadRows / 4; ++q) {
+    const int64_t m = r0 + q;
+    if (m >= M) break;
+    const float* xr = X + m * ldx;
+    float xv[NC];
+    float sacc = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int64_t k = lane + 64 * c;
+      xv[c] = k < K ? xr[k] : 0.f;
+      sacc = fmaf(xv[c], wr[c], sacc);
+    }
+    sacc = wave_sum(sacc);
+    float pc = 0.f, dzv = 0.f, l = 0.f;
+    if (lane == 0) {
+      head_row_math(sacc, target ? target[m] : 0.f, loss_kind, lo, gscale, invM, pc, dzv, l);
+      if (prob) prob[m] = pc;
+      if (dz) dz[m] = dzv;
+      row_loss[m] = l;
+    }
+    dzv = __shfl(dzv, 0, 64);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int64_t k = lane + 64 * c;
+      if (k < K) {
+        float g = dzv * wr[c];
+        if (mask && !(xv[c] > 0.f)) g = 0.f;
+        if (dX) dX[m * lddx + k] = g;
+      }
+      cp[c] = fmaf(dzv, xv[c], cp[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) red[wave][lane + 64 * c] = cp[c];
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += 256)
+    part[(int64_t)blockIdx.x * K + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+}
+
+// Column sums of the row-block partials -> weight gradient (stored, accumulated, or
+// applied as SGD to w); one wave per column: lane l sums blocks l, l+64, ... in order,
+// then a fixed xor-tree across lanes (deterministic).  The last workgroup also reduces the
+// per-row loss terms the same way.
+__global__ __launch_bounds__(256) void head_finalize_kernel(int64_t M, int64_t K, int64_t nblk,
+                                                            const float* __restrict__ part,
+                                                            float* __restrict__ w, float lr,
+                                                            float* __restrict__ dw, int accumulate,
+                                                            const float* __restrict__ row_loss,
+                                                            float* __restrict__ loss_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k < K) {
+    float s = 0.f;
+    for (int64_t b = lane; b < nblk; b += 64) s += part[b * K + k];
+    s = wave_sum(s);
+    if (lane == 0) {
+      if (dw) dw[k] = accumulate ? dw[k] + s : s;
+      else if (lr != 0.f) w[k] = fmaf(-lr, s, w[k]);
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && loss_out) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < M; i += 256) s += row_loss[i];
+    s = wave_sum(s);
+    if (lane == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) loss_out[0] = ((red[0] + red[1]) + red[2] + red[3]) / (float)M;
+  }
+}
+
 __global__ __launch_bounds__(256) void mean_kernel(int64_t M, const float* __restrict__ v,
                                                    float* __restrict__ out) {
   __shared__ float red[256];
@@ -393,5 +518,46 @@ extern "C" int dlrm_relu_backward(int64_t M, int64_t K, const float* dy, int64_t
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_stride_blocks(M * K)), dim3(256), 0,
                      dlrm::as_stream(stream), M, K, dy, lddy, y, ldy, dx, lddx);
   DLRM_LAUNCH_CHECK("dlrm_relu_backward");
+  return DLRM_OK;
+}
+
+extern "C" size_t dlrm_head_step_workspace_size(int64_t M, int64_t K) {
+  const int64_t nblk = dlrm::ceil_div(M > 0 ? M : 1, kHeadRows);
+  return (size_t)(M > 0 ? M : 1) * sizeof(float) + 256 +
+         (size_t)nblk * (K > 0 ? K : 1) * sizeof(float) + 256;
+}
+
+extern "C" int dlrm_head_step(int64_t M, int64_t K, const float* X, int64_t ldx, float* w,
+                              const float* target, int32_t loss_kind, float clamp_lo,
+                              float grad_scale, float* prob_out, float* dz_out, float* loss_out,
+                              float* dX, int64_t lddx, int32_t relu_mask, float* dw_out,
+                              int32_t accumulate, float lr, void* workspace,
+                              size_t workspace_bytes, dlrm_stream_t stream) {
+  const char* name = "dlrm_head_step";
+  DLRM_ARG(M > 0 && K > 0, "%s: bad sizes", name);
+  DLRM_ARG(X && w && ldx >= K && target, "%s: null X/w/target", name);
+  DLRM_ARG(loss_kind == DLRM_LOSS_MSE || loss_kind == DLRM_LOSS_BCE, "%s: bad loss", name);
+  DLRM_ARG(!dX || lddx >= K, "%s: bad lddx", name);
+  DLRM_REQUIRE(K <= kHeadMaxK, DLRM_ERR_UNSUPPORTED, "%s: K > %d", name, kHeadMaxK);
+  DLRM_ARG(workspace, "%s: null workspace", name);
+  DLRM_REQUIRE(workspace_bytes >= dlrm_head_step_workspace_size(M, K), DLRM_ERR_WORKSPACE,
+               "%s: workspace too small", name);
+  WsCarver wc(workspace);
+  float* row_loss = wc.take<float>(M);
+  const int64_t nblk = dlrm::ceil_div(M, kHeadRows);
+  float* part = wc.take<float>(nblk * K);
+  hipStream_t st = dlrm::as_stream(stream);
+  const int nc = (int)dlrm::ceil_div(K, 64);
+#define HR(NC_)                                                                               \
+  hipLaunchKernelGGL(head_fused_rows_kernel<NC_>, dim3(nblk), dim3(256), 0, st, M, K, X, ldx, w, \
+                     target, loss_kind, clamp_lo, grad_scale, prob_out, dz_out, row_loss, dX,  \
+                     lddx, relu_mask, part)
+  if (nc <= 2) HR(2); else if (nc <= 4) HR(4); else if (nc <= 5) HR(5); else if (nc <= 8) HR(8);
+  else if (nc <= 12) HR(12); else if (nc <= 17) HR(17); else if (nc <= 24) HR(24); else HR(32);
+#undef HR
+  DLRM_LAUNCH_CHECK(name);
+  hipLaunchKernelGGL(head_finalize_kernel, dim3(dlrm::ceil_div(K, 4)), dim3(256), 0, st, M, K,
+                     nblk, part, w, lr, dw_out, accumulate, row_loss, loss_out);
+  DLRM_LAUNCH_CHECK(name);
   return DLRM_OK;
 }

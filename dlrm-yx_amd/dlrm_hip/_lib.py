@@ -63,6 +63,10 @@ SIGNATURES = {
     "dlrm_head_workspace_size": (c_size_t, [c_int64]),
     "dlrm_head_forward_backward": (c_int32, [c_int64, c_int64, P, c_int64, P, P, P, c_int32,
                                              c_float, c_float, P, P, P, P, c_size_t, P]),
+    "dlrm_head_step_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "dlrm_head_step": (c_int32, [c_int64, c_int64, P, c_int64, P, P, c_int32, c_float, c_float,
+                                 P, P, P, P, c_int64, c_int32, P, c_int32, c_float, P, c_size_t,
+                                 P]),
     "dlrm_outer_drelu": (c_int32, [c_int64, c_int64, P, P, P, c_int64, c_int32, P, c_int64, P]),
     "dlrm_sgd_update": (c_int32, [P, P, c_int64, c_float, P]),
     "dlrm_adagrad_update": (c_int32, [P, P, P, c_int64, c_float, c_float, P]),

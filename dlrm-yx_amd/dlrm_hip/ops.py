@@ -304,6 +304,27 @@ def head_forward_backward(X: torch.Tensor, w: torch.Tensor, b: Optional[torch.Te
     return prob, dz, loss_out
 
 
+def head_step(X: torch.Tensor, w: torch.Tensor, target: torch.Tensor, loss: str = "mse",
+              clamp_lo: float = 0.0, grad_scale: float = 1.0,
+              prob: Optional[torch.Tensor] = None, dz: Optional[torch.Tensor] = None,
+              loss_out: Optional[torch.Tensor] = None, dX: Optional[torch.Tensor] = None,
+              relu_mask: bool = True, dw: Optional[torch.Tensor] = None, accumulate: bool = False,
+              lr: float = 0.0, workspace: Optional[torch.Tensor] = None):
+    """Fused head (dlrm_head_step): X [M, K] with the folded bias column, w [K] (updated in
+    place by SGD when lr != 0 and dw is None)."""
+    M, K = X.shape
+    need = _lib.query("dlrm_head_step_workspace_size", M, K)
+    if workspace is None or workspace.numel() < need:
+        workspace = _ws("head_step", need, X.device)
+    _check_cuda(X, w, target)
+    _lib.call("dlrm_head_step", M, K, _p(X), X.stride(0), _p(w), _p(target),
+              LOSS_BCE if loss == "bce" else LOSS_MSE, float(clamp_lo), float(grad_scale),
+              _p(prob), _p(dz), _p(loss_out), _p(dX), dX.stride(0) if dX is not None else 0,
+              int(relu_mask), _p(dw), int(accumulate), float(lr), _p(workspace),
+              workspace.numel(), _stream(X.device))
+    return prob, dz, loss_out
+
+
 def outer_drelu(dz: torch.Tensor, w: torch.Tensor, X: Optional[torch.Tensor], relu_mask: bool,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     M = dz.shape[0]

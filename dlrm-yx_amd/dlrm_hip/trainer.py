@@ -408,25 +408,19 @@ class DLRMTrainer:
             h = out
         last = self.top[-1]
         hin = h
-        with prof("head"):
-            # bias folded: [hin | 1] . [w | b]
-            ops.head_forward_backward(hin, last.W[0, :last.Kp], None, batch.target,
-                                      cfg.loss_function, cfg.loss_threshold, 1.0,
-                                      prob=bufs["prob"], dz=bufs["dz"], loss_out=bufs["loss"],
-                                      workspace=self._ws_head(Bl))
-        # ---------------- backward: head layer (K -> 1)
+        # ---------------- head: last layer + sigmoid + loss + dz + input grad + [dw | db]
+        # (bias folded: [hin | 1] . [w | b]) in two launches; the weight update (fused SGD on
+        # one GPU) follows every read of the weights
         G = bufs["g"]
         gi = 0
-        dz = bufs["dz"]
         gview = G[gi][:, :last.Kp]
         prev_is_relu = len(self.top) > 1
         with prof("head"):
-            ops.outer_drelu(dz, last.W[0, :last.Kp], hin if prev_is_relu else None, prev_is_relu,
-                            out=gview)
-        if c_top:
-            fork()
-        with side_if(c_top):
-            self._bias_and_w_head(last, hin, dz, fused_opt, lr)
+            ops.head_step(hin[:, :last.Kp], last.W[0, :last.Kp], batch.target, cfg.loss_function,
+                          cfg.loss_threshold, 1.0, prob=bufs["prob"], dz=bufs["dz"],
+                          loss_out=bufs["loss"], dX=gview, relu_mask=prev_is_relu,
+                          dw=None if fused_opt else last.gW[0, :last.Kp],
+                          lr=lr if fused_opt else 0.0, workspace=self._ws_head_step(Bl, last.Kp))
         g = gview
         # top hidden layers, last to first: dgrad on the main stream, wgrad beside it.
         # G rotates over three buffers; the dgrad that overwrites a buffer first waits for
@@ -548,6 +542,12 @@ class DLRMTrainer:
         if self._colsum_ws is None or self._colsum_ws.numel() < need:
             self._colsum_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
         return self._colsum_ws
+
+    def _ws_head_step(self, M: int, K: int) -> torch.Tensor:
+        need = int(ops._lib.query("dlrm_head_step_workspace_size", M, K))
+        if getattr(self, "_head_step_ws", None) is None or self._head_step_ws.numel() < need:
+            self._head_step_ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        return self._head_step_ws
 
     def _ws_head(self, M: int) -> torch.Tensor:
         need = int(ops._lib.query("dlrm_head_workspace_size", M))

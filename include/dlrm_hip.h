@@ -247,6 +247,25 @@ int dlrm_head_forward_backward(int64_t M, int64_t K, const float* X, int64_t ldx
                                float* prob_out, float* dz_out, float* loss_out, void* workspace,
                                size_t workspace_bytes, dlrm_stream_t stream);
 
+/* Workspace for dlrm_head_step. */
+size_t dlrm_head_step_workspace_size(int64_t M, int64_t K);
+/*
+ * The whole head of the training step in two launches (bias folded: X carries a
+ * constant-1 column and w[K] includes the bias):
+ *   z = X w, p = sigmoid(z), loss and dz exactly as dlrm_head_forward_backward;
+ *   dX[m][k] = dz[m] * w[k] * (relu_mask ? X[m][k] > 0 : 1)      (if dX != NULL)
+ *   s[k] = sum_m dz[m] X[m][k]  (fixed order: 16-row blocks, then blocks in order)
+ *   dw_out != NULL: dw_out = s (or += s when accumulate); else if lr != 0: w -= lr * s
+ *   (w is updated after every read of it, so dX uses the pre-update weights).
+ * K <= 2048.  Replaces head_forward_backward + outer_drelu + colsum for the DLRM head
+ * (dlrm_s_pytorch.py:170-178, 504-516, the last Linear of create_mlp).
+ */
+int dlrm_head_step(int64_t M, int64_t K, const float* X, int64_t ldx, float* w,
+                   const float* target, int32_t loss_kind, float clamp_lo, float grad_scale,
+                   float* prob_out, float* dz_out, float* loss_out, float* dX, int64_t lddx,
+                   int32_t relu_mask, float* dw_out, int32_t accumulate, float lr,
+                   void* workspace, size_t workspace_bytes, dlrm_stream_t stream);
+
 /* Elementwise: dX[m][k] = dz[m] * w[k] * (relu_mask ? (X[m][k] > 0) : 1). */
 int dlrm_outer_drelu(int64_t M, int64_t K, const float* dz, const float* w, const float* X,
                      int64_t ldx, int32_t relu_mask, float* dX, int64_t lddx,

@@ -311,6 +311,46 @@ def test_colsum_head_outer(ops):
     assert ok, msg
 
 
+@pytest.mark.parametrize("loss,clamp", [("mse", 0.0), ("bce", 0.0), ("bce", 0.2)])
+@pytest.mark.parametrize("M,K", [(2048, 260), (37, 13), (100, 700)])
+def test_head_step_fused(ops, loss, clamp, M, K):
+    """dlrm_head_step (bias folded into X's last column) vs torch autograd: prob, loss, dz,
+    the ReLU-masked input gradient, and the weight gradient (stored and as fused SGD)."""
+    torch.manual_seed(M + K)
+    X = torch.randn(M, K).relu()
+    X[:, K - 1] = 1.0  # folded bias column
+    w = torch.randn(K) * 0.1
+    t = torch.rand(M).round() if loss == "bce" else torch.rand(M)
+    Xr = X.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    z = Xr @ wr
+    z.retain_grad()
+    p = torch.sigmoid(z)
+    pc = p.clamp(clamp, 1 - clamp) if clamp > 0 else p
+    fn = torch.nn.MSELoss() if loss == "mse" else torch.nn.BCELoss()
+    E = fn(pc, t)
+    E.backward()
+    Xd, wd, td = X.to(dev), w.to(dev), t.to(dev)
+    prob, dz, L = (torch.empty(M, device=dev), torch.empty(M, device=dev),
+                   torch.empty(1, device=dev))
+    dX = torch.full((M, K + 3), 7.0, device=dev)
+    dw = torch.empty(K, device=dev)
+    ops.head_step(Xd, wd, td, loss, clamp, 1.0, prob=prob, dz=dz, loss_out=L, dX=dX[:, :K],
+                  relu_mask=True, dw=dw)
+    for got, ref in ((prob, pc.detach()), (L, E.detach().reshape(1)), (dz, z.grad),
+                     (dw, wr.grad)):
+        ok, msg = fp32_close(got.cpu().numpy(), ref.numpy())
+        assert ok, msg
+    ref_dx = dz.cpu()[:, None] * w[None, :] * (X > 0)
+    ok, msg = fp32_close(dX[:, :K].cpu().numpy(), ref_dx.numpy())
+    assert ok, msg
+    assert torch.all(dX[:, K:] == 7.0)
+    w2 = w.to(dev)
+    ops.head_step(Xd, w2, td, loss, clamp, 1.0, dX=None, lr=0.5)
+    ok, msg = fp32_close(w2.cpu().numpy(), (w - 0.5 * wr.grad).numpy())
+    assert ok, msg
+
+
 def test_dense_optimizers(ops):
     torch.manual_seed(5)
     p, g = torch.randn(1000), torch.randn(1000)
