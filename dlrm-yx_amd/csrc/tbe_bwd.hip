@@ -26,7 +26,7 @@
 
 namespace {
 
-constexpr int CH = 64;  // sorted lookups per block
+constexpr int CH = 16;  // sorted lookups per block (all gradient rows of a block in flight)
 
 // ---------------------------------------------------------------- backward --
 // Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags).
@@ -60,6 +60,75 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
   keys[p] = key;
   pos[p] = (int32_t)p;
   bag_of[p] = bag;
+}
+
+// Per-table sort (replaces keys + global radix sort when every table's lookups fit in
+// LDS): workgroup t builds the (row, position) keys of table t's lookups, bitonic-sorts
+// them in LDS as one 64-bit composite (row << 32 | position: unique, so the result equals
+// a stable sort) and writes the sorted rows / positions into the table's own range of
+// the output.  Tables own disjoint row ranges and occupy consecutive lookup ranges, so
+// the concatenation is a valid grouping for the block kernel.  Workgroup T marks the
+// lookups outside all bags (before off[0] / after off[T*B]) as sentinels.
+constexpr int kSegCap = 4096;
+template <typename IdxT, typename OffT>
+__global__ __launch_bounds__(512) void tbe_bwd_segsort_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
+    int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
+    int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of) {
+  __shared__ uint64_t kv[kSegCap];
+  const int t = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (t == T) {  // lookups outside every bag
+    const int64_t a = (int64_t)off[0], e = (int64_t)off[(int64_t)T * B];
+    for (int64_t p = tid; p < N; p += blockDim.x) {
+      if (p >= a && p < e) continue;
+      keys_out[p] = sentinel;
+      pos_out[p] = (int32_t)p;
+      bag_of[p] = -1;
+    }
+    return;
+  }
+  const int64_t s0 = (int64_t)off[(int64_t)t * B];
+  const int n = (int)((int64_t)off[(int64_t)(t + 1) * B] - s0);  // <= kSegCap (contract)
+  const int64_t rb = row_base[t];
+  const int64_t nrows = row_base[t + 1] - rb;
+  for (int b = tid; b < B; b += blockDim.x) {
+    const int64_t a = (int64_t)off[(int64_t)t * B + b], e = (int64_t)off[(int64_t)t * B + b + 1];
+    for (int64_t p = a; p < e; ++p) bag_of[p] = t * B + b;
+  }
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int i = tid; i < np2; i += blockDim.x) {
+    uint64_t v = ~0ull;
+    if (i < n) {
+      const int64_t p = s0 + i;
+      const int64_t r = (int64_t)idx[p];
+      const uint32_t key = (r >= 0 && r < nrows) ? (uint32_t)(rb + r) : sentinel;
+      v = ((uint64_t)key << 32) | (uint32_t)p;
+    }
+    kv[i] = v;
+  }
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np2; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = kv[i], b = kv[ixj];
+          if ((a > b) == ((i & k) == 0)) {
+            kv[i] = b;
+            kv[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < n; i += blockDim.x) {
+    const uint64_t v = kv[i];
+    keys_out[s0 + i] = (uint32_t)(v >> 32);
+    pos_out[s0 + i] = (int32_t)(v & 0xffffffffu);
+  }
 }
 
 enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2 };
@@ -187,12 +256,13 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
         }
         if (psw) my_w = psw[p];
       }
-      for (int j = 0; j < n; j += 4) {
-        KeyT ku[4];
-        int64_t ou[4];
-        float wu[4];
+      constexpr int U = LPB < CH ? LPB : CH;  // gradient rows in flight per group
+      for (int j = 0; j < n; j += U) {
+        KeyT ku[U];
+        int64_t ou[U];
+        float wu[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int src = g * LPB + ((j + u) < LPB ? (j + u) : 0);
           if constexpr (sizeof(KeyT) == 8)
             ku[u] = (KeyT)__shfl((long long)my_key, src, kWave);
@@ -202,9 +272,9 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
           wu[u] = __shfl(my_w, src, kWave);
           if (j + u >= n) ou[u] = -1;
         }
-        V gv[4][MAXV];
+        V gv[U][MAXV];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
           for (int c = 0; c < MAXV; ++c) {
             const int chunk = gl + c * LPB;
@@ -217,7 +287,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           if (j + u < n) {
             if (!have || ku[u] != cur) {
               if (have) flush(base + j + u);
@@ -270,6 +340,25 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
     }
     const bool starts = (a > i0) || (i0 == 0) || (keys[i0 - 1] != last);
     if (!starts) continue;  // the block where the run starts combines it
+    // Last block of the run: the run is contiguous, so "block kk continues it" (its first
+    // key equals `last`) holds for kk = k+1 .. kend and fails after.  The group's lanes
+    // probe LPB blocks per round in parallel instead of walking them one by one.
+    int64_t kend = k + 1;  // blocks k+1 .. kend-1 ... resolved below (kend = last one)
+    {
+      int64_t base = k + 1;
+      while (true) {
+        const int64_t kk = base + gl;
+        const bool cont = kk < nblocks && keys[kk * CH] == last;
+        // groups are LPB-aligned lane ranges: find the first lane (in order) that fails
+        uint64_t fail = __ballot(!cont);
+        if constexpr (LPB < 64) fail = (fail >> ((lane / LPB) * LPB)) & ((1ull << LPB) - 1);
+        if (fail) {
+          kend = base + __builtin_ctzll(fail) - 1;
+          break;
+        }
+        base += LPB;
+      }
+    }
     V acc[MAXV];
     const V* src = reinterpret_cast<const V*>(partial + (2 * k + (a == i0 ? 0 : 1)) * D);
 #pragma unroll
@@ -279,13 +368,27 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
       else
         vzero(acc[c]);
     }
-    for (int64_t kk = k + 1; kk < nblocks; ++kk) {
-      const V* s2 = reinterpret_cast<const V*>(partial + (2 * kk) * D);
+    // partials of blocks k+1 .. kend in block order, 8 loads in flight
+    for (int64_t kk0 = k + 1; kk0 <= kend; kk0 += 8) {
+      V pv[8][MAXV];
 #pragma unroll
-      for (int c = 0; c < MAXV; ++c)
-        if (gl + c * LPB < nchunks) vadd(acc[c], s2[gl + c * LPB]);
-      const int64_t e = (kk + 1) * CH;
-      if (e >= N || keys[e] != last) break;
+      for (int u = 0; u < 8; ++u) {
+        const int64_t kk = kk0 + u;
+        const V* s2 = reinterpret_cast<const V*>(partial + (2 * kk) * D);
+#pragma unroll
+        for (int c = 0; c < MAXV; ++c) {
+          if (kk <= kend && gl + c * LPB < nchunks)
+            pv[u][c] = s2[gl + c * LPB];
+          else
+            vzero(pv[u][c]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (kk0 + u <= kend) {
+#pragma unroll
+          for (int c = 0; c < MAXV; ++c) vadd(acc[c], pv[u][c]);
+        }
     }
     finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)last, acc, gl, nchunks, lr, eps);
   }
@@ -337,22 +440,30 @@ template <typename KeyT, typename IdxT, typename OffT>
 int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
                const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
                const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
-               hipStream_t st, const char* name) {
+               int64_t max_seg, hipStream_t st, const char* name) {
   if (N == 0) return DLRM_OK;
   const KeyT sentinel = (KeyT)total_rows;
   const int end_bit = bit_width_u64((uint64_t)total_rows);
   BwdWs<KeyT> w = carve_bwd_ws<KeyT>(ws, N, D, end_bit);
   DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
                name, ws_bytes, w.total);
-  hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(dlrm::ceil_div(N, 256)),
-                     dim3(256), 0, st, static_cast<const IdxT*>(idx),
-                     static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_in,
-                     w.pos_in, w.bag_of);
-  DLRM_LAUNCH_CHECK(name);
-  size_t tb = w.temp_bytes;
-  DLRM_HIP_CALL(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in,
-                                                   w.pos_out, (int)N, 0, end_bit, st),
-                name);
+  if (sizeof(KeyT) == 4 && max_seg > 0 && max_seg <= kSegCap && N < (int64_t)0x7fffffff) {
+    hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(512), 0, st,
+                       static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base, T,
+                       B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),
+                       w.pos_out, w.bag_of);
+    DLRM_LAUNCH_CHECK(name);
+  } else {
+    hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(dlrm::ceil_div(N, 256)),
+                       dim3(256), 0, st, static_cast<const IdxT*>(idx),
+                       static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_in,
+                       w.pos_in, w.bag_of);
+    DLRM_LAUNCH_CHECK(name);
+    size_t tb = w.temp_bytes;
+    DLRM_HIP_CALL(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in,
+                                                     w.pos_out, (int)N, 0, end_bit, st),
+                  name);
+  }
 
   const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
                     ((reinterpret_cast<uintptr_t>(gout) & 15) == 0) && (gbs % 4 == 0);
@@ -412,7 +523,8 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
 int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T,
                  int B, const void* idx, int ib, const void* off, int ob, int64_t N,
                  int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
-                 float eps, void* ws, size_t ws_bytes, dlrm_stream_t stream, const char* name) {
+                 float eps, void* ws, size_t ws_bytes, int64_t max_seg, dlrm_stream_t stream,
+                 const char* name) {
   DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
@@ -425,7 +537,7 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
   const bool k32 = (uint64_t)total_rows < 0xFFFFFFFFull;
 #define BWD(K, I, O)                                                                     \
   return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
-                             gout, gbs, lr, eps, ws, ws_bytes, st, name)
+                             gout, gbs, lr, eps, ws, ws_bytes, max_seg, st, name)
   if (k32) {
     if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
     if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
@@ -458,25 +570,25 @@ extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* r
                                      int32_t offset_bits, int64_t num_lookups,
                                      int64_t total_rows, const float* per_sample_weights,
                                      const float* grad_out, int64_t grad_batch_stride, float lr,
-                                     void* workspace, size_t workspace_bytes,
-                                     dlrm_stream_t stream) {
+                                     int64_t max_lookups_per_table, void* workspace,
+                                     size_t workspace_bytes, dlrm_stream_t stream) {
   return bwd_dispatch(MODE_SGD, weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
-                      grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes, stream,
-                      "dlrm_tbe_backward_sgd");
+                      grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes,
+                      max_lookups_per_table, stream, "dlrm_tbe_backward_sgd");
 }
 
 extern "C" int dlrm_tbe_backward_rowwise_adagrad(
     float* weights, float* momentum, int64_t D, const int64_t* row_base, int32_t T, int32_t B,
     const void* indices, int32_t index_bits, const void* offsets, int32_t offset_bits,
     int64_t num_lookups, int64_t total_rows, const float* per_sample_weights,
-    const float* grad_out, int64_t grad_batch_stride, float lr, float eps, void* workspace,
-    size_t workspace_bytes, dlrm_stream_t stream) {
+    const float* grad_out, int64_t grad_batch_stride, float lr, float eps,
+    int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes, dlrm_stream_t stream) {
   DLRM_ARG(momentum, "dlrm_tbe_backward_rowwise_adagrad: null momentum");
   return bwd_dispatch(MODE_ADAGRAD, weights, momentum, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
-                      grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes, stream,
-                      "dlrm_tbe_backward_rowwise_adagrad");
+                      grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes,
+                      max_lookups_per_table, stream, "dlrm_tbe_backward_rowwise_adagrad");
 }
 
 extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_base,
@@ -485,10 +597,10 @@ extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int
                                        int32_t offset_bits, int64_t num_lookups,
                                        int64_t total_rows, const float* per_sample_weights,
                                        const float* grad_out, int64_t grad_batch_stride,
-                                       void* workspace, size_t workspace_bytes,
-                                       dlrm_stream_t stream) {
+                                       int64_t max_lookups_per_table, void* workspace,
+                                       size_t workspace_bytes, dlrm_stream_t stream) {
   return bwd_dispatch(MODE_DENSE, grad_weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
-                      grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes, stream,
-                      "dlrm_tbe_backward_dense");
+                      grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes,
+                      max_lookups_per_table, stream, "dlrm_tbe_backward_dense");
 }

@@ -142,10 +142,11 @@ class EmbeddingBagsFunction(torch.autograd.Function):
         if m.grad_mode == "fused":
             m.fused_update(indices, offsets, g, psw, B)
             return (None, None, None, None, None, *nones)
+        mx = max(ctx.counts) if ctx.counts else 0
         if m.grad_mode == "dense":
             gw = torch.zeros_like(m.weight_flat)
             ops.tbe_backward("dense", gw, m.row_base, m.T, B, indices, offsets, g,
-                             per_sample_weights=psw)
+                             per_sample_weights=psw, max_lookups_per_table=mx)
             grads = [gw[a:b] for a, b in m.row_ranges]
             return (None, None, None, None, None, *grads)
         # sparse COO per table

@@ -92,9 +92,12 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
                  lr: float = 0.0, eps: float = 0.0, momentum: Optional[torch.Tensor] = None,
                  per_sample_weights: Optional[torch.Tensor] = None,
                  grad_batch_stride: Optional[int] = None,
-                 workspace: Optional[torch.Tensor] = None) -> None:
+                 workspace: Optional[torch.Tensor] = None,
+                 max_lookups_per_table: int = 0) -> None:
     """mode: 'sgd' (fused exact SGD), 'rowwise_adagrad' (fused RWSAdagrad) or
-    'dense' (weights is a gradient buffer to accumulate into)."""
+    'dense' (weights is a gradient buffer to accumulate into).  max_lookups_per_table:
+    upper bound on any table's lookups (0 = unknown); <= 4096 selects the per-table LDS
+    sort (bitwise the same result as the device-wide radix sort)."""
     _check_cuda(weights, row_base, indices, offsets, grad_out, momentum, per_sample_weights)
     D = weights.shape[1]
     N = indices.numel()
@@ -108,14 +111,15 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
                    _bits(offsets), N, total_rows, _p(per_sample_weights), _p(grad_out),
                    grad_batch_stride)
     st = _stream(weights.device)
+    mx = int(max_lookups_per_table)
     if mode == "sgd":
-        _lib.call("dlrm_tbe_backward_sgd", _p(weights), *args_common, lr, _p(workspace),
+        _lib.call("dlrm_tbe_backward_sgd", _p(weights), *args_common, lr, mx, _p(workspace),
                   workspace.numel(), st)
     elif mode == "rowwise_adagrad":
         _lib.call("dlrm_tbe_backward_rowwise_adagrad", _p(weights), _p(momentum), *args_common,
-                  lr, eps, _p(workspace), workspace.numel(), st)
+                  lr, eps, mx, _p(workspace), workspace.numel(), st)
     elif mode == "dense":
-        _lib.call("dlrm_tbe_backward_dense", _p(weights), *args_common, _p(workspace),
+        _lib.call("dlrm_tbe_backward_dense", _p(weights), *args_common, mx, _p(workspace),
                   workspace.numel(), st)
     else:
         raise ValueError(mode)

@@ -63,6 +63,7 @@ class Batch:
     offsets: torch.Tensor  # [T_local*B + 1] int32 CSR of the local tables, full batch
     indices: torch.Tensor  # int32 table-local rows
     target: torch.Tensor   # [B_local] fp32
+    max_per_table: int = 0  # upper bound on one table's lookups (0 = unknown)
 
 
 @dataclass
@@ -258,7 +259,8 @@ class DLRMTrainer:
         offsets = torch.cat(offs + [torch.tensor([start])]).to(torch.int32).to(self.dev)
         indices = torch.cat(idxs).to(torch.int32).to(self.dev)
         tg = torch.as_tensor(target).reshape(-1)[sl].to(torch.float32).to(self.dev)
-        return Batch(Xp, offsets, indices, tg)
+        mx = max([int(i.numel()) for i in idxs], default=0)
+        return Batch(Xp, offsets, indices, tg, mx)
 
     def synthetic_batch(self, B: int, L: int, seed: int) -> Batch:
         """Device-generated synthetic batch of the reference's shape: X ~ log(1+U[0,1))
@@ -280,7 +282,7 @@ class DLRMTrainer:
         tg = torch.rand(Bl, generator=g, device=self.dev)
         if self.cfg.loss_function == "bce":
             tg = tg.round()
-        return Batch(Xp, offsets, indices, tg)
+        return Batch(Xp, offsets, indices, tg, B * L)
 
     # ------------------------------------------------------------- buffers --
     def _buffers(self, Bl: int, B: int):
@@ -486,7 +488,8 @@ class DLRMTrainer:
                 ops.tbe_backward(mode, self.weights, self.row_base, self.T_local, B,
                                  batch.indices, batch.offsets, bufs["dE"], lr=elr,
                                  eps=cfg.adagrad_eps, momentum=self.momentum,
-                                 workspace=self._ws_tbe(batch.indices.numel()))
+                                 workspace=self._ws_tbe(batch.indices.numel()),
+                                 max_lookups_per_table=batch.max_per_table)
         if conc:
             join()
         if ar is not None:

@@ -107,17 +107,23 @@ size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows,
 /*
  * Exact-SGD backward fused with the update: for every lookup l of bag (t,b),
  *   W[row_base[t]+indices[l]] -= lr * w_l * grad_out[b*grad_batch_stride + t*D + :]
- * Duplicate rows are combined deterministically: lookups are radix-sorted by
- * global row (stable), the gradient of each unique row is summed in sorted order
- * (long runs in fixed 64-lookup blocks whose partials are added in block order),
- * and the row is read once and written once.  num_lookups = length of indices.
+ * Duplicate rows are combined deterministically: lookups are sorted by (global row,
+ * position), the gradient of each unique row is summed in sorted order (long runs in
+ * fixed 16-lookup blocks whose partials are added in block order), and the row is
+ * read once and written once.  num_lookups = length of indices.
+ * max_lookups_per_table: an upper bound on the lookups of any single table in this
+ * call (B*L for fixed bag size L), or 0 if unknown.  With 32-bit row ids and a bound
+ * <= 4096 each table is sorted in LDS by one workgroup; otherwise a device-wide radix
+ * sort is used.  A bound smaller than the real maximum is a contract violation.
+ * (The same applies to the two functions below.)
  */
 int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, int32_t T,
                           int32_t B, const void* indices, int32_t index_bits,
                           const void* offsets, int32_t offset_bits, int64_t num_lookups,
                           int64_t total_rows, const float* per_sample_weights,
                           const float* grad_out, int64_t grad_batch_stride, float lr,
-                          void* workspace, size_t workspace_bytes, dlrm_stream_t stream);
+                          int64_t max_lookups_per_table, void* workspace,
+                          size_t workspace_bytes, dlrm_stream_t stream);
 
 /*
  * Row-wise sparse Adagrad (RWSAdagrad, optim/rwsadagrad.py:92-115) fused into the
@@ -132,8 +138,8 @@ int dlrm_tbe_backward_rowwise_adagrad(float* weights, float* momentum, int64_t D
                                       int64_t num_lookups, int64_t total_rows,
                                       const float* per_sample_weights, const float* grad_out,
                                       int64_t grad_batch_stride, float lr, float eps,
-                                      void* workspace, size_t workspace_bytes,
-                                      dlrm_stream_t stream);
+                                      int64_t max_lookups_per_table, void* workspace,
+                                      size_t workspace_bytes, dlrm_stream_t stream);
 
 /*
  * Dense (non-fused) embedding-bag gradient scatter: grad_weights[row] += w_l * g
@@ -144,7 +150,8 @@ int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_b
                             int32_t T, int32_t B, const void* indices, int32_t index_bits,
                             const void* offsets, int32_t offset_bits, int64_t num_lookups,
                             int64_t total_rows, const float* per_sample_weights,
-                            const float* grad_out, int64_t grad_batch_stride, void* workspace,
+                            const float* grad_out, int64_t grad_batch_stride,
+                            int64_t max_lookups_per_table, void* workspace,
                             size_t workspace_bytes, dlrm_stream_t stream);
 
 /*

@@ -42,14 +42,17 @@ def test_tbe_forward_golden(ops, golden, D, idx_dtype):
 
 
 @pytest.mark.parametrize("D", [4, 16, 64, 128])
-def test_tbe_backward_sgd_golden(ops, golden, D):
+@pytest.mark.parametrize("per_table_sort", [False, True])
+def test_tbe_backward_sgd_golden(ops, golden, D, per_table_sort):
     g = golden(f"tbe_D{D}.npz")
     off, idx, row_base, W, rows = _csr_from_golden(g)
     T, B = len(rows), int(g["B"][0])
     grad = torch.stack([torch.tensor(g[f"g{t}"]) for t in range(T)], 1)  # [B, T, D]
     Wd = W.to(dev)
+    seg = off[::B].long()
+    mx = int((seg[1:] - seg[:-1]).max()) if per_table_sort else 0
     ops.tbe_backward("sgd", Wd, row_base.to(dev), T, B, idx.to(dev), off.to(dev), grad.to(dev),
-                     lr=0.1)
+                     lr=0.1, max_lookups_per_table=mx)
     W1 = Wd.cpu().split(rows, 0)
     for t in range(T):
         ok, msg = fp32_close(W1[t].numpy(), g[f"w1_{t}"])
@@ -98,6 +101,58 @@ def test_tbe_weighted_and_dense_grad(ops):
     ref_vals = G.permute(1, 0, 2).reshape(T * B, D)[bag] * psw[:, None]
     ok, msg = fp32_close(vals.numpy(), ref_vals.numpy())
     assert ok, msg
+
+
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad", "dense"])
+@pytest.mark.parametrize("invalid", [False, True])
+def test_tbe_backward_per_table_sort_vs_global_sort(ops, mode, invalid):
+    """The per-table LDS sort and the device-wide radix sort order lookups by (row, position)
+    alike: with all indices valid the updates are bitwise identical.  Out-of-range indices
+    (skipped) sit at a different place in the two sorted arrays, which shifts the fixed
+    16-lookup reduction blocks; both then still match the reference within fp32 tolerance.
+    Skewed tables (3 rows, ~340 lookups per row) exercise runs spanning many blocks."""
+    torch.manual_seed(7)
+    rows, D, B, L = [3, 5000, 4, 700, 1], 64, 512, 2
+    T = len(rows)
+    lo = [torch.arange(B) * L for _ in rows]
+    li = [torch.randint(0, n, (B * L,)) for n in rows]
+    if invalid:
+        li[1][5] = 999999  # out of range
+    off, idx = O.batched_csr(lo, li)
+    if invalid:
+        idx = torch.cat([idx, torch.tensor([1, 2], dtype=torch.int32)])  # outside every bag
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    G = torch.randn(B, T, D, device=dev)
+    W0 = torch.randn(sum(rows), D, device=dev)
+    mom0 = torch.rand(sum(rows), device=dev)
+    res = []
+    for mx in (0, B * L):
+        W = W0.clone() if mode != "dense" else torch.zeros_like(W0)
+        mom = mom0.clone()
+        ops.tbe_backward(mode, W, row_base, T, B, idx.to(dev), off.to(dev), G, lr=0.3, eps=1e-8,
+                         momentum=mom, max_lookups_per_table=mx)
+        res.append((W.cpu(), mom.cpu()))
+    if not invalid:
+        assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    # reference coalesced gradient
+    gsum = torch.zeros(sum(rows), D, dtype=torch.float64)
+    gt = G.cpu().double()
+    for t in range(T):
+        r = li[t]
+        ok_ = r < rows[t]
+        bag = torch.arange(B * L) // L
+        gsum.index_add_(0, (int(row_base[t]) + r[ok_]), gt[bag[ok_], t])
+    if mode == "dense":
+        ref = gsum
+    elif mode == "sgd":
+        ref = W0.cpu().double() - 0.3 * gsum
+    else:
+        touched = gsum.abs().sum(1) > 0
+        m = mom0.cpu().double() + torch.where(touched, (gsum ** 2).mean(1), torch.zeros(1, dtype=torch.float64))
+        ref = W0.cpu().double() - 0.3 * gsum / (m.sqrt()[:, None] + 1e-8)
+    for W, _ in res:
+        ok, msg = fp32_close(W.numpy(), ref.numpy())
+        assert ok, msg
 
 
 def test_tbe_out_of_range_flag(ops):
