@@ -62,20 +62,24 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
   bag_of[p] = bag;
 }
 
-// Per-table sort (replaces keys + global radix sort when every table's lookups fit in
-// LDS): workgroup t builds the (row, position) keys of table t's lookups, bitonic-sorts
-// them in LDS as one 64-bit composite (row << 32 | position: unique, so the result equals
-// a stable sort) and writes the sorted rows / positions into the table's own range of
-// the output.  Tables own disjoint row ranges and occupy consecutive lookup ranges, so
-// the concatenation is a valid grouping for the block kernel.  Workgroup T marks the
-// lookups outside all bags (before off[0] / after off[T*B]) as sentinels.
-constexpr int kSegCap = 4096;
+// Per-table sort (replaces keys + device radix sort when every table's lookups fit in
+// one workgroup): workgroup t builds table t's local row keys (out-of-range rows ->
+// rows_t) and sorts (key, position) with a stable block radix sort over only
+// bit_width(rows_t) bits, then writes global rows / positions into the table's own range
+// of the output.  Stable on positions, so the order equals the device-wide stable sort.
+// Tables own disjoint row ranges and consecutive lookup ranges, so the concatenation is
+// a valid grouping for the block kernel.  Workgroup T marks the lookups outside all bags
+// (before off[0] / after off[T*B]) as sentinels.
+constexpr int kSegThreads = 512;
+constexpr int kSegItems = 8;
+constexpr int kSegCap = kSegThreads * kSegItems;  // 4096 lookups per table
 template <typename IdxT, typename OffT>
-__global__ __launch_bounds__(512) void tbe_bwd_segsort_kernel(
+__global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
     int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of) {
-  __shared__ uint64_t kv[kSegCap];
+  using BRS = hipcub::BlockRadixSort<uint32_t, kSegThreads, kSegItems, int32_t>;
+  __shared__ typename BRS::TempStorage temp;
   const int t = blockIdx.x;
   const int tid = threadIdx.x;
   if (t == T) {  // lookups outside every bag
@@ -96,38 +100,29 @@ __global__ __launch_bounds__(512) void tbe_bwd_segsort_kernel(
     const int64_t a = (int64_t)off[(int64_t)t * B + b], e = (int64_t)off[(int64_t)t * B + b + 1];
     for (int64_t p = a; p < e; ++p) bag_of[p] = t * B + b;
   }
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (int i = tid; i < np2; i += blockDim.x) {
-    uint64_t v = ~0ull;
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) <= nrows) ++bits;  // keys in [0, nrows]
+  const uint32_t pad = bits >= 32 ? 0xffffffffu : (uint32_t)(((uint64_t)1 << bits) - 1);
+  uint32_t key[kSegItems];
+  int32_t pos[kSegItems];
+#pragma unroll
+  for (int u = 0; u < kSegItems; ++u) {
+    const int i = tid * kSegItems + u;  // blocked arrangement = position order
+    key[u] = pad;
+    pos[u] = i;
     if (i < n) {
-      const int64_t p = s0 + i;
-      const int64_t r = (int64_t)idx[p];
-      const uint32_t key = (r >= 0 && r < nrows) ? (uint32_t)(rb + r) : sentinel;
-      v = ((uint64_t)key << 32) | (uint32_t)p;
-    }
-    kv[i] = v;
-  }
-  __syncthreads();
-  for (int k = 2; k <= np2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < np2; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = kv[i], b = kv[ixj];
-          if ((a > b) == ((i & k) == 0)) {
-            kv[i] = b;
-            kv[ixj] = a;
-          }
-        }
-      }
-      __syncthreads();
+      const int64_t r = (int64_t)idx[s0 + i];
+      key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
     }
   }
-  for (int i = tid; i < n; i += blockDim.x) {
-    const uint64_t v = kv[i];
-    keys_out[s0 + i] = (uint32_t)(v >> 32);
-    pos_out[s0 + i] = (int32_t)(v & 0xffffffffu);
+  BRS(temp).Sort(key, pos, 0, bits);
+#pragma unroll
+  for (int u = 0; u < kSegItems; ++u) {
+    const int i = tid * kSegItems + u;
+    if (i < n) {
+      keys_out[s0 + i] = key[u] < (uint32_t)nrows ? (uint32_t)(rb + key[u]) : sentinel;
+      pos_out[s0 + i] = (int32_t)(s0 + pos[u]);
+    }
   }
 }
 
@@ -448,7 +443,7 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
                name, ws_bytes, w.total);
   if (sizeof(KeyT) == 4 && max_seg > 0 && max_seg <= kSegCap && N < (int64_t)0x7fffffff) {
-    hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(512), 0, st,
+    hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(kSegThreads), 0, st,
                        static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base, T,
                        B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),
                        w.pos_out, w.bag_of);
