@@ -4,7 +4,7 @@ WRITE_SIZE, counter unit KB) of `bench.py --no-graph --steps S --warmup W`.
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of
 wide coalesced reads -> doubled; WRITE_SIZE taken as is.
 
-Usage: python tools/pmc_summary.py <dir with pmc_FETCH_SIZE/ pmc_WRITE_SIZE/> <steps>
+Usage: python tools/pmc_summary.py <dir with pmc_FETCH_SIZE/ pmc_WRITE_SIZE/> <steps + warmup of the pass>
 """
 import csv
 import json
@@ -12,12 +12,12 @@ import sys
 from collections import defaultdict
 
 GROUPS = [
-    ("gemm", ("gemm_f32_mfma_kernel", "gemm_splitk_reduce_kernel")),
+    ("gemm", ("gemm_f32_", "gemm_splitk_reduce_kernel")),
     ("tbe_fwd", ("tbe_fwd_kernel",)),
     ("tbe_bwd", ("tbe_bwd_", "rocprim")),
     ("interaction", ("interact_",)),
     ("colsum", ("colsum_",)),
-    ("head", ("head_rows_kernel", "mean_kernel", "outer_drelu_kernel")),
+    ("head", ("head_", "mean_kernel", "outer_drelu_kernel")),
     ("relu_bwd", ("relu_bwd_kernel",)),
 ]
 
