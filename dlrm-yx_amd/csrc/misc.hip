@@ -561,3 +561,92 @@ extern "C" int dlrm_head_step(int64_t M, int64_t K, const float* X, int64_t ldx,
   DLRM_LAUNCH_CHECK(name);
   return DLRM_OK;
 }
+
+// ---------------------------------------------------------------------------------------
+// Criteo binary record decode (the CriteoBinDataset.__getitem__ + _transform_features
+// path, data_loader_terabyte.py:83-114, 237-252).  A record is int32
+// [label | n_dense | n_sparse]; one thread per int32 field in FLAT order, so the raw
+// block is read fully coalesced and each field is written where the step reads it:
+//   label            -> label[b] = (float)v
+//   dense field j    -> dense[b * ld_dense + j] = log((float)v + 1)
+//   sparse field t   -> indices[t * n + b] = v mod max_ind_range (floor mod, torch `%`),
+//                       table-major as lS_i = x_cat.t() / cat(lS_i) (:93-98)
+// and, for the table-batched form, offsets[i] = i for i <= n_sparse * n (L = 1, :99-100).
+// Integer work is bit-exact; the log is fp32.
+namespace {
+
+template <typename IT>
+__global__ __launch_bounds__(256) void criteo_decode_kernel(
+    const int32_t* __restrict__ rec, int64_t n, int32_t n_dense, int32_t n_sparse,
+    int64_t max_ind_range, float* __restrict__ dense, int64_t ld_dense,
+    float* __restrict__ label, IT* __restrict__ indices) {
+  const int32_t nf = 1 + n_dense + n_sparse;
+  const int64_t total = n * nf;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / nf;
+    const int32_t f = (int32_t)(i - b * nf);
+    const int32_t v = __builtin_nontemporal_load(rec + i);
+    if (f == 0) {
+      if (label) label[b] = (float)v;
+    } else if (f <= n_dense) {
+      if (dense) dense[b * ld_dense + (f - 1)] = logf((float)v + 1.f);
+    } else {
+      int64_t x = v;
+      if (max_ind_range > 0) {
+        x %= max_ind_range;
+        if (x < 0) x += max_ind_range;
+      }
+      indices[(int64_t)(f - 1 - n_dense) * n + b] = (IT)x;
+    }
+  }
+}
+
+template <typename OT>
+__global__ __launch_bounds__(256) void iota_kernel(OT* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (OT)i;
+}
+
+}  // namespace
+
+extern "C" int dlrm_criteo_decode(const int32_t* records, int64_t n, int32_t n_dense,
+                                  int32_t n_sparse, int64_t max_ind_range, float* dense,
+                                  int64_t ld_dense, float* label, void* indices,
+                                  int32_t index_bits, void* offsets, int32_t offset_bits,
+                                  dlrm_stream_t stream) {
+  const char* name = "dlrm_criteo_decode";
+  DLRM_ARG(n >= 0 && n_dense >= 0 && n_sparse >= 0, "%s: bad sizes", name);
+  DLRM_ARG(ld_dense >= n_dense, "%s: ld_dense < n_dense", name);
+  DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: bad index_bits", name);
+  DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: bad offset_bits", name);
+  DLRM_ARG(n == 0 || (records && (indices || n_sparse == 0)), "%s: null pointer", name);
+  DLRM_REQUIRE(index_bits == 64 || max_ind_range <= (int64_t)INT32_MAX + 1, DLRM_ERR_UNSUPPORTED,
+               "%s: int32 indices with max_ind_range > 2^31", name);
+  hipStream_t st = dlrm::as_stream(stream);
+  const int64_t total = n * (1 + n_dense + n_sparse);
+  if (total == 0) {
+    // nothing to decode; the CSR below still gets its single offsets[0] = 0
+  } else if (index_bits == 32)
+    hipLaunchKernelGGL(criteo_decode_kernel<int32_t>, dim3(grid_stride_blocks(total)), dim3(256),
+                       0, st, records, n, n_dense, n_sparse, max_ind_range, dense, ld_dense, label,
+                       static_cast<int32_t*>(indices));
+  else
+    hipLaunchKernelGGL(criteo_decode_kernel<int64_t>, dim3(grid_stride_blocks(total)), dim3(256),
+                       0, st, records, n, n_dense, n_sparse, max_ind_range, dense, ld_dense, label,
+                       static_cast<int64_t*>(indices));
+  if (offsets) {
+    const int64_t no = (int64_t)n_sparse * n + 1;
+    DLRM_REQUIRE(offset_bits == 64 || no <= (int64_t)INT32_MAX, DLRM_ERR_UNSUPPORTED,
+                 "%s: int32 offsets overflow", name);
+    if (offset_bits == 32)
+      hipLaunchKernelGGL(iota_kernel<int32_t>, dim3(grid_stride_blocks(no)), dim3(256), 0, st,
+                         static_cast<int32_t*>(offsets), no);
+    else
+      hipLaunchKernelGGL(iota_kernel<int64_t>, dim3(grid_stride_blocks(no)), dim3(256), 0, st,
+                         static_cast<int64_t*>(offsets), no);
+  }
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}

@@ -78,6 +78,8 @@ SIGNATURES = {
     "dlrm_uniform_fill": (c_int32, [P, c_int64, c_float, c_float, c_uint64, P]),
     "dlrm_uniform_int_fill": (c_int32, [P, c_int32, c_int64, c_int64, c_uint64, P]),
     "dlrm_csr_from_tables": (c_int32, [c_int32, c_int32, P, P, P, c_int32, P]),
+    "dlrm_criteo_decode": (c_int32, [P, c_int64, c_int32, c_int32, c_int64, P, c_int64, P, P,
+                                     c_int32, P, c_int32, P]),
 }
 
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "SHAPE", 3: "UNSUPPORTED", 4: "WORKSPACE", 5: "HIP"}

@@ -7,6 +7,7 @@ DLRMTrainer.synthetic_batch.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence
 
 import numpy as np
@@ -76,3 +77,78 @@ def batched_csr(lS_o: Sequence[torch.Tensor], lS_i: Sequence[torch.Tensor]):
 def log1p_dense(X: torch.Tensor) -> torch.Tensor:
     """The cached random path feeds log(X + 1) (dlrm_data_pytorch.py:727)."""
     return torch.log(X.to(torch.float32) + 1)
+
+
+class CriteoBinDataset(torch.utils.data.Dataset):
+    """Binary Criteo records, decoded on the GPU (data_loader_terabyte.py:195-252).
+
+    Same constructor, length and item layout as the reference: item ``idx`` is the
+    ``idx``-th block of ``batch_size`` int32 records [label | 13 dense | 26 sparse]
+    (the last block may be short), returned as (X, lS_o, lS_i, y) exactly as
+    ``_transform_features(..., flag_input_torch_tensor=True)`` returns them.  The raw block
+    goes to the device once (pinned, 160 B/sample) and one ``dlrm_criteo_decode`` launch
+    does the split, log(x+1), ``% max_ind_range`` and the (table-batched) CSR there.
+    """
+
+    def __init__(self, data_file, counts_file, batch_size=1, max_ind_range=-1,
+                 bytes_per_feature=4, batched_or_fbgemm_emb=False, device="cuda"):
+        if bytes_per_feature != 4:
+            raise NotImplementedError("CriteoBinDataset: only int32 records (bytes_per_feature=4)")
+        self.tar_fea, self.den_fea, self.spa_fea = 1, 13, 26
+        self.tad_fea = self.tar_fea + self.den_fea
+        self.tot_fea = self.tad_fea + self.spa_fea
+        self.batch_size = batch_size
+        self.max_ind_range = max_ind_range
+        self.bytes_per_entry = bytes_per_feature * self.tot_fea * batch_size
+        self.num_entries = -(-os.path.getsize(data_file) // self.bytes_per_entry)
+        self.data_file = data_file
+        with np.load(counts_file) as data:
+            self.counts = data["counts"]
+        self.m_den = 13
+        self.batched_or_fbgemm_emb = batched_or_fbgemm_emb
+        self.device = torch.device(device)
+
+    def __len__(self):
+        return self.num_entries
+
+    def read_raw(self, idx: int) -> torch.Tensor:
+        """The idx-th raw int32 block, host-side (the file read; no transform)."""
+        with open(self.data_file, "rb") as f:
+            f.seek(idx * self.bytes_per_entry, 0)
+            raw = f.read(self.bytes_per_entry)
+        return torch.from_numpy(np.frombuffer(raw, dtype=np.int32).copy())
+
+    def __getitem__(self, idx):
+        if idx < 0 or idx >= self.num_entries:
+            raise IndexError(idx)
+        rec = self.read_raw(idx)
+        if self.device.type == "cuda":
+            rec = rec.pin_memory().to(self.device, non_blocking=True)
+        return ops.criteo_decode(rec, self.den_fea, self.spa_fea, self.max_ind_range,
+                                 batched=self.batched_or_fbgemm_emb)
+
+
+def numpy_to_binary(input_files, output_file_path, split="train"):
+    """Write day_*_reordered.npz files as int32 records [y | X_int | X_cat]
+    (data_loader_terabyte.py:255-293): train concatenates every file; test / val take the
+    first / second half (ceil split) of the single input file."""
+    def rows(path):
+        with np.load(path) as d:
+            return np.concatenate([d["y"].reshape(-1, 1), d["X_int"], d["X_cat"]],
+                                  axis=1).astype(np.int32)
+
+    with open(output_file_path, "wb") as out:
+        if split == "train":
+            for path in input_files:
+                out.write(rows(path).tobytes())
+            return
+        if len(input_files) != 1:
+            raise ValueError("numpy_to_binary: test/val split takes exactly one input file")
+        data = rows(input_files[0])
+        mid = -(-data.shape[0] // 2)
+        if split == "test":
+            out.write(data[:mid].tobytes())
+        elif split == "val":
+            out.write(data[mid:].tobytes())
+        else:
+            raise ValueError(f"Unknown split value: {split}")

@@ -410,3 +410,34 @@ def csr_from_tables(table_offsets: Sequence[torch.Tensor], table_nnz: Sequence[i
     _lib.call("dlrm_csr_from_tables", T, B, ptrs, nnz, _p(out),
               32 if out_dtype == torch.int32 else 64, _stream(offs[0].device))
     return out
+
+
+def criteo_decode(records: torch.Tensor, n_dense: int = 13, n_sparse: int = 26,
+                  max_ind_range: int = -1, batched: bool = False,
+                  dense: Optional[torch.Tensor] = None):
+    """Device decode of raw Criteo binary records int32 [n, 1+n_dense+n_sparse]
+    (dlrm_criteo_decode; data_loader_terabyte.py:83-114).  Returns (dense [n, n_dense]
+    log(x+1), lS_o, lS_i, label [n, 1]) in the reference's layouts: batched -> int32
+    offsets [T*n+1] and int32 indices [T*n]; else int64 lS_o [T, n] = arange and int64
+    lS_i [T, n].  ``dense`` may be a caller buffer (row stride >= n_dense)."""
+    _check_cuda(records, dense)
+    nf = 1 + n_dense + n_sparse
+    if records.dtype != torch.int32 or not records.is_contiguous() or records.numel() % nf:
+        raise ValueError(f"criteo_decode: need contiguous int32 records of {nf} fields")
+    n = records.numel() // nf
+    dev = records.device
+    if dense is None:
+        dense = torch.empty((n, n_dense), dtype=torch.float32, device=dev)
+    elif dense.shape[0] != n or dense.shape[1] < n_dense or dense.stride(1) != 1:
+        raise ValueError("criteo_decode: dense buffer must be [n, >= n_dense] row-major")
+    label = torch.empty((n, 1), dtype=torch.float32, device=dev)
+    idt = torch.int32 if batched else torch.int64
+    indices = torch.empty(n_sparse * n, dtype=idt, device=dev)
+    offsets = torch.empty(n_sparse * n + 1, dtype=torch.int32, device=dev) if batched else None
+    _lib.call("dlrm_criteo_decode", _p(records), n, n_dense, n_sparse, int(max_ind_range),
+              _p(dense), dense.stride(0) if n else n_dense, _p(label), _p(indices),
+              32 if batched else 64, _p(offsets), 32, _stream(dev))
+    if batched:
+        return dense, offsets, indices, label
+    lS_o = torch.arange(n, device=dev).reshape(1, -1).repeat(n_sparse, 1)
+    return dense, lS_o, indices.view(n_sparse, n), label

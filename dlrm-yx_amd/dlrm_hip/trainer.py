@@ -262,6 +262,31 @@ class DLRMTrainer:
         mx = max([int(i.numel()) for i in idxs], default=0)
         return Batch(Xp, offsets, indices, tg, mx)
 
+    def batch_from_records(self, records: torch.Tensor, max_ind_range: int = -1) -> Batch:
+        """A Batch straight from raw Criteo binary records on the device (int32
+        [B_global, 1+13+26], the CriteoBinDataset block, data_loader_terabyte.py:237-252):
+        one dlrm_criteo_decode launch writes log(x+1) into the padded X (bias column kept),
+        the table-major indices (% max_ind_range) and the L = 1 CSR.  Same batch as
+        make_batch on the reference's transformed tensors."""
+        L0 = self.bot[0]
+        nf = 1 + L0.K + self.T
+        if records.dim() != 2 or records.shape[1] != nf:
+            raise ValueError(f"batch_from_records: records must be [B, {nf}] (1 + m_den + T)")
+        B = records.shape[0]
+        Bl = self.local_batch_size(B)
+        rec = records.reshape(-1).to(device=self.dev, dtype=torch.int32).contiguous()
+        dense = torch.empty((B, L0.Kp), dtype=torch.float32, device=self.dev)
+        dense[:, L0.K:] = 0.0
+        dense[:, L0.K] = 1.0  # bias column
+        X, offsets, indices, label = ops.criteo_decode(rec, L0.K, self.T, max_ind_range,
+                                                       batched=True, dense=dense)
+        sl = slice(self.rank * Bl, (self.rank + 1) * Bl)
+        if self.T_local != self.T:
+            indices = indices.view(self.T, B)[self.local_tables].reshape(-1).contiguous()
+            offsets = offsets[:self.T_local * B + 1].contiguous()
+        return Batch(dense[sl].contiguous() if Bl != B else dense, offsets, indices,
+                     label.reshape(-1)[sl].contiguous(), B)
+
     def synthetic_batch(self, B: int, L: int, seed: int) -> Batch:
         """Device-generated synthetic batch of the reference's shape: X ~ log(1+U[0,1))
         (dlrm_data_pytorch.py:727), L uniform indices per bag per table, targets U[0,1)

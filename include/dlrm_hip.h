@@ -41,6 +41,8 @@
  *   dlrm_uniform_fill         <- np.random.uniform table init (dlrm_s_pytorch.py:304-308),
  *                                device-side for tables too large for host init
  *   dlrm_csr_from_tables      <- table-batched CSR flatten (dlrm_data_pytorch.py:748-753,834-843)
+ *   dlrm_criteo_decode        <- CriteoBinDataset.__getitem__ + _transform_features
+ *                                (data_loader_terabyte.py:83-114,237-252)
  */
 #ifndef DLRM_HIP_H_
 #define DLRM_HIP_H_
@@ -313,6 +315,24 @@ int dlrm_uniform_int_fill(void* out, int32_t out_bits, int64_t n, int64_t hi, ui
 int dlrm_csr_from_tables(int32_t T, int32_t B, const int64_t* const* table_offsets,
                          const int64_t* table_nnz, void* out_offsets, int32_t out_offset_bits,
                          dlrm_stream_t stream);
+
+/*
+ * Criteo binary records -> one step's device inputs (replaces the host-side
+ * CriteoBinDataset.__getitem__ -> _transform_features, data_loader_terabyte.py:237-252,
+ * 83-114).  `records` is the raw int32 block [n][1 + n_dense + n_sparse] of the binary
+ * file written by numpy_to_binary (:255-293), already on the device.  Writes
+ *   label[n]                       = (float)label           (may be NULL)
+ *   dense[b * ld_dense + j]        = log((float)x_int + 1)  (may be NULL)
+ *   indices[t * n + b]             = x_cat[b][t] mod max_ind_range (floor mod, as torch
+ *                                    `%`; no mod when max_ind_range <= 0), table-major
+ *                                    = cat(x_cat.t()); index_bits 32 (batched) or 64
+ *   offsets[i] = i, i <= n_sparse*n  (table-batched CSR, L = 1; may be NULL)
+ * Integer outputs are bit-exact; the dense log is fp32.
+ */
+int dlrm_criteo_decode(const int32_t* records, int64_t n, int32_t n_dense, int32_t n_sparse,
+                       int64_t max_ind_range, float* dense, int64_t ld_dense, float* label,
+                       void* indices, int32_t index_bits, void* offsets, int32_t offset_bits,
+                       dlrm_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,7 @@ __all__ = [
     "generate_uniform_input_batch", "generate_random_output_batch", "batched_csr",
     "distribute_batched", "init_emb_tables", "init_mlp", "embedding_bag_sum", "interact",
     "OracleDLRM", "QREmbeddingBagOracle", "RWSAdagradOracle", "distributed_step",
-    "KAGGLE_ROWS", "TERABYTE_ROWS",
+    "criteo_transform", "KAGGLE_ROWS", "TERABYTE_ROWS",
 ]
 
 # tools/visualize.py:949 (Kaggle) and :964 (Terabyte) row counts; Terabyte capped at 1e7
@@ -378,3 +378,29 @@ class RWSAdagradOracle:
     def zero_grad(self):
         for p in self.params:
             p.grad = None
+
+
+def criteo_transform(records: np.ndarray, max_ind_range: int = -1, batched: bool = False,
+                     n_dense: int = 13):
+    """CriteoBinDataset.__getitem__ -> _transform_features(flag_input_torch_tensor=True)
+    (data_loader_terabyte.py:237-252, 83-114) on an int32 record block [n, 1+13+26]:
+    X = log(float(x_int) + 1); x_cat % max_ind_range (torch floor mod) when > 0;
+    lS_o = arange(n) per table, lS_i = x_cat.t(); batched: int32 cat(lS_i) and
+    offsets cat(lS_o[t] + t*n) ++ [T*n]."""
+    t = torch.from_numpy(np.ascontiguousarray(records, dtype=np.int32)).view(-1, 1 + n_dense + 26)
+    x_int, x_cat, y = t[:, 1:1 + n_dense], t[:, 1 + n_dense:], t[:, 0]
+    if max_ind_range > 0:
+        x_cat = x_cat % max_ind_range
+    X = torch.log(x_int.clone().detach().type(torch.float) + 1)
+    x_cat = x_cat.clone().detach().type(torch.long)
+    y = y.clone().detach().type(torch.float32).view(-1, 1)
+    n, T = x_cat.shape
+    lS_o = torch.arange(n).reshape(1, -1).repeat(T, 1)
+    lS_i = x_cat.t()
+    if batched:
+        indices = torch.cat([x.reshape(-1) for x in lS_i]).int()
+        starts = [0] + np.cumsum([x.numel() for x in lS_i]).tolist()
+        offsets = torch.cat([o + s for o, s in zip(lS_o, starts[:-1])]
+                            + [torch.tensor([starts[-1]])]).int()
+        lS_i, lS_o = indices, offsets
+    return X, lS_o, lS_i, y
