@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void tbe_fwd_kernel(
       if (gl < n) {
         int64_t r = (int64_t)idx[l0 + gl];
         if (r < 0 || r >= nrows) {
-          if (err) *err = 1;
+          if (err) atomicOr(err, DLRM_TBE_ERR_INDEX);
           r = -1;
         }
         my_row = r;

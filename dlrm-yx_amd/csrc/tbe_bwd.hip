@@ -34,7 +34,7 @@ template <typename IdxT, typename OffT, typename KeyT>
 __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, KeyT sentinel, KeyT* __restrict__ keys, int32_t* __restrict__ pos,
-    int32_t* __restrict__ bag_of) {
+    int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= N) return;
   const int64_t nb = (int64_t)T * B;
@@ -55,6 +55,8 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
     if (r >= 0 && r < nrows) {
       key = (KeyT)(row_base[t] + r);
       bag = (int32_t)lo;
+    } else if (err) {
+      atomicOr(err, DLRM_TBE_ERR_INDEX);
     }
   }
   keys[p] = key;
@@ -69,7 +71,10 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
 // of the output.  Stable on positions, so the order equals the device-wide stable sort.
 // Tables own disjoint row ranges and consecutive lookup ranges, so the concatenation is
 // a valid grouping for the block kernel.  Workgroup T marks the lookups outside all bags
-// (before off[0] / after off[T*B]) as sentinels.
+// (before off[0] / after off[T*B]) as sentinels.  A table with more than kSegCap lookups
+// (the caller's max_lookups_per_table was an underestimate) is not sorted: all its lookups
+// become sentinels (no update, no stale keys, no out-of-bounds row) and bit
+// DLRM_TBE_ERR_TABLE_CAP is raised in *err.
 constexpr int kSegThreads = 512;
 constexpr int kSegItems = 8;
 constexpr int kSegCap = kSegThreads * kSegItems;  // 4096 lookups per table
@@ -77,7 +82,7 @@ template <typename IdxT, typename OffT>
 __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
-    int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of) {
+    int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
   using BRS = hipcub::BlockRadixSort<uint32_t, kSegThreads, kSegItems, int32_t>;
   __shared__ typename BRS::TempStorage temp;
   const int t = blockIdx.x;
@@ -93,13 +98,22 @@ __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
     return;
   }
   const int64_t s0 = (int64_t)off[(int64_t)t * B];
-  const int n = (int)((int64_t)off[(int64_t)(t + 1) * B] - s0);  // <= kSegCap (contract)
+  const int64_t n64 = (int64_t)off[(int64_t)(t + 1) * B] - s0;  // <= kSegCap (contract)
   const int64_t rb = row_base[t];
   const int64_t nrows = row_base[t + 1] - rb;
   for (int b = tid; b < B; b += blockDim.x) {
     const int64_t a = (int64_t)off[(int64_t)t * B + b], e = (int64_t)off[(int64_t)t * B + b + 1];
     for (int64_t p = a; p < e; ++p) bag_of[p] = t * B + b;
   }
+  if (n64 > kSegCap) {  // contract violated: skip the table, report
+    for (int64_t i = tid; i < n64; i += blockDim.x) {
+      keys_out[s0 + i] = sentinel;
+      pos_out[s0 + i] = (int32_t)(s0 + i);
+    }
+    if (tid == 0 && err) atomicOr(err, DLRM_TBE_ERR_TABLE_CAP);
+    return;
+  }
+  const int n = (int)n64;
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) <= nrows) ++bits;  // keys in [0, nrows]
   const uint32_t pad = bits >= 32 ? 0xffffffffu : (uint32_t)(((uint64_t)1 << bits) - 1);
@@ -113,6 +127,7 @@ __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
     if (i < n) {
       const int64_t r = (int64_t)idx[s0 + i];
       key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
+      if (key[u] == (uint32_t)nrows && err) atomicOr(err, DLRM_TBE_ERR_INDEX);
     }
   }
   BRS(temp).Sort(key, pos, 0, bits);
@@ -435,7 +450,7 @@ template <typename KeyT, typename IdxT, typename OffT>
 int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
                const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
                const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
-               int64_t max_seg, hipStream_t st, const char* name) {
+               int64_t max_seg, int32_t* err, hipStream_t st, const char* name) {
   if (N == 0) return DLRM_OK;
   const KeyT sentinel = (KeyT)total_rows;
   const int end_bit = bit_width_u64((uint64_t)total_rows);
@@ -446,13 +461,13 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
     hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(kSegThreads), 0, st,
                        static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base, T,
                        B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),
-                       w.pos_out, w.bag_of);
+                       w.pos_out, w.bag_of, err);
     DLRM_LAUNCH_CHECK(name);
   } else {
     hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(dlrm::ceil_div(N, 256)),
                        dim3(256), 0, st, static_cast<const IdxT*>(idx),
                        static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_in,
-                       w.pos_in, w.bag_of);
+                       w.pos_in, w.bag_of, err);
     DLRM_LAUNCH_CHECK(name);
     size_t tb = w.temp_bytes;
     DLRM_HIP_CALL(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in,
@@ -518,8 +533,8 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
 int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T,
                  int B, const void* idx, int ib, const void* off, int ob, int64_t N,
                  int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
-                 float eps, void* ws, size_t ws_bytes, int64_t max_seg, dlrm_stream_t stream,
-                 const char* name) {
+                 float eps, void* ws, size_t ws_bytes, int64_t max_seg, int32_t* err,
+                 dlrm_stream_t stream, const char* name) {
   DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
@@ -532,7 +547,7 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
   const bool k32 = (uint64_t)total_rows < 0xFFFFFFFFull;
 #define BWD(K, I, O)                                                                     \
   return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
-                             gout, gbs, lr, eps, ws, ws_bytes, max_seg, st, name)
+                             gout, gbs, lr, eps, ws, ws_bytes, max_seg, err, st, name)
   if (k32) {
     if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
     if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
@@ -566,11 +581,12 @@ extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* r
                                      int64_t total_rows, const float* per_sample_weights,
                                      const float* grad_out, int64_t grad_batch_stride, float lr,
                                      int64_t max_lookups_per_table, void* workspace,
-                                     size_t workspace_bytes, dlrm_stream_t stream) {
+                                     size_t workspace_bytes, int32_t* error_flag,
+                                     dlrm_stream_t stream) {
   return bwd_dispatch(MODE_SGD, weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes,
-                      max_lookups_per_table, stream, "dlrm_tbe_backward_sgd");
+                      max_lookups_per_table, error_flag, stream, "dlrm_tbe_backward_sgd");
 }
 
 extern "C" int dlrm_tbe_backward_rowwise_adagrad(
@@ -578,12 +594,14 @@ extern "C" int dlrm_tbe_backward_rowwise_adagrad(
     const void* indices, int32_t index_bits, const void* offsets, int32_t offset_bits,
     int64_t num_lookups, int64_t total_rows, const float* per_sample_weights,
     const float* grad_out, int64_t grad_batch_stride, float lr, float eps,
-    int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes, dlrm_stream_t stream) {
+    int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes, int32_t* error_flag,
+    dlrm_stream_t stream) {
   DLRM_ARG(momentum, "dlrm_tbe_backward_rowwise_adagrad: null momentum");
   return bwd_dispatch(MODE_ADAGRAD, weights, momentum, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes,
-                      max_lookups_per_table, stream, "dlrm_tbe_backward_rowwise_adagrad");
+                      max_lookups_per_table, error_flag, stream,
+                      "dlrm_tbe_backward_rowwise_adagrad");
 }
 
 extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_base,
@@ -593,9 +611,10 @@ extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int
                                        int64_t total_rows, const float* per_sample_weights,
                                        const float* grad_out, int64_t grad_batch_stride,
                                        int64_t max_lookups_per_table, void* workspace,
-                                       size_t workspace_bytes, dlrm_stream_t stream) {
+                                       size_t workspace_bytes, int32_t* error_flag,
+                                       dlrm_stream_t stream) {
   return bwd_dispatch(MODE_DENSE, grad_weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes,
-                      max_lookups_per_table, stream, "dlrm_tbe_backward_dense");
+                      max_lookups_per_table, error_flag, stream, "dlrm_tbe_backward_dense");
 }

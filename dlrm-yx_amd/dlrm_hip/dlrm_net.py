@@ -89,12 +89,18 @@ class DLRM_Net(nn.Module):
         return emb_l, v_W_l
 
     def create_emb_batched(self, D, Es, weighted_pooling=None, learning_rate=0.1):
-        """dlrm_s_pytorch.py:321-334 (exact SGD fused, lr 0.1 hard-coded like the reference)."""
+        """dlrm_s_pytorch.py:321-334 (exact SGD fused, lr 0.1 hard-coded like the reference).
+
+        The reference hands table init to the external TableBatchedEmbeddingBags, which is
+        not in the reference tree (parity unpinned).  The tables are drawn from a private
+        numpy RandomState seeded from torch.initial_seed(), so the global numpy stream the
+        MLP init draws from afterwards is the same as the reference's."""
         assert weighted_pooling is None, "Weighted pooling not supported yet!"
         self.Es = Es[self.local_emb_indices] if ext_dist.my_size > 1 else Es
         T = len(self.Es)
-        tables = [np.random.uniform(low=-np.sqrt(1 / n), high=np.sqrt(1 / n),
-                                    size=(int(n), D)).astype(np.float32) for n in self.Es]
+        rng = np.random.RandomState(torch.initial_seed() % (2 ** 32))
+        tables = [rng.uniform(low=-np.sqrt(1 / n), high=np.sqrt(1 / n),
+                              size=(int(n), D)).astype(np.float32) for n in self.Es]
         return TableBatchedEmbeddingBags(T, self.Es, D, optimizer=Optimizer.SGD,
                                          learning_rate=learning_rate, eps=0.1,
                                          stochastic_rounding=False, tables=tables), [None] * T

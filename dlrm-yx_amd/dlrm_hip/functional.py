@@ -109,6 +109,18 @@ def interact(op: str, x: torch.Tensor, ly, itself: bool = False) -> torch.Tensor
 
 
 # ------------------------------------------------------------ embeddings ----
+def _error_flag(module, device) -> torch.Tensor:
+    """The module's device TBE error flag (int32, created on first use)."""
+    f = getattr(module, "tbe_error_flag", None)
+    if f is None or f.device != device:
+        f = torch.zeros(1, dtype=torch.int32, device=device)
+        try:
+            module.tbe_error_flag = f
+        except AttributeError:
+            pass
+    return f
+
+
 class EmbeddingBagsFunction(torch.autograd.Function):
     """Pooled-sum lookup over T tables that live in one flat [sum rows, D] buffer.
 
@@ -125,8 +137,14 @@ class EmbeddingBagsFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, module, counts, indices, offsets, per_sample_weights, *table_params):
         B = (offsets.numel() - 1) // module.T
+        flag = _error_flag(module, indices.device)
         out = ops.tbe_forward(module.weight_flat, module.row_base, module.T, B, indices, offsets,
-                              per_sample_weights=per_sample_weights)
+                              per_sample_weights=per_sample_weights, error_flag=flag)
+        if getattr(module, "strict_indices", True):
+            # nn.EmbeddingBag raises IndexError on an out-of-range index; the kernel skips
+            # and flags it, and this reads the flag (one sync, like the driver's per-step
+            # loss read).  Set module.strict_indices = False for graph capture.
+            ops.check_tbe_errors(flag)
         ctx.module, ctx.B, ctx.counts = module, B, counts
         ctx.save_for_backward(indices, offsets, per_sample_weights)
         ctx.n_params = len(table_params)

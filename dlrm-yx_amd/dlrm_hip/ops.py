@@ -14,6 +14,24 @@ import torch
 from . import _lib
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_DRELU, EPI_SGD, EPI_ACCUM, EPI_RELU = range(7)
+TBE_ERR_INDEX, TBE_ERR_TABLE_CAP = 1, 2  # dlrm_tbe_error bits
+
+
+class TBEIndexError(IndexError):
+    """Raised by check_tbe_errors: the reference's EmbeddingBag raises IndexError for an
+    index outside its table; the device kernels skip such lookups and flag them."""
+
+
+def check_tbe_errors(flag: torch.Tensor, reset: bool = True) -> None:
+    """Read a TBE error flag (synchronises with its stream) and raise on any bit."""
+    v = int(flag.item())
+    if reset:
+        flag.zero_()
+    if v & TBE_ERR_INDEX:
+        raise TBEIndexError("embedding index out of range for its table (lookup skipped)")
+    if v & TBE_ERR_TABLE_CAP:
+        raise ValueError("a table had more lookups than max_lookups_per_table "
+                         "(its backward update was skipped)")
 LOSS_MSE, LOSS_BCE = 0, 1
 QR_OPS = {"mult": 0, "add": 1, "concat": 2}
 
@@ -93,11 +111,13 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
                  per_sample_weights: Optional[torch.Tensor] = None,
                  grad_batch_stride: Optional[int] = None,
                  workspace: Optional[torch.Tensor] = None,
-                 max_lookups_per_table: int = 0) -> None:
+                 max_lookups_per_table: int = 0,
+                 error_flag: Optional[torch.Tensor] = None) -> None:
     """mode: 'sgd' (fused exact SGD), 'rowwise_adagrad' (fused RWSAdagrad) or
     'dense' (weights is a gradient buffer to accumulate into).  max_lookups_per_table:
     upper bound on any table's lookups (0 = unknown); <= 4096 selects the per-table LDS
-    sort (bitwise the same result as the device-wide radix sort)."""
+    sort (bitwise the same result as the device-wide radix sort).  ``error_flag``: device
+    int32 that receives TBE_ERR_INDEX / TBE_ERR_TABLE_CAP bits (see check_tbe_errors)."""
     _check_cuda(weights, row_base, indices, offsets, grad_out, momentum, per_sample_weights)
     D = weights.shape[1]
     N = indices.numel()
@@ -114,13 +134,13 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
     mx = int(max_lookups_per_table)
     if mode == "sgd":
         _lib.call("dlrm_tbe_backward_sgd", _p(weights), *args_common, lr, mx, _p(workspace),
-                  workspace.numel(), st)
+                  workspace.numel(), _p(error_flag), st)
     elif mode == "rowwise_adagrad":
         _lib.call("dlrm_tbe_backward_rowwise_adagrad", _p(weights), _p(momentum), *args_common,
-                  lr, eps, mx, _p(workspace), workspace.numel(), st)
+                  lr, eps, mx, _p(workspace), workspace.numel(), _p(error_flag), st)
     elif mode == "dense":
         _lib.call("dlrm_tbe_backward_dense", _p(weights), *args_common, mx, _p(workspace),
-                  workspace.numel(), st)
+                  workspace.numel(), _p(error_flag), st)
     else:
         raise ValueError(mode)
 
@@ -235,7 +255,7 @@ def interact_backward(op: str, x: torch.Tensor, ly, grad_out: torch.Tensor,
     gfeats, gstrides = feature_views(grad_x, grad_ly)
     ptrs, bs = _feature_arrays(feats, strides)
     gptrs, gbs = _feature_arrays(gfeats, gstrides)
-    g = grad_out.contiguous()
+    g = grad_out if grad_out.stride(1) == 1 else grad_out.contiguous()  # row stride is passed
     if op == "dot":
         _lib.call("dlrm_interact_dot_backward", B, F, D, ptrs, bs, int(self_interaction), _p(g),
                   g.stride(0), gptrs, gbs, _stream(x.device))
@@ -269,8 +289,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool 
     if C is None:
         C = torch.empty((M, N), dtype=torch.float32, device=A.device)
     need = gemm_workspace_size(M, N, K, trans_a, trans_b)
-    if need and (workspace is None or workspace.numel() < need):
+    if need and workspace is None:
         workspace = _ws("gemm", need, A.device)
+    elif need and workspace.numel() < need:
+        # never fall back to a shared buffer behind the caller's back: two streams could
+        # then write split-K partials into the same scratch
+        raise ValueError(f"gemm workspace too small: {workspace.numel()} < {need} bytes")
     _lib.call("dlrm_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), _p(A),
               A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0), epilogue, _p(bias), _p(aux),
               aux.stride(0) if aux is not None else 0, _p(workspace) if need else None,

@@ -169,6 +169,9 @@ class DLRMTrainer:
         self.overlaps = set(os.environ.get("DLRM_OVERLAPS", "").split(","))
         self._side = torch.cuda.Stream(device=self.dev)
         self._tbe_ws: Optional[torch.Tensor] = None
+        # device TBE error bits (ops.TBE_ERR_*): out-of-range indices are skipped by the
+        # kernels and flagged here; check_errors() reads it (the step never syncs)
+        self.tbe_error_flag = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self._colsum_ws: Optional[torch.Tensor] = None
         self._head_ws: Optional[torch.Tensor] = None
         self.step_count = 0
@@ -332,8 +335,10 @@ class DLRMTrainer:
             shapes += [(Bl, L.N, L.Kp, False, True), (Bl, L.K, L.N, False, False),
                        (L.N, L.Kp, Bl, True, False)]
         gws = max([ops.gemm_workspace_size(*s) for s in shapes] + [256])
-        self._gemm_ws = torch.empty(gws, dtype=torch.uint8, device=dev)
-        self._gemm_ws_side = torch.empty(gws, dtype=torch.uint8, device=dev)
+        # split-K workspaces belong to this batch size: a hipGraph captured for it keeps
+        # their addresses, and the main and side streams never share one
+        bufs["gemm_ws"] = torch.empty(gws, dtype=torch.uint8, device=dev)
+        bufs["gemm_ws_side"] = torch.empty(gws, dtype=torch.uint8, device=dev)
         # three gradient buffers: a weight-gradient GEMM on the side stream may still read
         # g_l while the main stream's next two data-gradient GEMMs produce g_{l-1}, g_{l-2}
         bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(3)]
@@ -383,6 +388,7 @@ class DLRMTrainer:
         Bl = batch.X.shape[0]
         B = Bl * self.world
         bufs = self._buffers(Bl, B)
+        self._cur = bufs
         prof = profile or (lambda name: _NullCtx())
         self._prof = prof
         fused_opt = self.grads is None  # single GPU SGD: updates fused into backward
@@ -412,7 +418,7 @@ class DLRMTrainer:
         with prof("tbe_fwd"):
             if self.T_local > 0:
                 ops.tbe_forward(self.weights, self.row_base, self.T_local, B, batch.indices,
-                                batch.offsets, out=bufs["E"])
+                                batch.offsets, out=bufs["E"], error_flag=self.tbe_error_flag)
         work = None
         if self.world > 1:
             work = self._alltoall_fwd(bufs, Bl)
@@ -514,7 +520,8 @@ class DLRMTrainer:
                                  batch.indices, batch.offsets, bufs["dE"], lr=elr,
                                  eps=cfg.adagrad_eps, momentum=self.momentum,
                                  workspace=self._ws_tbe(batch.indices.numel()),
-                                 max_lookups_per_table=batch.max_per_table)
+                                 max_lookups_per_table=batch.max_per_table,
+                                 error_flag=self.tbe_error_flag)
         if conc:
             join()
         if ar is not None:
@@ -532,10 +539,17 @@ class DLRMTrainer:
         self.step_count += 1
         return bufs["prob"], bufs["loss"]
 
+    def check_errors(self) -> None:
+        """Raise (ops.TBEIndexError / ValueError) if any step since the last check hit an
+        index outside its table or exceeded max_per_table; synchronises the device.  The
+        reference's EmbeddingBag raises IndexError at the bad lookup itself."""
+        ops.check_tbe_errors(self.tbe_error_flag)
+
     # -------------------------------------------------------------- pieces --
     def _gemm(self, *args, side=False, **kw):
         with self._prof("gemm"):
-            ops.gemm(*args, workspace=self._gemm_ws_side if side else self._gemm_ws, **kw)
+            ops.gemm(*args, workspace=self._cur["gemm_ws_side" if side else "gemm_ws"],
+                     **kw)
 
     def _colsum(self, *args, **kw):
         with self._prof("colsum"):

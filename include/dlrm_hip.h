@@ -79,9 +79,19 @@ enum dlrm_epilogue {
 
 enum dlrm_loss { DLRM_LOSS_MSE = 0, DLRM_LOSS_BCE = 1 };
 
+/* Bits a TBE launch ORs into its device error_flag (int32; the caller zeroes it and
+ * reads it when convenient — the launches never synchronise). */
+enum dlrm_tbe_error {
+  DLRM_TBE_ERR_INDEX = 1,    /* an index outside [0, rows of its table): the lookup
+                                contributed nothing / received no update             */
+  DLRM_TBE_ERR_TABLE_CAP = 2 /* backward: a table had more lookups than the caller's
+                                max_lookups_per_table; that table was not updated     */
+};
+
 enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
 
 /* ---------------------------------------------------------------- library -- */
+/* 2: the TBE backward entry points take an error_flag (round 2). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 
@@ -95,8 +105,8 @@ const char* dlrm_last_error(void);
  * rows (device, int32 or int64 by index_bits).
  *   out[b*out_batch_stride + t*D + d] = sum_l w_l * W[row_base[t] + indices[l]][d]
  * (w_l = per_sample_weights[l], or 1 when per_sample_weights == NULL), summed in
- * lookup order in fp32.  An out-of-range index contributes nothing and sets
- * *error_flag = 1 (error_flag may be NULL).
+ * lookup order in fp32.  An out-of-range index contributes nothing and ORs
+ * DLRM_TBE_ERR_INDEX into *error_flag (error_flag may be NULL).
  */
 int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base, int32_t T,
                      int32_t B, const void* indices, int32_t index_bits, const void* offsets,
@@ -116,7 +126,10 @@ size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows,
  * max_lookups_per_table: an upper bound on the lookups of any single table in this
  * call (B*L for fixed bag size L), or 0 if unknown.  With 32-bit row ids and a bound
  * <= 4096 each table is sorted in LDS by one workgroup; otherwise a device-wide radix
- * sort is used.  A bound smaller than the real maximum is a contract violation.
+ * sort is used.  A bound smaller than the real maximum is a contract violation: the
+ * offending table is skipped and DLRM_TBE_ERR_TABLE_CAP is set in *error_flag.
+ * Out-of-range indices are skipped and set DLRM_TBE_ERR_INDEX (the reference's
+ * EmbeddingBag raises IndexError there).  error_flag may be NULL.
  * (The same applies to the two functions below.)
  */
 int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, int32_t T,
@@ -125,7 +138,7 @@ int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, in
                           int64_t total_rows, const float* per_sample_weights,
                           const float* grad_out, int64_t grad_batch_stride, float lr,
                           int64_t max_lookups_per_table, void* workspace,
-                          size_t workspace_bytes, dlrm_stream_t stream);
+                          size_t workspace_bytes, int32_t* error_flag, dlrm_stream_t stream);
 
 /*
  * Row-wise sparse Adagrad (RWSAdagrad, optim/rwsadagrad.py:92-115) fused into the
@@ -141,7 +154,8 @@ int dlrm_tbe_backward_rowwise_adagrad(float* weights, float* momentum, int64_t D
                                       const float* per_sample_weights, const float* grad_out,
                                       int64_t grad_batch_stride, float lr, float eps,
                                       int64_t max_lookups_per_table, void* workspace,
-                                      size_t workspace_bytes, dlrm_stream_t stream);
+                                      size_t workspace_bytes, int32_t* error_flag,
+                                      dlrm_stream_t stream);
 
 /*
  * Dense (non-fused) embedding-bag gradient scatter: grad_weights[row] += w_l * g
@@ -154,7 +168,7 @@ int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_b
                             int64_t total_rows, const float* per_sample_weights,
                             const float* grad_out, int64_t grad_batch_stride,
                             int64_t max_lookups_per_table, void* workspace,
-                            size_t workspace_bytes, dlrm_stream_t stream);
+                            size_t workspace_bytes, int32_t* error_flag, dlrm_stream_t stream);
 
 /*
  * Sparse-gradient values of an EmbeddingBag(sparse=True) backward

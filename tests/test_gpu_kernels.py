@@ -449,3 +449,48 @@ def test_uniform_fill(ops):
     i = torch.empty(1 << 20, dtype=torch.int32, device=dev)
     ops.uniform_int_fill_(i, 1000, 9)
     assert i.min().item() >= 0 and i.max().item() == 999
+
+
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
+def test_tbe_backward_table_cap_violation_is_skipped_and_flagged(ops, mode):
+    """A caller bound below a table's real lookup count (contract violation):
+    the per-table sort must not leave stale keys behind.  That table is skipped and flagged
+    (TBE_ERR_TABLE_CAP); the other tables are updated exactly as without the bound."""
+    torch.manual_seed(3)
+    rows, D, B = [1000, 300, 50], 32, 2048
+    T = len(rows)
+    L = [1, 3, 1]  # table 1 has 6144 > 4096 lookups
+    lo = [torch.arange(B) * L[t] for t in range(T)]
+    li = [torch.randint(0, rows[t], (B * L[t],)) for t in range(T)]
+    off, idx = O.batched_csr(lo, li)
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    G = torch.randn(B, T, D, device=dev)
+    W0 = torch.randn(sum(rows), D, device=dev)
+    mom0 = torch.rand(sum(rows), device=dev)
+    out = []
+    for mx in (0, 2048):  # exact (device sort) vs underestimated bound
+        W, mom = W0.clone(), mom0.clone()
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops.tbe_backward(mode, W, row_base, T, B, idx.to(dev), off.to(dev), G, lr=0.3,
+                         eps=1e-8, momentum=mom, max_lookups_per_table=mx, error_flag=flag)
+        out.append((W.cpu(), mom.cpu(), int(flag.item())))
+    (Wa, ma, fa), (Wb, mb, fb) = out
+    assert fa == 0 and fb == ops.TBE_ERR_TABLE_CAP
+    a1, b1 = int(row_base[1]), int(row_base[2])
+    assert torch.equal(Wb[a1:b1], W0.cpu()[a1:b1])  # skipped table untouched
+    assert torch.equal(mb[a1:b1], mom0.cpu()[a1:b1])
+    for s, e in ((0, a1), (b1, sum(rows))):  # the others: same values as the exact run
+        ok, msg = fp32_close(Wb[s:e].numpy(), Wa[s:e].numpy())
+        assert ok, msg
+
+
+def test_module_lookup_raises_index_error(ops):
+    """The drop-in EmbeddingBag path raises IndexError like nn.EmbeddingBag."""
+    from dlrm_hip.modules import TableBatchedEmbeddingBags
+    m = TableBatchedEmbeddingBags(2, [10, 20], 8).to(dev)
+    off = torch.tensor([0, 1, 2, 3, 4], dtype=torch.int32, device=dev)
+    idx = torch.tensor([1, 2, 3, 4], dtype=torch.int32, device=dev)
+    assert m(idx, off).shape == (2, 2, 8)
+    bad = torch.tensor([1, 10, 3, 4], dtype=torch.int32, device=dev)  # 10 >= rows of table 0
+    with pytest.raises(IndexError):
+        m(bad, off)

@@ -173,3 +173,48 @@ def test_side_stream_schedule_matches_serial(graph):
                     tr._bufs[(512, 512)]["prob"].cpu().clone()))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_batch_size_changes_with_overlaps_match_serial():
+    """B, a smaller B', then B again (a short last Criteo block does this) with every side-
+    stream overlap on: each batch size keeps its own split-K workspaces, so the result is
+    bitwise the serial schedule's (a shared workspace raced between streams)."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES["c3_small"]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function="bce",
+                        learning_rate=0.1)
+    res = []
+    for conc in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=13)
+        tr.concurrent = conc
+        tr.overlaps = {"fwd", "top", "bot"}
+        seq = [tr.synthetic_batch(B, 1, seed=s) for s, B in enumerate((2048, 1000, 2048, 1000))]
+        for b in seq:
+            tr.step(b)
+        torch.cuda.synchronize()
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
+                    tr._bufs[(2048, 2048)]["prob"].cpu().clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_out_of_range_index_is_flagged():
+    """The reference's EmbeddingBag raises IndexError on a bad index; the fused step skips
+    the lookup, flags it on the device, and check_errors() raises."""
+    from dlrm_hip import ops
+    DLRMTrainer, TrainerConfig = _trainer()
+    rows, D = [100, 50], 8
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=[13, 16, 8], ln_top=[_num_int(2, D), 8, 1],
+                        loss_function="bce", learning_rate=0.1)
+    tr = DLRMTrainer(cfg, device=dev, seed=1)
+    rng = np.random.RandomState(0)
+    X, lS_o, lS_i, T = _rand_batch(rng, rows, 16, 1, 13, "bce")
+    tr.step(tr.make_batch(X, lS_o, lS_i, T))
+    tr.check_errors()  # clean batch: no error
+    lS_i[1][3] = 50    # == rows of table 1
+    tr.step(tr.make_batch(X, lS_o, lS_i, T))
+    with pytest.raises(ops.TBEIndexError):
+        tr.check_errors()
+    tr.check_errors()  # the flag was reset
