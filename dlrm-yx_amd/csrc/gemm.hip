@@ -1,30 +1,39 @@
 // Exact-fp32 GEMM with fused epilogues on the gfx950 fp32 matrix core
-// (v_mfma_f32_32x32x2_f32: 64 FLOP/clk/SIMD, k-ordered fmaf chain, no xf32).
+// (v_mfma_f32_16x16x4_f32 / 32x32x2_f32: 64 FLOP/clk/SIMD, k-ordered fmaf chain, no xf32).
 //
 // Serves the DLRM MLPs (DLRM_Net.create_mlp / apply_mlp, dlrm_s_pytorch.py:227-265,
 // 518-524): Linear forward with bias(+ReLU) fused, dgrad with the ReLU mask of the
 // previous activation fused, wgrad with the SGD update fused (single GPU) or stored
 // into the flat gradient bucket (multi GPU, all-reduced before the update).
 //
-// Structure: 256-thread workgroups = 4 waves in a 2x2 arrangement, each wave owning a
-// (BM/2)x(BN/2) sub-tile of 32x32 MFMA accumulators (16 AGPRs each).  K is staged
-// BK deep through double-buffered LDS.  The k-order inside a K-tile is permuted so
-// that a lane's operands are CONTIGUOUS: lane (l, h) (l = lane & 31, h = lane >> 5)
-// feeds k = h*BK/2 + s at MFMA step s, for both operands, so
-//   * an operand that is k-contiguous in HBM (X rows, nn.Linear W rows) is staged
-//     [mn][k] with float4 loads + ds_write_b128 and its fragments are ds_read_b128
-//     (16 k-values in 4 instructions);
-//   * an mn-contiguous operand is staged [k][mn] (float4 along mn, ds_write_b128) and
-//     read with conflict-free ds_read_b32 (32 consecutive floats per half-wave).
-// The next K-tile is fetched into registers before the MFMAs of the current one and
-// written after them (one barrier per K-tile).  Workgroups are remapped bijectively
-// so each XCD (private 4 MiB L2) receives a contiguous run of output tiles.
+// Main kernel (gemm_group_kernel): up to four INDEPENDENT GEMMs in one launch (a grouped
+// GEMM: e.g. the dgrad of layer l beside the wgrad of layer l+1, which read the same
+// gradient and write different buffers), each with its own operand layout, epilogue and
+// K split.  Workgroups are 256 threads = 4 waves in a 2x2 arrangement, each wave owning
+// a (BM/2)x(BN/2) sub-tile of 16x16 accumulators, software-pipelined over BK = 32:
+//   * the fragments of K-tile t are in registers before its MFMAs start;
+//   * while tile t multiplies, tile t+1 (fetched one iteration earlier) is written to the
+//     other LDS buffer one float4 per k-step and each freed register is refilled with
+//     tile t+2 (raw buffer loads: out-of-range float4s read as zeros, no branches);
+//   * one barrier per K-tile, then tile t+1's fragments are read under the last k-step.
+// The k-order inside a K-tile is permuted so a lane's operands are CONTIGUOUS: an
+// operand that is k-contiguous in HBM (X rows, nn.Linear W rows) is staged [mn][k] and
+// read with ds_read_b128; an mn-contiguous one is staged [k][mn] and read with
+// conflict-free ds_read_b32.  The grid is remapped bijectively so each XCD (private
+// 4 MiB L2) receives a contiguous run of blocks: neighbouring tiles of one problem, and
+// all the K splits of one tile.
 //
-// DLRM's GEMMs are small for 256 CUs (M = batch <= 2048, N,K <= 1024) and the weight
-// gradients have a long K (= the batch) over a small M x N: the planner may split K;
-// split partials go to a caller workspace and a reduce kernel sums them IN SPLIT ORDER
-// (deterministic) and applies the epilogue.  Tile / BK / split per shape come from
-// on-device sweeps (tools/gemm_sweep.py), with a heuristic for other shapes.
+// Bias as a row sum: the wgrad of a Linear layer with its bias stored as an extra weight
+// column (bias folding, trainer layout) needs db[m] = sum_k dY(k, m) = (op(A) . 1)[m].
+// With ones_col >= 0 the kernel accumulates the A fragments it already holds (one VALU
+// add per fragment, beside the MFMAs) and writes C[m][ones_col] = epi(alpha * db[m]), so
+// N stays the weight width (1024, not 1028: no mostly-empty 17th column of tiles).
+//
+// Split-K inside the launch: split workgroups store their fp32 partial tile (and row
+// sums) into a per-(tile, split) record in fragment order (every lane writes and reads
+// 64 contiguous bytes); the LAST workgroup of a tile to finish (agent-scope ticket) sums
+// the records IN SPLIT ORDER - deterministic, and bitwise the sum a separate reduce over
+// s = 0..S-1 would give - and applies the epilogue.  No reduce launch.
 #include <cstdlib>
 #include <cstring>
 
@@ -36,7 +45,9 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 constexpr int kThreads = 256;
 constexpr int kMaxSplit = 32;
-constexpr int kMinSplitK = 128;
+constexpr int kMaxGroup = 4;
+constexpr int64_t kTicketCap = 16384;  // int32 tickets in the fixed 64 KiB workspace head
+constexpr int kBK = 32;
 
 struct GemmParams {
   int64_t M, N, K;
@@ -51,9 +62,23 @@ struct GemmParams {
   const float* bias;
   const float* aux;
   int64_t ldaux;
+  int64_t ones_col;  // >= 0: C[m][ones_col] = epi(alpha * sum_k op(A)(m, k))
+  int layout;        // 0: A,B k-contiguous  1: A k-contig, B mn  2: A,B mn  3: A mn, B k-contig
   int tiles_m, tiles_n;
-  int64_t kchunk;  // K range per split (multiple of BK)
-  float* ws;       // split partials [splits][M][N] (splits > 1 only)
+  int splits;        // K splits per output tile (1 = no split)
+  int block0;        // first (virtual) block of this problem in its launch
+  int64_t kchunk;    // K range per split (multiple of kBK)
+  float* ws;         // split records [tile][split][BM*BN + BM] (splits > 1)
+  int* counters;     // per-tile arrival tickets (splits > 1; zero between launches)
+  int pub;           // split-K hand-off: 0 = release/acquire fences, 1 = write-through (sc1)
+  int mode;          // DLRM_GEMM_FULL / _PARTIAL (split partials -> part) / _REDUCE
+  float* part;       // PARTIAL/REDUCE: [splits][M][N] fp32, then [splits][M] row sums
+};
+
+struct GemmGroup {
+  GemmParams p[kMaxGroup];
+  int n;
+  int total;  // blocks in the launch
 };
 
 // One operand's (MN x BKT) panel, staged global -> registers -> LDS.
@@ -150,6 +175,33 @@ struct Stage {
     regs[v] = __builtin_bit_cast(float4, t);
   }
 
+  // Pipelined fetch with per-thread offsets precomputed once (32-bit, bytes, at K-tile 0 of
+  // the split) so a K-tile costs one add + one compare per float4.  Out-of-range float4s
+  // read as zeros: rows/columns past the operand are outside the buffer descriptor except
+  // (KC) the columns k >= K of a row and (!KC) the columns mn >= MN of a row, masked here.
+  struct Fetch {
+    int off[NV];   // byte offset at tile 0 (or -1: masked for every tile)
+    int kpos[NV];  // KC: the float4's k within a K-tile
+  };
+  __device__ __forceinline__ void fetch_init(Fetch& f, int64_t ld, int64_t mn0, int64_t mnlim,
+                                             int64_t kbeg, int tid) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      int mn, k;
+      coords(tid + v * NT, mn, k);
+      const int64_t gmn = mn0 + mn, gk = kbeg + k;
+      const int64_t e = KC ? gmn * ld + gk : gk * ld + gmn;
+      f.off[v] = (KC || gmn < mnlim) ? (int)(e * 4) : -1;
+      f.kpos[v] = k;
+    }
+  }
+  __device__ __forceinline__ void fetch4(int v, const Fetch& f, __amdgpu_buffer_rsrc_t rsrc,
+                                         int tile_step, int t, int kt0, int klim) {
+    const bool ok = f.off[v] >= 0 && (!KC || kt0 + f.kpos[v] < klim);
+    const int off = ok ? f.off[v] + t * tile_step : 0x7ffffff0;
+    regs[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+  }
+
   __device__ __forceinline__ void store_one(int v, float* __restrict__ lds, int tid) const {
     int mn, k;
     coords(tid + v * NT, mn, k);
@@ -190,8 +242,16 @@ struct Stage {
   }
 };
 
+// One scalar f32 add the SLP vectorizer cannot fuse into v_pk_add_f32 (a packed f32 op
+// beside MFMAs costs ~26 cycles per MFMA gap on gfx950; a plain v_add_f32 is ~free).
+__device__ __forceinline__ float add_f32(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  // Contiguous tile runs per XCD (blocks b and b+8 share an XCD); bijective for any nwg.
+  // Contiguous block runs per XCD (blocks b and b+8 share an XCD); bijective for any nwg.
   const int xcd = bid % 8;
   const int q = nwg / 8, r = nwg % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
@@ -226,302 +286,144 @@ __device__ __forceinline__ void apply_epilogue(const GemmParams& p, int64_t row,
   *cp = v;
 }
 
-// KS = 1: 4 waves (2x2) share the K-tile.  KS = 2: 8 waves, two k-groups of 4; group g
-// takes k in [g*BK/2, (g+1)*BK/2) of every K-tile (twice the waves per SIMD for the
-// same output tile, no extra global traffic) and the groups' accumulators are summed
-// through LDS in group order before the epilogue.
-template <int BM, int BN, int BKT, int KS, bool A_KC, bool B_KC, bool VEC>
-__global__ __launch_bounds__(kThreads * KS, (BM * BN * KS >= 128 * 128 * 2 || BKT >= 64) ? 1 : 2)
-void gemm_f32_mfma_kernel(GemmParams p) {
-  constexpr int NT = kThreads * KS;
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int KW = BKT / KS;   // k per wave per K-tile
-  constexpr int NSTEP = KW / 2;  // MFMA k-steps per wave per K-tile
-  constexpr int CH = NSTEP < 16 ? NSTEP : 16;
-  using SA = Stage<BM, BKT, A_KC, VEC, NT>;
-  using SB = Stage<BN, BKT, B_KC, VEC, NT>;
-  static_assert(KS == 1 || 2 * (SA::SIZE + SB::SIZE) >= BM * BN, "LDS too small for k-group sum");
-  __shared__ __attribute__((aligned(16))) float smem[2 * (SA::SIZE + SB::SIZE)];
-  float* As0 = smem;
-  float* Bs0 = smem + SA::SIZE;
-  float* As1 = smem + SA::SIZE + SB::SIZE;
-  float* Bs1 = As1 + SA::SIZE;
 
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tm = wg / p.tiles_n;
-  const int tn = wg - tm * p.tiles_n;
-  const int64_t m0 = (int64_t)tm * BM;
-  const int64_t n0 = (int64_t)tn * BN;
-  const int split = blockIdx.y;
-  const int64_t kbeg = (int64_t)split * p.kchunk;
-  const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
-
+// Split-K completion.  Each split workgroup stores its NV accumulators (fragment order,
+// thread-major: rec[tid*NV + q]) and its row sums (rec[BM*BN + local row]) into its
+// record, then takes a ticket; the last arriver sums every split's record in split order
+// and applies the epilogue.  Publication is the agent-scope release/acquire hand-off
+// (per-XCD L2s are not coherent): plain stores -> s_waitcnt vmcnt(0) -> barrier ->
+// release fence -> vmcnt(0) -> relaxed agent ticket; last arriver: acquire fence ->
+// vmcnt(0) -> barrier -> plain loads (unconditional, two splits in flight).  The last
+// arriver resets the tile's ticket for the next launch.  Returns true in the workgroup
+// that must write the output (always when unsplit); v / rs then hold the full sums.
+template <int BM, int BN, int NV, int FM>
+__device__ __forceinline__ bool splitk_reduce(const GemmParams& p, int tile, int split,
+                                              float (&v)[NV], float (&rs)[FM], int rs_row0,
+                                              int rs_stride, bool rs_owner, float* smem) {
+  if (p.splits <= 1 || p.pub == 2) return true;  // (pub 2: timing probe only, wrong sums)
+  constexpr int REC = BM * BN + BM;
+  static_assert(NV % 4 == 0, "record chunks are float4");
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
   const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int kg = wave >> 2;  // k-group
-  const int wq = wave & 3;
-  const int lane = tid & 63;
-  const int h = lane >> 5;
-  const int l32 = lane & 31;
-  const int wm0 = (wq >> 1) * WM;
-  const int wn0 = (wq & 1) * WN;
-
-  // A single 32x32 accumulator per wave would be one dependent MFMA chain (64-cycle
-  // issue == 64-cycle accumulate latency: any bubble stalls the wave); such waves
-  // alternate two chains over the k-steps and add them at the end.
-  constexpr int NCH = (TM * TN >= 2) ? 1 : 2;
-  f32x16 acc[TM][TN], acc2[TM][TN];
+  const bool wt = p.pub == 1;  // write-through records: no fences (MI355X guide, sc1 form)
+  float* tile_base = p.ws + (int64_t)tile * p.splits * REC;
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)tile_base, (short)0, (int)(p.splits * REC * 4), 0x00020000);
+  float* rec = tile_base + (int64_t)split * REC;
+  if (wt) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = acc2[i][j][r] = 0.f;
-
-  SA sa;
-  SB sb;
-  const int64_t nk = (kend - kbeg + BKT - 1) / BKT;
-  if (nk > 0) {
-    sa.load(p.A, p.lda, m0, p.M, kbeg, kend, tid);
-    sb.load(p.B, p.ldb, n0, p.N, kbeg, kend, tid);
-    sa.store(As0, tid);
-    sb.store(Bs0, tid);
-  }
-  __syncthreads();
-
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const bool odd = kt & 1;
-    const float* As = odd ? As1 : As0;
-    const float* Bs = odd ? Bs1 : Bs0;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      sa.load(p.A, p.lda, m0, p.M, kbeg + (kt + 1) * BKT, kend, tid);
-      sb.load(p.B, p.ldb, n0, p.N, kbeg + (kt + 1) * BKT, kend, tid);
+    for (int q = 0; q < NV; q += 4) {
+      const float4 f = make_float4(v[q], v[q + 1], v[q + 2], v[q + 3]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), rr,
+                                             (split * REC + tid * NV + q) * 4, 0, 16 /*sc1*/);
     }
-#pragma unroll
-    for (int sub = 0; sub < NSTEP / CH; ++sub) {
-      const int kbase = kg * KW + h * NSTEP + sub * CH;
-      float a[TM][CH], b[TN][CH];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) sa.template frag<CH>(As, wm0 + i * 32, l32, kbase, a[i]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) sb.template frag<CH>(Bs, wn0 + j * 32, l32, kbase, b[j]);
-#pragma unroll
-      for (int s = 0; s < CH; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            if (NCH == 2 && (s & 1))
-              acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc2[i][j], 0, 0, 0);
-            else
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
-          }
-    }
-    if (more) {
-      sa.store(odd ? As0 : As1, tid);
-      sb.store(odd ? Bs0 : Bs1, tid);
-    }
-    __syncthreads();
-  }
-
-  if constexpr (NCH == 2) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] += acc2[i][j];
-  }
-  if constexpr (KS == 2) {
-    // group 1 hands its accumulators to group 0 through LDS (free after the last barrier)
-    float* red = smem + (size_t)wq * (WM * WN);
-    if (kg == 1) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) red[((i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
-    }
-    __syncthreads();
-    if (kg == 1) return;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] += red[((i * TN + j) * 16 + r) * 64 + lane];
-  }
-
-  // Epilogue: accumulator register r of a 32x32 tile holds
-  //   row (r&3) + 8*(r>>2) + 4*(lane>>5), column lane&31.
-  const bool partial = gridDim.y > 1;
-  float* wsp = partial ? p.ws + (int64_t)split * p.M * p.N : nullptr;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = n0 + wn0 + j * 32 + l32;
-      if (col >= p.N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= p.M) continue;
-        if (partial)
-          wsp[row * p.N + col] = acc[i][j][r];
-        else
-          apply_epilogue(p, row, col, p.alpha * acc[i][j][r]);
-      }
-    }
-  }
-}
-
-// 16x16x4 variant: v_mfma_f32_16x16x4_f32 (32-cycle issue, 40-cycle accumulate latency)
-// with FM x FN independent 16x16 accumulators per wave, so a single wave per SIMD keeps
-// the matrix pipe busy.  Lane l feeds row/col l & 15 and k = (l >> 4) * BK/4 + s at
-// step s (BK/4 contiguous k per lane: two ds_read_b128 per k-contiguous fragment).
-template <int BM, int BN, bool A_KC, bool B_KC, bool VEC>
-__global__ __launch_bounds__(kThreads, 2) void gemm_f32_mfma16_kernel(GemmParams p) {
-  constexpr int BKT = 32;
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int KL = BKT / 4;
-  using SA = Stage<BM, BKT, A_KC, VEC, kThreads>;
-  using SB = Stage<BN, BKT, B_KC, VEC, kThreads>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (SA::SIZE + SB::SIZE)];
-  float* As0 = smem;
-  float* Bs0 = smem + SA::SIZE;
-  float* As1 = smem + SA::SIZE + SB::SIZE;
-  float* Bs1 = As1 + SA::SIZE;
-
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tm = wg / p.tiles_n;
-  const int tn = wg - tm * p.tiles_n;
-  const int64_t m0 = (int64_t)tm * BM;
-  const int64_t n0 = (int64_t)tn * BN;
-  const int split = blockIdx.y;
-  const int64_t kbeg = (int64_t)split * p.kchunk;
-  const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
-
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-  const int kq = lane >> 4;
-  const int l16 = lane & 15;
-  const int wm0 = (wave >> 1) * WM;
-  const int wn0 = (wave & 1) * WN;
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // Two-deep register ring: tile t+2 is in flight while tile t is multiplied and tile
-  // t+1 is written to LDS, so each global load has two MFMA blocks to arrive.
-  const int64_t nk = (kend - kbeg + BKT - 1) / BKT;
-  SA ra0, ra1;
-  SB rb0, rb1;
-  auto fetch = [&](SA& ra, SB& rb, int64_t t) {
-    if (t < nk) {
-      ra.load(p.A, p.lda, m0, p.M, kbeg + t * BKT, kend, tid);
-      rb.load(p.B, p.ldb, n0, p.N, kbeg + t * BKT, kend, tid);
-    }
-  };
-  auto compute = [&](const float* As, const float* Bs) {
-    float a[FM][KL], b[FN][KL];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) ra0.template frag<KL>(As, wm0 + i * 16, l16, kq * KL, a[i]);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) rb0.template frag<KL>(Bs, wn0 + j * 16, l16, kq * KL, b[j]);
-#pragma unroll
-    for (int s = 0; s < KL; ++s)
+    if (rs_owner) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, rs[i]), rr,
+                                              (split * REC + BM * BN + rs_row0 + i * rs_stride) * 4,
+                                              0, 16);
+    }
+  } else {
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
-  };
-  fetch(ra0, rb0, 0);
-  fetch(ra1, rb1, 1);
-  if (nk > 0) {
-    ra0.store(As0, tid);
-    rb0.store(Bs0, tid);
+    for (int q = 0; q < NV; q += 4)
+      *reinterpret_cast<float4*>(rec + tid * NV + q) = make_float4(v[q], v[q + 1], v[q + 2], v[q + 3]);
+    if (rs_owner) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) rec[BM * BN + rs_row0 + i * rs_stride] = rs[i];
+    }
   }
-  fetch(ra0, rb0, 2);
+  if (p.pub == 3) return split == 0;  // (timing probe only: records stored, no hand-off)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int64_t kt = 0; kt < nk; kt += 2) {
-    compute(As0, Bs0);
-    if (kt + 1 < nk) {
-      ra1.store(As1, tid);
-      rb1.store(Bs1, tid);
+  if (tid == 0) {
+    if (!wt) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    fetch(ra1, rb1, kt + 3);
-    __syncthreads();
-    if (kt + 1 >= nk) break;
-    compute(As1, Bs1);
-    if (kt + 2 < nk) {
-      ra0.store(As0, tid);
-      rb0.store(Bs0, tid);
-    }
-    fetch(ra0, rb0, kt + 4);
-    __syncthreads();
-  }
-
-  // Epilogue: register r of a 16x16 accumulator holds row 4*(lane>>4) + r, col lane&15.
-  const bool partial = gridDim.y > 1;
-  float* wsp = partial ? p.ws + (int64_t)split * p.M * p.N : nullptr;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int64_t col = n0 + wn0 + j * 16 + l16;
-      if (col >= p.N) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
-        if (row >= p.M) continue;
-        if (partial)
-          wsp[row * p.N + col] = acc[i][j][r];
-        else
-          apply_epilogue(p, row, col, p.alpha * acc[i][j][r]);
+    const int t = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == p.splits - 1;
+    if (last) {
+      if (!wt) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    reinterpret_cast<volatile int*>(smem)[0] = last;
   }
+  __syncthreads();
+  if (!reinterpret_cast<volatile int*>(smem)[0]) return false;
+  const int rrow = rs_owner ? rs_row0 : 0;  // every lane loads (valid address), owners use it
+  auto load_rec = [&](int s, float4 (&t)[NV / 4], float (&tr)[FM]) {
+    const int o = s * REC;
+    if (wt) {  // every load of the records is an sc1 load
+#pragma unroll
+      for (int q = 0; q < NV / 4; ++q)
+        t[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rr, (o + tid * NV + 4 * q) * 4, 0, 16));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        tr[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rr, (o + BM * BN + rrow + i * rs_stride) * 4, 0, 16));
+    } else {
+      const float* r = tile_base + o;
+#pragma unroll
+      for (int q = 0; q < NV / 4; ++q)
+        t[q] = *reinterpret_cast<const float4*>(r + tid * NV + 4 * q);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) tr[i] = r[BM * BN + rrow + i * rs_stride];
+    }
+  };
+  auto add_rec = [&](const float4 (&t)[NV / 4], const float (&tr)[FM], bool first) {
+#pragma unroll
+    for (int q = 0; q < NV / 4; ++q) {
+      v[4 * q + 0] = first ? t[q].x : v[4 * q + 0] + t[q].x;
+      v[4 * q + 1] = first ? t[q].y : v[4 * q + 1] + t[q].y;
+      v[4 * q + 2] = first ? t[q].z : v[4 * q + 2] + t[q].z;
+      v[4 * q + 3] = first ? t[q].w : v[4 * q + 3] + t[q].w;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) rs[i] = first ? tr[i] : rs[i] + tr[i];
+  };
+  int s = 0;
+  for (; s + 1 < p.splits; s += 2) {
+    float4 t0[NV / 4], t1[NV / 4];
+    float r0[FM], r1[FM];
+    load_rec(s, t0, r0);
+    load_rec(s + 1, t1, r1);
+    add_rec(t0, r0, s == 0);
+    add_rec(t1, r1, false);
+  }
+  if (s < p.splits) {
+    float4 t0[NV / 4];
+    float r0[FM];
+    load_rec(s, t0, r0);
+    add_rec(t0, r0, s == 0);
+  }
+  return true;
 }
 
-// Software-pipelined 16x16x4 kernel (one barrier per K-tile, MFMAs kept dense):
-//   * the fragments of K-tile t are in registers before its MFMAs start (read from LDS
-//     at the end of iteration t-1, under the last MFMA step);
-//   * during the MFMAs of tile t, the staged registers of tile t+1 (fetched from HBM one
-//     iteration earlier) are written to the other LDS buffer one float4 per k-step, and
-//     each freed register is immediately refilled with tile t+2's float4;
-//   * one barrier, then tile t+1's fragments are read while the last k-step multiplies.
-template <int BM, int BN, bool A_KC, bool B_KC, bool VEC>
-__global__ __launch_bounds__(kThreads, BM * BN >= 128 * 64 ? 1 : 2)
-void gemm_f32_pipe_kernel(GemmParams p) {
-  constexpr int BKT = 32;
+// One output tile (and K split) of problem p: the software-pipelined 16x16x4 body.
+template <int BM, int BN, bool A_KC, bool B_KC, bool RS>
+__device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* smem) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int KL = BKT / 4;  // k-steps per K-tile (each lane group owns KL consecutive k)
-  using SA = Stage<BM, BKT, A_KC, VEC, kThreads>;
-  using SB = Stage<BN, BKT, B_KC, VEC, kThreads>;
+  constexpr int KL = kBK / 4;  // k-steps per K-tile (each lane group owns KL consecutive k)
+  using SA = Stage<BM, kBK, A_KC, true, kThreads>;
+  using SB = Stage<BN, kBK, B_KC, true, kThreads>;
   constexpr int NS = SA::NV + SB::NV;  // staged float4 per thread per K-tile
   static_assert(NS <= KL - 1, "staging must finish before the barrier step");
-  __shared__ __attribute__((aligned(16))) float smem[2 * (SA::SIZE + SB::SIZE)];
 
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tm = wg / p.tiles_n;
-  const int tn = wg - tm * p.tiles_n;
+  const int tile = lb / p.splits;
+  const int split = lb - tile * p.splits;
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
   const int64_t m0 = (int64_t)tm * BM;
   const int64_t n0 = (int64_t)tn * BN;
-  const int split = blockIdx.y;
   const int64_t kbeg = (int64_t)split * p.kchunk;
   const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
-  const bool mn_full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -536,11 +438,13 @@ void gemm_f32_pipe_kernel(GemmParams p) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rs[FM];  // row sums of op(A) over this lane's k (ones_col)
+#pragma unroll
+  for (int i = 0; i < FM; ++i) rs[i] = 0.f;
 
-  const int64_t nk = (kend - kbeg + BKT - 1) / BKT;
+  const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
   SA sa;
   SB sb;
-  (void)mn_full;
   // buffer descriptors over exactly the addressed extent (host guarantees < 2 GiB)
   const int64_t a_ext = A_KC ? (p.M - 1) * p.lda + p.K : (p.K - 1) * p.lda + p.M;
   const int64_t b_ext = B_KC ? (p.N - 1) * p.ldb + p.K : (p.K - 1) * p.ldb + p.N;
@@ -548,12 +452,18 @@ void gemm_f32_pipe_kernel(GemmParams p) {
       __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)(a_ext * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)(b_ext * 4), 0x00020000);
-  auto fetch_one = [&](int c, int64_t t) {  // staged float4 c of K-tile t (zeros past nk)
-    const int64_t k0 = kbeg + t * BKT;
+  typename SA::Fetch fa;
+  typename SB::Fetch fb;
+  sa.fetch_init(fa, p.lda, m0, p.M, kbeg, tid);
+  sb.fetch_init(fb, p.ldb, n0, p.N, kbeg, tid);
+  const int a_step = A_KC ? kBK * 4 : (int)(kBK * p.lda * 4);
+  const int b_step = B_KC ? kBK * 4 : (int)(kBK * p.ldb * 4);
+  const int kb32 = (int)kbeg, K32 = (int)p.K;
+  auto fetch_one = [&](int c, int t) {  // staged float4 c of K-tile t (unused past nk)
     if (c < SA::NV)
-      sa.load_one4(c, ra, p.lda, m0, p.M, k0, kend, tid);
+      sa.fetch4(c, fa, ra, a_step, t, kb32 + t * kBK, K32);
     else
-      sb.load_one4(c - SA::NV, rb, p.ldb, n0, p.N, k0, kend, tid);
+      sb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * kBK, K32);
   };
   auto put_one = [&](int c, float* buf) {
     if (c < SA::NV)
@@ -584,7 +494,7 @@ void gemm_f32_pipe_kernel(GemmParams p) {
   // One K-tile: MFMAs on (ca, cb) with the staging of tile t+1 / fetch of t+2 interleaved,
   // barrier, then tile t+1's fragments into (na, nb) under the last k-step.  The loop is
   // unrolled by two so the fragment sets ping-pong without register copies.
-  auto iteration = [&](int64_t kt, float (&ca)[FM][KL], float (&cb)[FN][KL], float (&na)[FM][KL],
+  auto iteration = [&](int kt, float (&ca)[FM][KL], float (&cb)[FN][KL], float (&na)[FM][KL],
                        float (&nb)[FN][KL]) {
     float* nbuf = smem + ((kt + 1) & 1) * (SA::SIZE + SB::SIZE);
 #pragma unroll
@@ -594,6 +504,10 @@ void gemm_f32_pipe_kernel(GemmParams p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][s], cb[j][s], acc[i][j], 0, 0, 0);
+      if constexpr (RS) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][s]);
+      }
       if (s < NS) {
         put_one(s, nbuf);      // tile t+1 (staged last iteration) -> LDS
         fetch_one(s, kt + 2);  // refill the register with tile t+2
@@ -607,52 +521,254 @@ void gemm_f32_pipe_kernel(GemmParams p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][KL - 1], cb[j][KL - 1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][KL - 1], cb[j][KL - 1], acc[i][j],
+                                                         0, 0, 0);
+    if constexpr (RS) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][KL - 1]);
+    }
   };
   float a1[FM][KL], b1[FN][KL];
-  for (int64_t kt = 0; kt < nk; kt += 2) {
+  for (int kt = 0; kt < nk; kt += 2) {
     iteration(kt, a, b, a1, b1);
     if (kt + 1 >= nk) break;
     iteration(kt + 1, a1, b1, a, b);
   }
 
-  // Epilogue: register r of a 16x16 accumulator holds row 4*(lane>>4) + r, col lane&15.
-  const bool partial = gridDim.y > 1;
-  float* wsp = partial ? p.ws + (int64_t)split * p.M * p.N : nullptr;
+  // Row sums: lanes l16, l16+16, l16+32, l16+48 hold the four k-quarters of row l16
+  // (fixed pairing order: deterministic).  Owners: kq == 0 lanes of the left wave column,
+  // in the first column of tiles.
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
+    rs[i] += __shfl_xor(rs[i], 16, 64);
+    rs[i] += __shfl_xor(rs[i], 32, 64);
+  }
+  const bool rs_owner = RS && tn == 0 && (wave & 1) == 0 && kq == 0;
+
+  // Register r of a 16x16 accumulator holds row 4*(lane>>4) + r, col lane&15.
+  constexpr int NV = FM * FN * 4;
+  float v[NV];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[(i * FN + j) * 4 + r] = acc[i][j][r];
+  if (p.mode == DLRM_GEMM_PARTIAL) {
+    // raw partial sums for a REDUCE job of a later launch (the kernel boundary publishes)
+    float* slab = p.part + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t col = n0 + wn0 + j * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
+          if (row < p.M && col < p.N) slab[row * p.N + col] = v[(i * FN + j) * 4 + r];
+        }
+      }
+    if (rs_owner) {
+      float* rslab = p.part + (int64_t)p.splits * p.M * p.N + (int64_t)split * p.M;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int64_t row = m0 + wm0 + i * 16 + l16;
+        if (row < p.M) rslab[row] = rs[i];
+      }
+    }
+    return;
+  }
+  if (!splitk_reduce<BM, BN, NV, FM>(p, tile, split, v, rs, wm0 + l16, 16, rs_owner, smem))
+    return;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int64_t col = n0 + wn0 + j * 16 + l16;
-      if (col >= p.N) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
-        if (row >= p.M) continue;
-        if (partial)
-          wsp[row * p.N + col] = acc[i][j][r];
-        else
-          apply_epilogue(p, row, col, p.alpha * acc[i][j][r]);
+        if (row < p.M && col < p.N)
+          apply_epilogue(p, row, col, p.alpha * v[(i * FN + j) * 4 + r]);
       }
+    }
+  if (rs_owner) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int64_t row = m0 + wm0 + i * 16 + l16;
+      if (row < p.M) apply_epilogue(p, row, p.ones_col, p.alpha * rs[i]);
     }
   }
 }
 
-// Sum the split partials in split order, scale, apply the epilogue.
-__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmParams p, int splits) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// REDUCE job: C = epi(alpha * sum_s part[s]) in split order (the same additions as the
+// in-launch reduction), one float4 of the [M][N] slab per thread, then one row sum per
+// thread for ones_col.  Up to 8 splits' loads in flight.
+__device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
   const int64_t MN = p.M * p.N;
-  if (i >= MN) return;
-  float s = p.ws[i];
-  for (int k = 1; k < splits; ++k) s += p.ws[(int64_t)k * MN + i];
-  const int64_t row = i / p.N;
-  apply_epilogue(p, row, i - row * p.N, p.alpha * s);
+  const int64_t i = (int64_t)lb * kThreads + threadIdx.x;
+  const int64_t n4 = MN / 4;  // N % 4 == 0 (host check)
+  const int S = p.splits;
+  if (i < n4) {
+    const float4* src = reinterpret_cast<const float4*>(p.part) + i;
+    const int64_t stride = MN / 4;
+    float4 acc = src[0];
+    for (int s0 = 1; s0 < S; s0 += 8) {
+      float4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (s0 + u < S) t[u] = src[(int64_t)(s0 + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (s0 + u < S) {
+          acc.x += t[u].x;
+          acc.y += t[u].y;
+          acc.z += t[u].z;
+          acc.w += t[u].w;
+        }
+    }
+    const int64_t e = 4 * i, row = e / p.N, col = e - row * p.N;
+    apply_epilogue(p, row, col, p.alpha * acc.x);
+    apply_epilogue(p, row, col + 1, p.alpha * acc.y);
+    apply_epilogue(p, row, col + 2, p.alpha * acc.z);
+    apply_epilogue(p, row, col + 3, p.alpha * acc.w);
+  } else if (p.ones_col >= 0 && i - n4 < p.M) {
+    const int64_t row = i - n4;
+    const float* rsrc = p.part + (int64_t)S * MN + row;
+    float acc = rsrc[0];
+    for (int s = 1; s < S; ++s) acc += rsrc[(int64_t)s * p.M];
+    apply_epilogue(p, row, p.ones_col, p.alpha * acc);
+  }
 }
 
+template <int BM, int BN>
+constexpr int group_smem_floats() {
+  // the largest LDS image over the four operand layouts (double-buffered A and B panels)
+  return 2 * ((BM * (kBK + 4) > kBK * (BM + 4) ? BM * (kBK + 4) : kBK * (BM + 4)) +
+              (BN * (kBK + 4) > kBK * (BN + 4) ? BN * (kBK + 4) : kBK * (BN + 4)));
+}
+
+// Body kinds: the four operand layouts, plus 4 = layout 2 (wgrad) with the row sums.
+__host__ __device__ constexpr int kind_bit(int layout, bool rs) { return 1 << (rs ? 4 : layout); }
+
+// Up to kMaxGroup independent problems; block -> (problem, tile, split) after the XCD remap.
+// KINDS is the set of body kinds compiled in (a launch uses the smallest instantiation that
+// covers its problems: fewer bodies, fewer registers).
+template <int BM, int BN, int KINDS>
+__global__ __launch_bounds__(kThreads, 2) void gemm_group_kernel(const GemmGroup g) {
+  __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
+  // Problems own consecutive PHYSICAL block ranges, so each one is dealt round-robin over
+  // all eight XCDs (a remap across the whole launch would give each problem a few XCDs);
+  // inside its range the XCD remap gives each XCD a contiguous run of that problem's tiles.
+  const int b = blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxGroup; ++i)
+    if (i < g.n && b >= g.p[i].block0) q = i;
+  const GemmParams& p = g.p[q];
+  const int nq = (q + 1 < g.n ? g.p[q + 1].block0 : g.total) - p.block0;
+  const int lb = xcd_remap(b - p.block0, nq);
+  if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
+  const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
+  if constexpr ((KINDS & 1) != 0)
+    if (kind == 0) return pipe_body<BM, BN, true, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 2) != 0)
+    if (kind == 1) return pipe_body<BM, BN, true, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 4) != 0)
+    if (kind == 2) return pipe_body<BM, BN, false, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 8) != 0)
+    if (kind == 3) return pipe_body<BM, BN, false, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 16) != 0)
+    if (kind == 4) return pipe_body<BM, BN, false, false, true>(p, lb, smem);
+}
+
+// Fallback for operands the pipelined body cannot take (unaligned rows, ragged float4
+// extents, > 2 GiB extents): 32x32x2 MFMA, register-staged, unsplit, element-guarded.
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(kThreads, 2) void gemm_generic_kernel(const GemmParams p) {
+  constexpr int BM = 64, BN = 64, BKT = 32;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int NSTEP = BKT / 2;  // MFMA k-steps per wave per K-tile
+  using SA = Stage<BM, BKT, A_KC, false, kThreads>;
+  using SB = Stage<BN, BKT, B_KC, false, kThreads>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (SA::SIZE + SB::SIZE)];
+  float* As0 = smem;
+  float* Bs0 = smem + SA::SIZE;
+  float* As1 = smem + SA::SIZE + SB::SIZE;
+  float* Bs1 = As1 + SA::SIZE;
+  const int tile = xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n);
+  const int tm = tile / p.tiles_n, tn = tile - (tile / p.tiles_n) * p.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int wm0 = (wave >> 1) * WM, wn0 = (wave & 1) * WN;
+  f32x16 acc, acc2;  // two chains alternate over the k-steps (64-cycle accumulate latency)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
+  SA sa;
+  SB sb;
+  const int64_t nk = (p.K + BKT - 1) / BKT;
+  if (nk > 0) {
+    sa.load(p.A, p.lda, m0, p.M, 0, p.K, tid);
+    sb.load(p.B, p.ldb, n0, p.N, 0, p.K, tid);
+    sa.store(As0, tid);
+    sb.store(Bs0, tid);
+  }
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const bool odd = kt & 1;
+    const float* As = odd ? As1 : As0;
+    const float* Bs = odd ? Bs1 : Bs0;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(p.A, p.lda, m0, p.M, (kt + 1) * BKT, p.K, tid);
+      sb.load(p.B, p.ldb, n0, p.N, (kt + 1) * BKT, p.K, tid);
+    }
+    float a[NSTEP], b[NSTEP];
+    sa.template frag<NSTEP>(As, wm0, l32, h * NSTEP, a);
+    sb.template frag<NSTEP>(Bs, wn0, l32, h * NSTEP, b);
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+      if (s & 1)
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc2, 0, 0, 0);
+      else
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    }
+    if (more) {
+      sa.store(odd ? As0 : As1, tid);
+      sb.store(odd ? Bs0 : Bs1, tid);
+    }
+    __syncthreads();
+  }
+  acc += acc2;
+  // accumulator register r of a 32x32 tile: row (r&3) + 8*(r>>2) + 4*(lane>>5), col lane&31
+  const int64_t col = n0 + wn0 + l32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t row = m0 + wm0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (row < p.M && col < p.N) apply_epilogue(p, row, col, p.alpha * acc[r]);
+  }
+}
+
+// Fallback row sum (ones_col for the generic kernel): C[m][ones_col] =
+// epi(alpha * sum_k op(A)(m, k)); 64 rows x 4 k-slices per block, slices added in order.
+__global__ __launch_bounds__(kThreads) void gemm_rowsum_kernel(const GemmParams p, bool a_kc) {
+  __shared__ float part[4][64];
+  const int tid = threadIdx.x, r = tid & 63, ks = tid >> 6;
+  const int64_t m = (int64_t)blockIdx.x * 64 + r;
+  float s = 0.f;
+  if (m < p.M)
+    for (int64_t k = ks; k < p.K; k += 4) s += a_kc ? p.A[m * p.lda + k] : p.A[k * p.lda + m];
+  part[ks][r] = s;
+  __syncthreads();
+  if (ks == 0 && m < p.M)
+    apply_epilogue(p, m, p.ones_col, p.alpha * (((part[0][r] + part[1][r]) + part[2][r]) + part[3][r]));
+}
+
+// ------------------------------------------------------------------- planning --
 struct Plan {
-  int bm, bn, bk, splits;
-  int64_t kchunk;
-  int ks = 1;
+  int splits = 1;
+  int64_t kchunk = 0;
 };
 
 int env_int(const char* name, int dflt) {
@@ -660,124 +776,343 @@ int env_int(const char* name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
-Plan finish_plan(int bm, int bn, int bk, int64_t s, int64_t K) {
-  int64_t smax = K / kMinSplitK;
-  if (s > smax) s = smax;
+Plan make_plan(int64_t s, int64_t K) {
   if (s > kMaxSplit) s = kMaxSplit;
+  int64_t smax = dlrm::ceil_div(K, kBK);
+  if (s > smax) s = smax;
   if (s < 1) s = 1;
-  int64_t kchunk = dlrm::ceil_div(dlrm::ceil_div(K, s), bk) * bk;
-  if (kchunk < bk) kchunk = bk;
-  s = dlrm::ceil_div(K, kchunk);
-  if (s < 1) s = 1;
-  return {bm, bn, bk, (int)s, kchunk};
+  int64_t kchunk = dlrm::ceil_div(dlrm::ceil_div(K, s), kBK) * kBK;
+  if (kchunk < kBK) kchunk = kBK;
+  Plan pl;
+  pl.splits = (int)dlrm::ceil_div(K, kchunk);
+  pl.kchunk = kchunk;
+  return pl;
 }
 
-bool valid_cfg(int bm, int bn, int bk, int ks) {
-  const bool tile = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
-  if (ks == 16) return tile && bk == 32;
-  if (ks == 32) return tile && bk == 32 && bm * bn <= 128 * 64;
-  if (ks == 2) return tile && bk == 32 || (bm == 64 && bn == 64 && bk == 64);
-  return ks == 1 && tile && (bk == 32 || bk == 64);
+struct Desc {  // one problem as the host sees it
+  int32_t trans_a, trans_b;
+  int64_t M, N, K;
+  float alpha;
+  const float *A, *B;
+  int64_t lda, ldb;
+  float* C;
+  int64_t ldc;
+  int32_t epi;
+  const float* bias;
+  const float* aux;
+  int64_t ldaux;
+  int64_t ones_col;
+  int32_t mode = DLRM_GEMM_FULL;
+  int32_t splits = 0;
+  float* part = nullptr;
+};
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// The pipelined body moves whole float4s through 32-bit buffer offsets.
+bool pipe_ok(const Desc& d) {
+  const bool a_kc = !d.trans_a, b_kc = d.trans_b != 0;
+  const int64_t a_ext = a_kc ? (d.M - 1) * d.lda + d.K : (d.K - 1) * d.lda + d.M;
+  const int64_t b_ext = b_kc ? (d.N - 1) * d.ldb + d.K : (d.K - 1) * d.ldb + d.N;
+  return aligned16(d.A) && aligned16(d.B) && d.lda % 4 == 0 && d.ldb % 4 == 0 && d.K % 4 == 0 &&
+         (a_kc || d.M % 4 == 0) && (b_kc || d.N % 4 == 0) && a_ext * 4 < 0x7ff00000LL &&
+         b_ext * 4 < 0x7ff00000LL;
+}
+
+int layout_of(const Desc& d) {
+  const bool a_kc = !d.trans_a, b_kc = d.trans_b != 0;
+  return a_kc ? (b_kc ? 0 : 1) : (b_kc ? 3 : 2);
 }
 
 struct PlanEntry {
   int64_t M, N, K;
-  int ta, tb, bm, bn, bk, split, ks;
+  int layout, bm, bn, split;
 };
 
-// Measured plans for the DLRM step shapes (exact match), from tools/gemm_sweep.py.
+// Measured plans for the DLRM step shapes of single-problem launches (exact match), from
+// tools/gemm_sweep.py on MI355X.
 constexpr PlanEntry kPlans[] = {
 #include "gemm_plans.inc"
+    {0, 0, 0, 0, 64, 64, 1},  // sentinel (never matches: M = 0)
 };
 
-// Tuning overrides (read per call, for sweeps): DLRM_GEMM_CFG=<BM>x<BN>x<BK>,
-// DLRM_GEMM_SPLIT=<n>, DLRM_GEMM_TARGET=<workgroups>.
-Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc) {
-  const int force_split = env_int("DLRM_GEMM_SPLIT", 0);
-  const char* cfg = getenv("DLRM_GEMM_CFG");
-  if (cfg && *cfg) {
-    int bm = 64, bn = 64, bk = 32, ks = 1;
-    const int n = sscanf(cfg, "%dx%dx%dx%d", &bm, &bn, &bk, &ks);
-    if (n < 3) bm = bn = 64, bk = 32;
-    if (n < 4) ks = 1;
-    if (!valid_cfg(bm, bn, bk, ks)) bm = bn = 64, bk = 32, ks = 1;
-    const int64_t s = force_split > 0 ? force_split : 1;
-    Plan pl = finish_plan(bm, bn, bk, s, K);
-    pl.ks = ks;
-    return pl;
-  }
-  const int ta = a_kc ? 0 : 1, tb = b_kc ? 1 : 0;
-  for (const PlanEntry& e : kPlans)
-    if (e.M == M && e.N == N && e.K == K && e.ta == ta && e.tb == tb && !getenv("DLRM_GEMM_NOTABLE"))
-    {
-      Plan pl = finish_plan(e.bm, e.bn, e.bk, e.split, K);
-      pl.ks = e.ks;
-      return pl;
-    }
-  // Heuristic: the largest tile that still gives >= target workgroups; split K of the
-  // 64x64 tiling up to the target otherwise.
-  const int target = env_int("DLRM_GEMM_TARGET", (a_kc && b_kc) ? 512 : 1536);
-  const int64_t t128 = dlrm::ceil_div(M, 128) * dlrm::ceil_div(N, 128);
-  if (t128 >= target) return {128, 128, 32, 1, K};
-  const int64_t t64x128 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 128);
-  if (t64x128 >= target) return {64, 128, 32, 1, K};
-  const int64_t t64 = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 64);
-  const int64_t s = force_split > 0 ? force_split : dlrm::ceil_div(target, t64);
-  return finish_plan(64, 64, 32, s, K);
+// Compiled tiles: 64x64, 128x64, 64x128, 32x64, 64x32.
+bool tile_ok(int bm, int bn) {
+  return (bm == 64 && bn == 64) || (bm == 128 && bn == 64) || (bm == 64 && bn == 128) ||
+         (bm == 32 && bn == 64) || (bm == 64 && bn == 32);
 }
 
-template <int BM, int BN, int BKT, int KS>
-int launch_cfg(GemmParams p, int splits, bool a_kc, bool b_kc, bool vec, hipStream_t st) {
-  p.tiles_m = (int)dlrm::ceil_div(p.M, BM);
-  p.tiles_n = (int)dlrm::ceil_div(p.N, BN);
-  constexpr bool M16 = KS == 16;   // KS == 16 selects the 16x16x4 kernel
-  constexpr bool PIPE = KS == 32;  // KS == 32 selects the pipelined 16x16x4 kernel
-  const dim3 grid(p.tiles_m * p.tiles_n, splits), block((M16 || PIPE) ? kThreads : kThreads * KS);
-#define G(AK, BK_, V_)                                                                          \
-  do {                                                                                          \
-    if constexpr (PIPE)                                                                         \
-      hipLaunchKernelGGL((gemm_f32_pipe_kernel<BM, BN, AK, BK_, V_>), grid, block, 0, st, p);   \
-    else if constexpr (M16)                                                                     \
-      hipLaunchKernelGGL((gemm_f32_mfma16_kernel<BM, BN, AK, BK_, V_>), grid, block, 0, st, p); \
-    else                                                                                        \
-      hipLaunchKernelGGL((gemm_f32_mfma_kernel<BM, BN, BKT, ((M16 || PIPE) ? 1 : KS), AK, BK_, V_>), grid, \
-                         block, 0, st, p);                                                      \
-  } while (0)
-#define G_V(AK, BK_)  \
-  if (vec)            \
-    G(AK, BK_, true); \
-  else                \
-    G(AK, BK_, false);
-  if (a_kc && b_kc) {
-    G_V(true, true)
-  } else if (a_kc) {
-    G_V(true, false)
-  } else if (b_kc) {
-    G_V(false, true)
-  } else {
-    G_V(false, false)
+// Plan of ONE problem, independent of what it is grouped with (so a problem's result is
+// bitwise the same in any group: the split decides the summation order, the tile shape
+// does not).  Tuning overrides (read per call, for sweeps): DLRM_GEMM_CFG=<BM>x<BN>,
+// DLRM_GEMM_SPLIT=<n>.
+void plan_one(const Desc& d, int& bm, int& bn, Plan& pl) {
+  bm = bn = 64;
+  if (d.mode == DLRM_GEMM_REDUCE) {  // elementwise job: no tiles, no K
+    pl.splits = d.splits;
+    pl.kchunk = 0;
+    return;
   }
-#undef G_V
-#undef G
+  if (d.mode == DLRM_GEMM_PARTIAL && d.splits > 0) {  // caller-sized partial buffer
+    int a, b;
+    Desc q = d;
+    q.mode = DLRM_GEMM_FULL;
+    plan_one(q, a, b, pl);
+    bm = a, bn = b;
+    pl = make_plan(d.splits, d.K);
+    return;
+  }
+  const char* cfg = getenv("DLRM_GEMM_CFG");
+  const int force_split = env_int("DLRM_GEMM_SPLIT", 0);
+  if (cfg && *cfg) {
+    int a = 64, b = 64;
+    if (sscanf(cfg, "%dx%d", &a, &b) == 2 && tile_ok(a, b))
+      bm = a, bn = b;
+    pl = make_plan(force_split > 0 ? force_split : 1, d.K);
+    return;
+  }
+  if (!getenv("DLRM_GEMM_NOTABLE"))
+    for (const PlanEntry& e : kPlans)
+      if (e.M == d.M && e.N == d.N && e.K == d.K && e.layout == layout_of(d)) {
+        bm = e.bm, bn = e.bn;
+        pl = make_plan(e.split, d.K);
+        return;
+      }
+  // Heuristic (shapes not in the table): 64x32 tiles (the sweep's best almost everywhere);
+  // FULL problems run unsplit unless they have fewer than one tile per CU (an in-launch
+  // split costs a hand-off); PARTIAL ones split K until >= 2 blocks per CU, every K chunk
+  // >= 256 (8 K-tiles).
+  bm = 64, bn = 32;
+  const int64_t tiles = dlrm::ceil_div(d.M, 64) * dlrm::ceil_div(d.N, 32);
+  const int target = env_int("DLRM_GEMM_TARGET", d.mode == DLRM_GEMM_PARTIAL ? 512 : 256);
+  int64_t s = 1;
+  while (tiles * s < target && dlrm::ceil_div(d.K, s + 1) >= 256 && s < kMaxSplit) ++s;
+  pl = make_plan(s, d.K);
+}
+
+// Tile config of a launch: the GEMM problems' common choice, else 64x32 (REDUCE jobs have
+// no tiles and do not vote).
+void plan_launch(int n, const Desc* d, int& bm, int& bn, Plan* pl) {
+  bool first = true;
+  bm = bn = 64;
+  for (int i = 0; i < n; ++i) {
+    int a, b;
+    plan_one(d[i], a, b, pl[i]);
+    if (d[i].mode == DLRM_GEMM_REDUCE) continue;
+    if (first) {
+      bm = a, bn = b;
+      first = false;
+    } else if (a != bm || b != bn) {
+      bm = 64, bn = 32;
+    }
+  }
+}
+
+// Split-K workspace: the fixed 64 KiB ticket head, then each problem's records.
+size_t group_ws_bytes(int n, const Desc* d, int bm, int bn, const Plan* pl) {
+  WsCarver c(nullptr);
+  c.take<int>(kTicketCap);
+  bool any = false;
+  for (int i = 0; i < n; ++i)
+    if (pl[i].splits > 1 && d[i].mode == DLRM_GEMM_FULL) {
+      any = true;
+      const int64_t tiles = dlrm::ceil_div(d[i].M, bm) * dlrm::ceil_div(d[i].N, bn);
+      c.take<float>((size_t)tiles * pl[i].splits * (bm * bn + bm));
+    }
+  return any ? c.used + 256 : 0;
+}
+
+template <int BM, int BN>
+int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes, hipStream_t st) {
+  GemmGroup g{};
+  g.n = n;
+  const int pub = env_int("DLRM_GEMM_PUB", 1);
+  WsCarver c(ws);
+  int* tickets = c.take<int>(kTicketCap);
+  int64_t tick = 0, blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    GemmParams& p = g.p[i];
+    p.M = d[i].M, p.N = d[i].N, p.K = d[i].K, p.alpha = d[i].alpha;
+    p.A = d[i].A, p.lda = d[i].lda, p.B = d[i].B, p.ldb = d[i].ldb;
+    p.C = d[i].C, p.ldc = d[i].ldc, p.epi = d[i].epi, p.bias = d[i].bias;
+    p.aux = d[i].aux, p.ldaux = d[i].ldaux, p.ones_col = d[i].ones_col;
+    p.layout = layout_of(d[i]);
+    p.pub = pub;
+    p.mode = d[i].mode;
+    p.part = d[i].part;
+    p.tiles_m = (int)dlrm::ceil_div(p.M, BM);
+    p.tiles_n = (int)dlrm::ceil_div(p.N, BN);
+    p.splits = pl[i].splits;
+    p.kchunk = pl[i].kchunk > 0 ? pl[i].kchunk : kBK;
+    p.block0 = (int)blocks;
+    if (p.mode == DLRM_GEMM_REDUCE) {
+      blocks += dlrm::ceil_div(p.M * p.N / 4 + (p.ones_col >= 0 ? p.M : 0), kThreads);
+      continue;
+    }
+    if (p.splits > 1 && p.mode == DLRM_GEMM_FULL) {
+      const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+      p.counters = tickets + tick;
+      p.ws = c.take<float>((size_t)tiles * p.splits * (BM * BN + BM));
+      tick += tiles;
+    }
+    blocks += (int64_t)p.tiles_m * p.tiles_n * p.splits;
+  }
+  DLRM_REQUIRE(tick <= kTicketCap && blocks < INT32_MAX, DLRM_ERR_UNSUPPORTED,
+               "dlrm_gemm_f32: too many split tiles in one launch");
+  DLRM_REQUIRE(tick == 0 || (ws && ws_bytes >= c.used), DLRM_ERR_WORKSPACE,
+               "dlrm_gemm_f32: workspace too small");
+  g.total = (int)blocks;
+  int kinds = 0;
+  for (int i = 0; i < n; ++i)
+    if (g.p[i].mode != DLRM_GEMM_REDUCE)
+      kinds |= kind_bit(g.p[i].layout, g.p[i].layout == 2 && g.p[i].ones_col >= 0);
+  const dim3 grid(g.total), block(kThreads);
+  // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
+  // row sums, two wgrads), else all kinds
+  switch (kinds) {
+#define K_(M_)                                                                          \
+  case M_:                                                                             \
+    hipLaunchKernelGGL((gemm_group_kernel<BM, BN, M_>), grid, block, 0, st, g);         \
+    break;
+    K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
+#undef K_
+    default:
+      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, 31>), grid, block, 0, st, g);
+  }
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32");
-  if (splits > 1) {
-    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(dlrm::ceil_div(p.M * p.N, 256)), dim3(256),
-                       0, st, p, splits);
-    DLRM_LAUNCH_CHECK("dlrm_gemm_f32 (split-K reduce)");
+  return DLRM_OK;
+}
+
+int launch_generic(const Desc& d, hipStream_t st) {
+  GemmParams p{};
+  p.M = d.M, p.N = d.N, p.K = d.K, p.alpha = d.alpha;
+  p.A = d.A, p.lda = d.lda, p.B = d.B, p.ldb = d.ldb;
+  p.C = d.C, p.ldc = d.ldc, p.epi = d.epi, p.bias = d.bias;
+  p.aux = d.aux, p.ldaux = d.ldaux, p.ones_col = d.ones_col;
+  p.tiles_m = (int)dlrm::ceil_div(p.M, 64);
+  p.tiles_n = (int)dlrm::ceil_div(p.N, 64);
+  p.splits = 1;
+  const bool a_kc = !d.trans_a, b_kc = d.trans_b != 0;
+  const dim3 grid(p.tiles_m * p.tiles_n), block(kThreads);
+  if (a_kc && b_kc)
+    hipLaunchKernelGGL((gemm_generic_kernel<true, true>), grid, block, 0, st, p);
+  else if (a_kc)
+    hipLaunchKernelGGL((gemm_generic_kernel<true, false>), grid, block, 0, st, p);
+  else if (b_kc)
+    hipLaunchKernelGGL((gemm_generic_kernel<false, true>), grid, block, 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_generic_kernel<false, false>), grid, block, 0, st, p);
+  DLRM_LAUNCH_CHECK("dlrm_gemm_f32 (generic)");
+  if (d.ones_col >= 0) {
+    hipLaunchKernelGGL(gemm_rowsum_kernel, dim3(dlrm::ceil_div(d.M, 64)), dim3(kThreads), 0, st, p,
+                       a_kc);
+    DLRM_LAUNCH_CHECK("dlrm_gemm_f32 (row sum)");
   }
   return DLRM_OK;
 }
 
-inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-inline bool kbeg_ok(int64_t kchunk) { return kchunk % 4 == 0; }
+int check_desc(const Desc& d) {
+  DLRM_ARG(d.mode >= DLRM_GEMM_FULL && d.mode <= DLRM_GEMM_REDUCE, "dlrm_gemm_f32: bad mode");
+  if (d.mode != DLRM_GEMM_FULL) {
+    DLRM_ARG(d.part, "dlrm_gemm_f32: PARTIAL/REDUCE need a partial buffer");
+    DLRM_ARG(d.mode != DLRM_GEMM_REDUCE || (d.splits >= 1 && d.N % 4 == 0 && d.M >= 0 && d.C &&
+                                            d.ldc >= d.N),
+             "dlrm_gemm_f32: REDUCE needs splits >= 1, N %% 4 == 0 and C");
+    if (d.mode == DLRM_GEMM_REDUCE) {
+      DLRM_ARG(d.ones_col < 0 || (d.ones_col >= d.N && d.ones_col < d.ldc),
+               "dlrm_gemm_f32: ones_col outside [N, ldc)");
+      return DLRM_OK;
+    }
+    DLRM_REQUIRE(pipe_ok(d), DLRM_ERR_UNSUPPORTED,
+                 "dlrm_gemm_f32: PARTIAL needs 16-B aligned operands, K %% 4 == 0");
+  }
+  DLRM_ARG(d.M >= 0 && d.N >= 0 && d.K >= 0, "dlrm_gemm_f32: negative size");
+  if (d.M == 0 || (d.N == 0 && d.ones_col < 0)) return DLRM_OK;
+  DLRM_ARG(d.C, "dlrm_gemm_f32: null C");
+  DLRM_ARG(d.K == 0 || (d.A && d.B), "dlrm_gemm_f32: null A/B");
+  DLRM_ARG(d.epi >= DLRM_EPI_STORE && d.epi <= DLRM_EPI_RELU, "dlrm_gemm_f32: bad epilogue");
+  DLRM_ARG(!(d.epi == DLRM_EPI_BIAS || d.epi == DLRM_EPI_BIAS_RELU) || d.bias,
+           "dlrm_gemm_f32: epilogue needs bias");
+  DLRM_ARG(d.epi != DLRM_EPI_DRELU || (d.aux && d.ldaux >= d.N), "dlrm_gemm_f32: DRELU needs aux");
+  DLRM_ARG(d.ldc >= d.N && (d.ones_col < 0 || (d.ones_col >= d.N && d.ones_col < d.ldc)),
+           "dlrm_gemm_f32: ldc < N or ones_col outside [N, ldc)");
+  DLRM_ARG(d.trans_a ? d.lda >= d.M : d.lda >= d.K, "dlrm_gemm_f32: bad lda");
+  DLRM_ARG(d.trans_b ? d.ldb >= d.K : d.ldb >= d.N, "dlrm_gemm_f32: bad ldb");
+  DLRM_REQUIRE(dlrm::ceil_div(d.M, 64) * dlrm::ceil_div(d.N, 64) < (int64_t)INT32_MAX / kMaxSplit,
+               DLRM_ERR_UNSUPPORTED, "dlrm_gemm_f32: too large");
+  return DLRM_OK;
+}
+
+// Plans n problems: the pipelined group (problems it can take) + generic fallbacks.
+size_t ws_for(int n, const Desc* d) {
+  Desc q[kMaxGroup];
+  int m = 0;
+  for (int i = 0; i < n; ++i)
+    if (d[i].M > 0 && d[i].N > 0 && d[i].K > 0 && pipe_ok(d[i])) q[m++] = d[i];
+  if (m == 0) return 0;
+  int bm, bn;
+  Plan pl[kMaxGroup];
+  plan_launch(m, q, bm, bn, pl);
+  return group_ws_bytes(m, q, bm, bn, pl);
+}
+
+int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
+  DLRM_ARG(n >= 1 && n <= kMaxGroup, "dlrm_gemm_f32_group: 1..%d problems", kMaxGroup);
+  Desc q[kMaxGroup];
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    const int rc = check_desc(d[i]);
+    if (rc != DLRM_OK) return rc;
+    if (d[i].M == 0 || (d[i].N == 0 && d[i].ones_col < 0)) continue;
+    if (d[i].mode == DLRM_GEMM_REDUCE) {
+      q[m++] = d[i];
+      continue;
+    }
+    if (d[i].K == 0 || !pipe_ok(d[i])) {
+      const int r2 = launch_generic(d[i], st);
+      if (r2 != DLRM_OK) return r2;
+      continue;
+    }
+    q[m++] = d[i];
+  }
+  if (m == 0) return DLRM_OK;
+  int bm, bn;
+  Plan pl[kMaxGroup];
+  plan_launch(m, q, bm, bn, pl);
+  const size_t need = group_ws_bytes(m, q, bm, bn, pl);
+  if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: every problem unsplit
+    for (int i = 0; i < m; ++i) pl[i] = make_plan(1, q[i].K);
+  }
+  if (bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, st);
+  if (bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, st);
+  if (bm == 32) return launch_group<32, 64>(m, q, pl, ws, ws_bytes, st);
+  if (bn == 32) return launch_group<64, 32>(m, q, pl, ws, ws_bytes, st);
+  return launch_group<64, 64>(m, q, pl, ws, ws_bytes, st);
+}
+
+Desc desc_of(const dlrm_gemm_problem& g) {
+  Desc d;
+  d.trans_a = g.trans_a, d.trans_b = g.trans_b;
+  d.M = g.M, d.N = g.N, d.K = g.K, d.alpha = g.alpha;
+  d.A = g.A, d.lda = g.lda, d.B = g.B, d.ldb = g.ldb;
+  d.C = g.C, d.ldc = g.ldc, d.epi = g.epilogue, d.bias = g.bias;
+  d.aux = g.aux, d.ldaux = g.ld_aux, d.ones_col = g.ones_col;
+  d.mode = g.mode, d.splits = g.splits, d.part = g.partial;
+  return d;
+}
 
 }  // namespace
 
 extern "C" size_t dlrm_gemm_f32_workspace_size(int32_t trans_a, int32_t trans_b, int64_t M,
                                                int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  const Plan pl = plan_gemm(M, N, K, !trans_a, trans_b != 0);
-  return pl.splits > 1 ? (size_t)pl.splits * M * N * sizeof(float) : 0;
+  Desc d{};
+  d.trans_a = trans_a, d.trans_b = trans_b, d.M = M, d.N = N, d.K = K;
+  // aligned, padded placeholders: the size covers any aligned call of this shape
+  d.lda = ((trans_a ? M : K) + 3) / 4 * 4, d.ldb = ((trans_b ? K : N) + 3) / 4 * 4;
+  d.A = d.B = reinterpret_cast<const float*>(256);
+  d.ones_col = -1;
+  return ws_for(1, &d);
 }
 
 extern "C" int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
@@ -785,81 +1120,41 @@ extern "C" int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_
                              int64_t ldb, float* C, int64_t ldc, int32_t epilogue,
                              const float* bias, const float* aux, int64_t ld_aux,
                              void* workspace, size_t workspace_bytes, dlrm_stream_t stream) {
-  DLRM_ARG(M >= 0 && N >= 0 && K >= 0, "dlrm_gemm_f32: negative size");
-  if (M == 0 || N == 0) return DLRM_OK;
-  DLRM_ARG(C, "dlrm_gemm_f32: null C");
-  DLRM_ARG(K == 0 || (A && B), "dlrm_gemm_f32: null A/B");
-  DLRM_ARG(epilogue >= DLRM_EPI_STORE && epilogue <= DLRM_EPI_RELU, "dlrm_gemm_f32: bad epilogue");
-  DLRM_ARG(!(epilogue == DLRM_EPI_BIAS || epilogue == DLRM_EPI_BIAS_RELU) || bias,
-           "dlrm_gemm_f32: epilogue needs bias");
-  DLRM_ARG(epilogue != DLRM_EPI_DRELU || (aux && ld_aux >= N), "dlrm_gemm_f32: DRELU needs aux");
-  DLRM_ARG(ldc >= N, "dlrm_gemm_f32: ldc < N");
-  DLRM_ARG(trans_a ? lda >= M : lda >= K, "dlrm_gemm_f32: bad lda");
-  DLRM_ARG(trans_b ? ldb >= K : ldb >= N, "dlrm_gemm_f32: bad ldb");
-  const int64_t tiles_max = dlrm::ceil_div(M, 64) * dlrm::ceil_div(N, 64);
-  DLRM_REQUIRE(tiles_max < (int64_t)INT32_MAX, DLRM_ERR_UNSUPPORTED, "dlrm_gemm_f32: too large");
+  Desc d;
+  d.trans_a = trans_a, d.trans_b = trans_b, d.M = M, d.N = N, d.K = K, d.alpha = alpha;
+  d.A = A, d.lda = lda, d.B = B, d.ldb = ldb, d.C = C, d.ldc = ldc, d.epi = epilogue;
+  d.bias = bias, d.aux = aux, d.ldaux = ld_aux, d.ones_col = -1;
+  return run(1, &d, workspace, workspace_bytes, dlrm::as_stream(stream));
+}
 
-  GemmParams p{};
-  p.M = M;
-  p.N = N;
-  p.K = K;
-  p.alpha = alpha;
-  p.A = A;
-  p.lda = lda;
-  p.B = B;
-  p.ldb = ldb;
-  p.C = C;
-  p.ldc = ldc;
-  p.epi = epilogue;
-  p.bias = bias;
-  p.aux = aux;
-  p.ldaux = ld_aux;
-  Plan pl = plan_gemm(M, N, K, !trans_a, trans_b != 0);
-  if (pl.splits > 1) {
-    const size_t need = (size_t)pl.splits * M * N * sizeof(float);
-    if (!workspace || workspace_bytes < need) {  // no workspace: single pass
-      pl.splits = 1;
-      pl.kchunk = K;
-    } else {
-      p.ws = static_cast<float*>(workspace);
-    }
-  }
-  p.kchunk = pl.kchunk > 0 ? pl.kchunk : 1;
-  const bool a_kc = !trans_a;
-  const bool b_kc = trans_b != 0;
-  const bool vec = aligned16(A) && (lda % 4 == 0) && aligned16(B) && (ldb % 4 == 0);
-  // the pipelined kernel moves whole float4s: K and the mn extent of an mn-contiguous
-  // operand must be multiples of 4 (else the planner's pick falls back to the 16x16 kernel)
-  const int64_t a_ext = a_kc ? (M - 1) * lda + K : (K - 1) * lda + M;
-  const int64_t b_ext = b_kc ? (N - 1) * ldb + K : (K - 1) * ldb + N;
-  const bool vec4 = vec && K % 4 == 0 && (a_kc || M % 4 == 0) && (b_kc || N % 4 == 0) &&
-                    kbeg_ok(pl.kchunk) && a_ext * 4 < 0x7ff00000LL && b_ext * 4 < 0x7ff00000LL;
-  if (pl.ks == 32 && !vec4) pl.ks = 16;
-  hipStream_t st = dlrm::as_stream(stream);
-#define CFG(BM_, BN_, BK_, KS_)                                      \
-  if (pl.bm == BM_ && pl.bn == BN_ && pl.bk == BK_ && pl.ks == KS_) \
-    return launch_cfg<BM_, BN_, BK_, KS_>(p, pl.splits, a_kc, b_kc, vec, st);
-  CFG(64, 64, 32, 1)
-  CFG(128, 64, 32, 1)
-  CFG(64, 128, 32, 1)
-  CFG(128, 128, 32, 1)
-  CFG(64, 64, 64, 1)
-  CFG(128, 64, 64, 1)
-  CFG(64, 128, 64, 1)
-  CFG(128, 128, 64, 1)
-  CFG(64, 64, 32, 2)
-  CFG(128, 64, 32, 2)
-  CFG(64, 128, 32, 2)
-  CFG(128, 128, 32, 2)
-  CFG(64, 64, 64, 2)
-  CFG(64, 64, 32, 16)
-  CFG(128, 64, 32, 16)
-  CFG(64, 128, 32, 16)
-  CFG(128, 128, 32, 16)
-  CFG(64, 64, 32, 32)
-  CFG(128, 64, 32, 32)
-  CFG(64, 128, 32, 32)
-#undef CFG
-  dlrm::set_error("dlrm_gemm_f32: no kernel for plan %dx%dx%dx%d", pl.bm, pl.bn, pl.bk, pl.ks);
-  return DLRM_ERR_UNSUPPORTED;
+extern "C" size_t dlrm_gemm_f32_group_workspace_size(int32_t n, const dlrm_gemm_problem* probs) {
+  if (n < 1 || n > kMaxGroup || !probs) return 0;
+  Desc d[kMaxGroup];
+  for (int i = 0; i < n; ++i) d[i] = desc_of(probs[i]);
+  return ws_for(n, d);
+}
+
+extern "C" int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* probs, void* workspace,
+                                   size_t workspace_bytes, dlrm_stream_t stream) {
+  DLRM_ARG(probs && n >= 1 && n <= kMaxGroup, "dlrm_gemm_f32_group: 1..%d problems", kMaxGroup);
+  Desc d[kMaxGroup];
+  for (int i = 0; i < n; ++i) d[i] = desc_of(probs[i]);
+  return run(n, d, workspace, workspace_bytes, dlrm::as_stream(stream));
+}
+
+extern "C" int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem) {
+  if (!problem) return 0;
+  Desc d = desc_of(*problem);
+  if (d.mode == DLRM_GEMM_REDUCE) d.mode = DLRM_GEMM_FULL;
+  d.splits = 0;
+  if (d.M <= 0 || d.N <= 0 || d.K <= 0) return 1;
+  int bm, bn;
+  Plan pl;
+  plan_one(d, bm, bn, pl);
+  return pl.splits;
+}
+
+extern "C" size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits) {
+  if (M <= 0 || N <= 0 || splits <= 0) return 0;
+  return (size_t)splits * (size_t)(M * N + M) * sizeof(float);
 }

@@ -26,6 +26,16 @@ class DLRMHipError(RuntimeError):
         self.code = code
 
 
+class GemmProblem(ctypes.Structure):
+    """struct dlrm_gemm_problem (include/dlrm_hip.h)."""
+    _fields_ = [("trans_a", c_int32), ("trans_b", c_int32), ("M", c_int64), ("N", c_int64),
+                ("K", c_int64), ("alpha", c_float), ("A", c_void_p), ("lda", c_int64),
+                ("B", c_void_p), ("ldb", c_int64), ("C", c_void_p), ("ldc", c_int64),
+                ("epilogue", c_int32), ("bias", c_void_p), ("aux", c_void_p),
+                ("ld_aux", c_int64), ("ones_col", c_int64), ("mode", c_int32),
+                ("splits", c_int32), ("partial", c_void_p)]
+
+
 # name -> (restype, argtypes); mirrors include/dlrm_hip.h exactly.
 P = c_void_p
 SIGNATURES = {
@@ -58,6 +68,10 @@ SIGNATURES = {
     "dlrm_gemm_f32_workspace_size": (c_size_t, [c_int32, c_int32, c_int64, c_int64, c_int64]),
     "dlrm_gemm_f32": (c_int32, [c_int32, c_int32, c_int64, c_int64, c_int64, c_float, P, c_int64,
                                 P, c_int64, P, c_int64, c_int32, P, P, c_int64, P, c_size_t, P]),
+    "dlrm_gemm_f32_group_workspace_size": (c_size_t, [c_int32, P]),
+    "dlrm_gemm_f32_group": (c_int32, [c_int32, P, P, c_size_t, P]),
+    "dlrm_gemm_f32_splits": (c_int32, [P]),
+    "dlrm_gemm_f32_partial_bytes": (c_size_t, [c_int64, c_int64, c_int32]),
     "dlrm_colsum_workspace_size": (c_size_t, [c_int64, c_int64]),
     "dlrm_colsum_f32": (c_int32, [c_int64, c_int64, P, c_int64, P, c_float, P, c_int32, P,
                                   c_float, P, c_size_t, P]),

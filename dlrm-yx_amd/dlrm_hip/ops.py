@@ -59,14 +59,16 @@ def _bits(t: torch.Tensor) -> int:
 
 
 class Workspace:
-    """Grow-only device scratch buffer (one per owner, reused across calls)."""
+    """Grow-only device scratch buffer (one per owner, reused across calls).  Zeroed when
+    allocated: the GEMM split-K tickets at its start must begin at 0 (the kernels leave
+    them at 0 after every launch)."""
 
     def __init__(self):
         self.buf: Optional[torch.Tensor] = None
 
     def get(self, nbytes: int, device) -> torch.Tensor:
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != torch.device(device):
-            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self.buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         return self.buf
 
 
@@ -271,12 +273,19 @@ def gemm_workspace_size(M: int, N: int, K: int, trans_a: bool = False,
     return _lib.query("dlrm_gemm_f32_workspace_size", int(trans_a), int(trans_b), M, N, K)
 
 
-def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
-         C: Optional[torch.Tensor] = None, alpha: float = 1.0, epilogue: int = EPI_STORE,
-         bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
-         workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D operands (unit inner stride).
-    Split-K uses ``workspace`` (or a cached one) when the planner asks for it."""
+GEMM_FULL, GEMM_PARTIAL, GEMM_REDUCE = 0, 1, 2  # dlrm_gemm_mode
+
+
+def gemm_problem(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False,
+                 trans_b: bool = False, C: Optional[torch.Tensor] = None, alpha: float = 1.0,
+                 epilogue: int = EPI_STORE, bias: Optional[torch.Tensor] = None,
+                 aux: Optional[torch.Tensor] = None, ones_col: int = -1,
+                 partial: Optional[torch.Tensor] = None, splits: int = 0):
+    """One dlrm_gemm_problem: C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D
+    operands (unit inner stride); ones_col >= 0 also writes C[:, ones_col] =
+    epilogue(alpha * op(A).sum(1)) (a Linear bias gradient).  With ``partial`` the problem
+    is a PARTIAL one: K split ``splits`` ways, raw partials into ``partial``, C untouched
+    until reduce_problem(...) runs in a later launch.  Returns (struct, C)."""
     _check_cuda(A, B, C, bias, aux)
     if A.stride(1) != 1 or B.stride(1) != 1:
         raise ValueError("gemm operands need unit inner stride")
@@ -287,18 +296,79 @@ def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool 
     if K != Kb:
         raise ValueError(f"gemm inner dims differ: {K} vs {Kb}")
     if C is None:
-        C = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    need = gemm_workspace_size(M, N, K, trans_a, trans_b)
+        C = torch.empty((M, N if ones_col < 0 else max(N, ones_col + 1)), dtype=torch.float32,
+                        device=A.device)
+    if C.stride(1) != 1 or C.shape[0] != M or C.shape[1] < N:
+        raise ValueError("gemm output must be [M, >= N] with unit inner stride")
+    if ones_col >= 0 and not (N <= ones_col < C.shape[1]):
+        raise ValueError("ones_col must be a column of C outside [0, N)")
+    pr = _lib.GemmProblem(int(trans_a), int(trans_b), M, N, K, float(alpha), A.data_ptr(),
+                          A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                          int(epilogue), bias.data_ptr() if bias is not None else None,
+                          aux.data_ptr() if aux is not None else None,
+                          aux.stride(0) if aux is not None else 0, int(ones_col),
+                          GEMM_PARTIAL if partial is not None else GEMM_FULL, int(splits),
+                          partial.data_ptr() if partial is not None else None)
+    return pr, C
+
+
+def gemm_splits(pr, partial: bool = False) -> int:
+    """The planner's K split for a problem launched alone (dlrm_gemm_f32_splits); with
+    partial=True, as a PARTIAL problem (deferred reduction)."""
+    q = _lib.GemmProblem.from_buffer_copy(pr)
+    if partial:
+        q.mode = GEMM_PARTIAL
+    return int(_lib.load().dlrm_gemm_f32_splits(ctypes.byref(q)))
+
+
+def gemm_partial_bytes(M: int, N: int, splits: int) -> int:
+    return _lib.query("dlrm_gemm_f32_partial_bytes", M, N, splits)
+
+
+def reduce_problem(pr_partial):
+    """The REDUCE problem finishing a PARTIAL one (same C, alpha, epilogue, ones_col)."""
+    q = _lib.GemmProblem.from_buffer_copy(pr_partial)
+    q.mode = GEMM_REDUCE
+    return q
+
+
+def _problems(prs):
+    arr = (_lib.GemmProblem * len(prs))(*prs)
+    return arr
+
+
+def gemm_group_workspace_size(problems) -> int:
+    return _lib.query("dlrm_gemm_f32_group_workspace_size", len(problems),
+                      ctypes.cast(_problems(problems), ctypes.c_void_p))
+
+
+def gemm_group(problems, workspace: Optional[torch.Tensor] = None, device=None) -> None:
+    """Launch up to 4 independent GEMM problems (gemm_problem structs) in ONE kernel.
+    ``workspace``: zero-initialised uint8 buffer (split-K tickets + partials); a cached one
+    is used when None."""
+    arr = _problems(problems)
+    need = _lib.query("dlrm_gemm_f32_group_workspace_size", len(problems),
+                      ctypes.cast(arr, ctypes.c_void_p))
+    dev = device if device is not None else torch.cuda.current_device()
     if need and workspace is None:
-        workspace = _ws("gemm", need, A.device)
+        workspace = _ws("gemm", need, dev)
     elif need and workspace.numel() < need:
         # never fall back to a shared buffer behind the caller's back: two streams could
         # then write split-K partials into the same scratch
         raise ValueError(f"gemm workspace too small: {workspace.numel()} < {need} bytes")
-    _lib.call("dlrm_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), _p(A),
-              A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0), epilogue, _p(bias), _p(aux),
-              aux.stride(0) if aux is not None else 0, _p(workspace) if need else None,
-              workspace.numel() if (need and workspace is not None) else 0, _stream(A.device))
+    _lib.call("dlrm_gemm_f32_group", len(problems), ctypes.cast(arr, ctypes.c_void_p),
+              _p(workspace) if need else None, workspace.numel() if need else 0,
+              _stream(dev))
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+         C: Optional[torch.Tensor] = None, alpha: float = 1.0, epilogue: int = EPI_STORE,
+         bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
+         workspace: Optional[torch.Tensor] = None, ones_col: int = -1) -> torch.Tensor:
+    """C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D operands (unit inner stride).
+    Split-K uses ``workspace`` (or a cached one) when the planner asks for it."""
+    pr, C = gemm_problem(A, B, trans_a, trans_b, C, alpha, epilogue, bias, aux, ones_col)
+    gemm_group([pr], workspace, A.device)
     return C
 
 

@@ -329,16 +329,12 @@ class DLRMTrainer:
             a[:, L.N] = 1.0
         bufs["R"][:, self.num_int] = 1.0
         wmax = max([L.Kp for L in self.layers] + [self.ldR])
-        # one split-K workspace sized for the largest GEMM of the step
-        shapes = []
-        for L in self.layers[:-1]:
-            shapes += [(Bl, L.N, L.Kp, False, True), (Bl, L.K, L.N, False, False),
-                       (L.N, L.Kp, Bl, True, False)]
-        gws = max([ops.gemm_workspace_size(*s) for s in shapes] + [256])
-        # split-K workspaces belong to this batch size: a hipGraph captured for it keeps
-        # their addresses, and the main and side streams never share one
-        bufs["gemm_ws"] = torch.empty(gws, dtype=torch.uint8, device=dev)
-        bufs["gemm_ws_side"] = torch.empty(gws, dtype=torch.uint8, device=dev)
+        # split-K workspaces: sized on the first step for this batch size (self._gemm grows
+        # them before any capture), zeroed because the split-K tile tickets must start at 0
+        # (the kernels leave them at 0).  They belong to this batch size: a hipGraph
+        # captured for it keeps their addresses, and the main and side streams never share.
+        bufs["gemm_ws"] = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+        bufs["gemm_ws_side"] = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
         # three gradient buffers: a weight-gradient GEMM on the side stream may still read
         # g_l while the main stream's next two data-gradient GEMMs produce g_{l-1}, g_{l-2}
         bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(3)]
@@ -379,10 +375,12 @@ class DLRMTrainer:
         ``profile``: optional callable(name) -> context manager around kernel groups (the
         step then runs on one stream so each group's events bracket only its kernels).
 
-        Independent work runs on a side stream (joined before return; hipGraph capture keeps
-        the fork/join): the bottom MLP forward beside the embedding lookup, each top-layer
-        weight-gradient GEMM (+ fused SGD) beside the next data-gradient GEMM, and the whole
-        bottom-MLP backward beside the embedding backward."""
+        MLP backward as grouped GEMM launches: the data gradient of layer l and the weight
+        gradient (+ fused SGD on one GPU) of layer l+1 read the same upstream gradient and
+        write disjoint buffers, so they run in ONE launch; the wgrad of layer l+1 may update
+        W_{l+1} there because the dgrad that reads W_{l+1} ran in the previous launch.
+        Optional side-stream overlaps (self.overlaps): "fwd" = bottom MLP || lookup, "bot" =
+        bottom-MLP backward || embedding backward (joined before return)."""
         cfg = self.cfg
         D = self.D
         Bl = batch.X.shape[0]
@@ -406,7 +404,6 @@ class DLRMTrainer:
                 s0.wait_stream(s1)
 
         c_fwd = conc and "fwd" in self.overlaps
-        c_top = conc and "top" in self.overlaps
         c_bot = conc and "bot" in self.overlaps
 
         def side_if(flag):
@@ -425,7 +422,7 @@ class DLRMTrainer:
         with side_if(c_fwd):
             h = batch.X
             for L, out in zip(self.bot, bufs["bot_act"]):
-                self._gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU, side=c_fwd)
+                self._gemm([self._fwd(L, h, out)], side=c_fwd)
                 h = out
         if c_fwd:
             join()
@@ -437,7 +434,7 @@ class DLRMTrainer:
                                  cfg.arch_interaction_itself, out=bufs["R"])
         h = bufs["R"]
         for L, out in zip(self.top[:-1], bufs["top_act"]):
-            self._gemm(h, L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)
+            self._gemm([self._fwd(L, h, out)])
             h = out
         last = self.top[-1]
         hin = h
@@ -455,30 +452,21 @@ class DLRMTrainer:
                           dw=None if fused_opt else last.gW[0, :last.Kp],
                           lr=lr if fused_opt else 0.0, workspace=self._ws_head_step(Bl, last.Kp))
         g = gview
-        # top hidden layers, last to first: dgrad on the main stream, wgrad beside it.
-        # G rotates over three buffers; the dgrad that overwrites a buffer first waits for
-        # the side-stream wgrad that read it (issued two layers earlier).
-        readers = {}  # buffer index -> event recorded on s1 after its last reader
+        # top hidden layers, last to first.  Each layer's weight gradient is split-K into a
+        # per-layer partial buffer; its reduction (+ fused SGD) is a REDUCE job inside the
+        # NEXT GEMM launch (the kernel boundary publishes the partials; no reduce launch,
+        # no in-launch hand-off).  dgrad(l) reads W_l, never W_{l+1} which that job writes.
+        # G rotates over three buffers.
+        rq = []  # reduce jobs riding on the next launch
         for li in range(len(self.top) - 2, -1, -1):
             L = self.top[li]
             inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
             gn = (gi + 1) % 3
-            if c_top and gn in readers:
-                s0.wait_event(readers.pop(gn))
-            dinp = G[gn][:, :L.K]
-            if li > 0:
-                self._gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp)
-            else:
-                self._gemm(g[:, :L.N], L.W[:, :L.K], C=dinp)
-            if c_top:
-                fork()  # the weight update may run once W has been read by the dgrad
-            with side_if(c_top):
-                self._wgrad(L, g, inp, fused_opt, lr, side=c_top)
-            if c_top:
-                ev = torch.cuda.Event()
-                ev.record(s1)
-                readers[gi] = ev
-            g, gi = dinp, gn
+            self._gemm([self._dgrad(L, g, inp if li > 0 else None, G[gn])] + rq)
+            w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li))
+            self._gemm([w])
+            rq = [r] if r is not None else []
+            g, gi = G[gn], gn
         # ---------------- backward: interaction -> dR = g
         xg, gfeats = self._features(bufs, Bl, grad=True)
         with prof("interaction_bwd"):
@@ -487,8 +475,11 @@ class DLRMTrainer:
         work = None
         if self.world > 1:
             work = self._alltoall_bwd(bufs, Bl)
-        # ---------------- backward: bottom MLP on the side stream || embeddings
+        # ---------------- backward: bottom MLP; a last launch finishes the reductions
         if c_bot:
+            if rq:
+                self._gemm(rq)
+            rq = []
             fork()
         with side_if(c_bot):
             xin = bufs["bot_act"][-1][:, :D]
@@ -499,12 +490,15 @@ class DLRMTrainer:
                 L = self.bot[li]
                 inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
                 if li > 0:
-                    dinp = bg[li % 2][:, :L.K]
-                    self._gemm(g[:, :L.N], L.W[:, :L.K], C=dinp, epilogue=ops.EPI_DRELU, aux=inp,
-                               side=c_bot)
-                self._wgrad(L, g, inp, fused_opt, lr, side=c_bot)
+                    self._gemm([self._dgrad(L, g, inp, bg[li % 2])] + rq, side=c_bot)
+                    rq = []
+                w, r = self._wg(L, g, inp, fused_opt, lr, ("bot", li))
+                self._gemm([w] + rq, side=c_bot)
+                rq = [r] if r is not None else []
                 if li > 0:
-                    g = dinp
+                    g = bg[li % 2]
+            if rq:
+                self._gemm(rq, side=c_bot)
         ar = None
         if self.world > 1:
             if conc:
@@ -546,22 +540,63 @@ class DLRMTrainer:
         ops.check_tbe_errors(self.tbe_error_flag)
 
     # -------------------------------------------------------------- pieces --
-    def _gemm(self, *args, side=False, **kw):
+    @staticmethod
+    def _fwd(L: _Layer, h, out):
+        """[h | 1] . [W | b]^T with ReLU (bias folded into the last k-term)."""
+        return ops.gemm_problem(h[:, :L.Kp], L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)[0]
+
+    @staticmethod
+    def _dgrad(L: _Layer, g, inp, out):
+        """dX = g W (x ReLU'(inp) when inp is given).  Widths that are not a multiple of 4
+        run over Kp (the bias column's gradient lands in a column nobody reads)."""
+        n = L.K if L.K % 4 == 0 else L.Kp
+        if inp is not None:
+            return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n], epilogue=ops.EPI_DRELU,
+                                    aux=inp)[0]
+        return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n])[0]
+
+    @staticmethod
+    def _wgrad(L: _Layer, g, inp, fused_opt, lr, **part):
+        """[dW | db] = g^T [inp | 1]; fused SGD on one GPU.  With K % 4 == 0 the bias
+        gradient is the row sum of g^T (ones_col) and the GEMM covers only the K weight
+        columns; otherwise the constant-1 column of inp is multiplied like a weight column."""
+        C = L.W if fused_opt else L.gW
+        kw = dict(alpha=lr, epilogue=ops.EPI_SGD) if fused_opt else {}
+        if L.K % 4 == 0:
+            return ops.gemm_problem(g[:, :L.N], inp[:, :L.K], trans_a=True, C=C, ones_col=L.K,
+                                    **kw, **part)[0]
+        return ops.gemm_problem(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=C, **kw, **part)[0]
+
+    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key):
+        """The wgrad of L as (problem, reduce job or None): split-K wgrads write partials
+        into a per-layer buffer and their reduction (+ SGD) runs in the NEXT launch."""
+        bufs = self._cur
+        sp = bufs.setdefault("splits", {})
+        if key not in sp:
+            sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr), partial=True)
+        s = sp[key]
+        if s <= 1:
+            return self._wgrad(L, g, inp, fused_opt, lr), None
+        parts = bufs.setdefault("partials", {})
+        M, N = L.N, (L.K if L.K % 4 == 0 else L.Kp)
+        need = ops.gemm_partial_bytes(M, N, s)
+        if key not in parts or parts[key].numel() * 4 < need:
+            parts[key] = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
+        pr = self._wgrad(L, g, inp, fused_opt, lr, partial=parts[key], splits=s)
+        return pr, ops.reduce_problem(pr)
+
+    def _gemm(self, problems, side=False):
         with self._prof("gemm"):
-            ops.gemm(*args, workspace=self._cur["gemm_ws_side" if side else "gemm_ws"],
-                     **kw)
+            ws = self._cur["gemm_ws_side" if side else "gemm_ws"]
+            need = ops.gemm_group_workspace_size(problems)
+            if need > ws.numel():  # first use of a new group shape: grow (not in capture)
+                ws = torch.zeros(need, dtype=torch.uint8, device=self.dev)
+                self._cur["gemm_ws_side" if side else "gemm_ws"] = ws
+            ops.gemm_group(problems, ws, self.dev)
 
     def _colsum(self, *args, **kw):
         with self._prof("colsum"):
             ops.colsum(*args, **kw)
-
-    def _wgrad(self, L: _Layer, g, inp, fused_opt, lr, side=False):
-        """[dW | db] = g^T [inp | 1] in one GEMM (bias folded); fused SGD on one GPU."""
-        if fused_opt:
-            self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.W, alpha=lr,
-                       epilogue=ops.EPI_SGD, side=side)
-        else:
-            self._gemm(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=L.gW, side=side)
 
     def _bias_and_w_head(self, last: _Layer, hin, dz, fused_opt, lr):
         """Head layer (K -> 1): [dw | db] = sum_m dz[m] [hin[m] | 1] as one column sum."""

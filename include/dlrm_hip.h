@@ -223,7 +223,7 @@ int dlrm_interact_cat_backward(int32_t B, int32_t F, int32_t D, const float* gra
 /* ------------------------------------------------------------------- MLP --- */
 /*
  * C[M][N] = epilogue(alpha * op(A)[M][K] . op(B)[K][N]) in exact fp32 on the
- * gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32), row-major everywhere:
+ * gfx950 fp32 MFMA (v_mfma_f32_16x16x4_f32), row-major everywhere:
  *   op(A)(m,k) = trans_a ? A[k*lda + m] : A[m*lda + k]
  *   op(B)(k,n) = trans_b ? B[n*ldb + k] : B[k*ldb + n]
  * Linear forward  Y = X W^T + b : trans_a=0, trans_b=1, EPI_BIAS[_RELU]
@@ -233,8 +233,12 @@ int dlrm_interact_cat_backward(int32_t B, int32_t F, int32_t D, const float* gra
  * matching extra column of W, the forward needs no bias epilogue (EPI_RELU) and the
  * wgrad GEMM produces the bias gradient in that column.
  * Small-M*N / long-K shapes are split along K into >= 2 workgroups per CU when a
- * workspace of dlrm_gemm_f32_workspace_size() bytes is given (partials summed in
- * split order: deterministic); with workspace == NULL the GEMM runs unsplit.
+ * workspace of dlrm_gemm_f32_workspace_size() bytes is given: the last workgroup of
+ * each output tile sums the partials in split order (deterministic) inside the same
+ * launch.  The first 64 KiB of the workspace are per-tile tickets that MUST be zero
+ * before its first use (hipMemset once); every call leaves them zero again.  Concurrent calls
+ * (different streams) need different workspaces.  With workspace == NULL the GEMM runs
+ * unsplit.
  */
 size_t dlrm_gemm_f32_workspace_size(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
                                     int64_t K);
@@ -243,6 +247,60 @@ int dlrm_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_
                   float* C, int64_t ldc, int32_t epilogue, const float* bias,
                   const float* aux, int64_t ld_aux, void* workspace, size_t workspace_bytes,
                   dlrm_stream_t stream);
+
+/* dlrm_gemm_problem.mode */
+enum dlrm_gemm_mode {
+  DLRM_GEMM_FULL = 0,    /* C = epilogue(...) (split-K, if planned, reduced in-launch)  */
+  DLRM_GEMM_PARTIAL = 1, /* K split `splits` ways; raw partials -> partial buffer:
+                            [splits][M][N] (+ [splits][M] row sums for ones_col); no C */
+  DLRM_GEMM_REDUCE = 2   /* C = epilogue(alpha * sum_s partial[s]) in split order (+ the
+                            ones_col row sums): finishes an earlier PARTIAL problem; a
+                            later launch's kernel boundary publishes the partials       */
+};
+
+/*
+ * Grouped GEMM: up to 4 INDEPENDENT problems in one launch (e.g. the dgrad of layer l
+ * beside the wgrad of layer l+1 of an MLP backward: both read dY_{l+1}, neither writes
+ * what the other reads).  Each problem is dlrm_gemm_f32's contract, plus:
+ *   ones_col >= 0:  C[m][ones_col] = epilogue(alpha * sum_k op(A)(m,k))   (ones_col in
+ *                   [N, ldc)) — the bias gradient of a Linear layer whose bias is stored
+ *                   as the weight column ones_col (dW and db of [W | b] in one launch).
+ * mode PARTIAL + REDUCE defer a split-K reduction to a LATER launch (typically the next
+ * group of an MLP backward, which runs anyway), fully parallel and with no in-launch
+ * hand-off; the sum order is fixed (bitwise the in-launch result).  PARTIAL needs
+ * aligned operands (K % 4 == 0); REDUCE needs N % 4 == 0; `partial` holds
+ * dlrm_gemm_f32_partial_bytes(M, N, splits) bytes.  `splits` = 0 in PARTIAL takes the
+ * planner's choice (dlrm_gemm_f32_splits); REDUCE must repeat the PARTIAL's value.
+ * Problems with unaligned operands run on a generic kernel (separate launch, unsplit).
+ * The workspace follows dlrm_gemm_f32's rules (zeroed 64 KiB ticket head before first
+ * use; one workspace per stream).
+ */
+typedef struct dlrm_gemm_problem {
+  int32_t trans_a, trans_b;
+  int64_t M, N, K;
+  float alpha;
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  int32_t epilogue;
+  const float* bias;
+  const float* aux;
+  int64_t ld_aux;
+  int64_t ones_col; /* -1: none */
+  int32_t mode;     /* dlrm_gemm_mode */
+  int32_t splits;   /* PARTIAL / REDUCE */
+  float* partial;   /* PARTIAL / REDUCE */
+} dlrm_gemm_problem;
+size_t dlrm_gemm_f32_group_workspace_size(int32_t n, const dlrm_gemm_problem* problems);
+/* The planner's K split for one problem as if launched alone, in its mode (FULL: an
+ * in-launch split; PARTIAL: the split a deferred REDUCE will finish). */
+int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem);
+size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits);
+int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
+                        size_t workspace_bytes, dlrm_stream_t stream);
 
 /* Workspace for dlrm_colsum_f32 (deterministic two-pass column reduction). */
 size_t dlrm_colsum_workspace_size(int64_t M, int64_t N);

@@ -14,7 +14,7 @@ dev = "cuda"
 A = torch.randn((K, M) if ta else (M, K), device=dev)
 B = torch.randn((N, K) if tb else (K, N), device=dev)
 C = torch.empty(M, N, device=dev)
-ws = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+ws = torch.zeros(256 << 20, dtype=torch.uint8, device=dev)  # split-K tickets start at 0
 blas = os.environ.get("GEMM_ONE_BLAS") == "1"
 At = A.t() if ta else A
 Bt = B.t() if tb else B

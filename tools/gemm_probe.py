@@ -17,7 +17,7 @@ def main():
     shapes = sys.argv[1:] or ["4096,4096,4096,0,1", "2048,1024,1028,0,1", "2048,1024,1024,0,0",
                               "1024,1028,2048,1,0"]
     dev = "cuda"
-    ws = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(256 << 20, dtype=torch.uint8, device=dev)  # split-K tickets start at 0
     for sh in shapes:
         M, N, K, ta, tb = (int(v) for v in sh.split(","))
         A = torch.randn((K, M) if ta else (M, K), device=dev)

@@ -48,7 +48,7 @@ def main():
     A = torch.randn(2048, 1028, device=dev)
     W = torch.randn(1024, 1028, device=dev)
     C = torch.empty(2048, 1024, device=dev)
-    ws = torch.empty(ops.gemm_workspace_size(2048, 1024, 1028, False, True) + 256,
+    ws = torch.zeros(ops.gemm_workspace_size(2048, 1024, 1028, False, True) + 256,
                      dtype=torch.uint8, device=dev)
 
     def gemms():
