@@ -221,20 +221,17 @@ def main():
     batches = [tr.synthetic_batch(B, c["L"], seed=100 + i) for i in range(nb)]
     torch.cuda.synchronize()
 
-    use_graph = (world == 1) and not args.no_graph
+    # hipGraphs: one per batch on one GPU; on several GPUs the step's kernel segments are
+    # graphs replayed around the eager RCCL collectives (trainer.capture)
+    use_graph = not args.no_graph
     graphs = None
     if use_graph:
         try:
             for i in range(3):
                 tr.step(batches[i % nb])
             torch.cuda.synchronize()
-            graphs = []
             pool = torch.cuda.graph_pool_handle()
-            for i in range(nb):
-                gph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gph, pool=pool):
-                    tr.step(batches[i])
-                graphs.append(gph)
+            graphs = [tr.capture(batches[i], pool=pool) for i in range(nb)]
             torch.cuda.synchronize()
         except Exception as e:  # capture unsupported -> eager
             print(f"[bench] hipGraph capture failed ({e!r}); eager launches", file=sys.stderr)
@@ -243,7 +240,7 @@ def main():
 
     def run_step(k):
         if graphs is not None:
-            graphs[k % nb].replay()
+            graphs[k % nb]()
         else:
             tr.step(batches[k % nb])
 

@@ -373,14 +373,24 @@ class DLRMTrainer:
     def step(self, batch: Batch, profile=None):
         """One fwd + loss + bwd + update.  Returns (prob [B_local], loss [1]) device tensors.
         ``profile``: optional callable(name) -> context manager around kernel groups (the
-        step then runs on one stream so each group's events bracket only its kernels).
+        step then runs on one stream so each group's events bracket only its kernels)."""
+        for _kind, fn in self.segments(batch, profile):
+            fn()
+        return self._cur["prob"], self._cur["loss"]
 
-        MLP backward as grouped GEMM launches: the data gradient of layer l and the weight
-        gradient (+ fused SGD on one GPU) of layer l+1 read the same upstream gradient and
-        write disjoint buffers, so they run in ONE launch; the wgrad of layer l+1 may update
-        W_{l+1} there because the dgrad that reads W_{l+1} ran in the previous launch.
-        Optional side-stream overlaps (self.overlaps): "fwd" = bottom MLP || lookup, "bot" =
-        bottom-MLP backward || embedding backward (joined before return)."""
+    def segments(self, batch: Batch, profile=None):
+        """The step as an ordered list of ("gpu", fn) / ("comm", fn) items.  "gpu" items only
+        enqueue HIP kernels on the current stream (no host sync, no allocation after the
+        first step of a batch size): each one can be captured in its own hipGraph.  "comm"
+        items issue or wait for the RCCL collectives between them (multi GPU only), so a
+        multi-GPU step replays a few graphs around its three collectives.
+
+        MLP backward: each layer's weight gradient is split-K into a per-layer partial
+        buffer and its reduction (+ fused SGD on one GPU) is a REDUCE job inside the NEXT
+        GEMM launch (the kernel boundary publishes the partials: no reduce launch, no
+        in-launch hand-off); the dgrad in that launch reads W_l, never the W_{l+1} the job
+        writes.  Optional side-stream overlaps (self.overlaps): "fwd" = bottom MLP || lookup,
+        "bot" = bottom-MLP backward || embedding backward (joined inside the segment)."""
         cfg = self.cfg
         D = self.D
         Bl = batch.X.shape[0]
@@ -392,96 +402,83 @@ class DLRMTrainer:
         fused_opt = self.grads is None  # single GPU SGD: updates fused into backward
         lr, elr = self.lr, self.emb_lr
         conc = self.concurrent and profile is None
-        s0 = torch.cuda.current_stream(self.dev)
-        s1 = self._side if conc else s0
+        dist = self.world > 1
+        c_fwd = conc and "fwd" in self.overlaps and not dist
+        c_bot = conc and "bot" in self.overlaps and not dist
+        st = {}  # state shared by the segments (collective handles, pending reductions)
 
-        def fork():
-            if conc:
-                s1.wait_stream(s0)
+        def streams():
+            s0 = torch.cuda.current_stream(self.dev)
+            return s0, self._side if conc else s0
 
-        def join():
-            if conc:
-                s0.wait_stream(s1)
-
-        c_fwd = conc and "fwd" in self.overlaps
-        c_bot = conc and "bot" in self.overlaps
-
-        def side_if(flag):
+        def side_if(flag, s1):
             return torch.cuda.stream(s1) if flag else _NullCtx()
 
-        # ---------------- forward: embeddings (full batch, local tables) || bottom MLP
-        if c_fwd:
-            fork()
-        with prof("tbe_fwd"):
-            if self.T_local > 0:
-                ops.tbe_forward(self.weights, self.row_base, self.T_local, B, batch.indices,
-                                batch.offsets, out=bufs["E"], error_flag=self.tbe_error_flag)
-        work = None
-        if self.world > 1:
-            work = self._alltoall_fwd(bufs, Bl)
-        with side_if(c_fwd):
+        def lookup():  # embeddings (full batch, local tables)
+            with prof("tbe_fwd"):
+                if self.T_local > 0:
+                    ops.tbe_forward(self.weights, self.row_base, self.T_local, B, batch.indices,
+                                    batch.offsets, out=bufs["E"],
+                                    error_flag=self.tbe_error_flag)
+
+        def bottom_fwd():
             h = batch.X
             for L, out in zip(self.bot, bufs["bot_act"]):
                 self._gemm([self._fwd(L, h, out)], side=c_fwd)
                 h = out
-        if c_fwd:
-            join()
-        if work is not None:
-            work.wait()
-        x, feats = self._features(bufs, Bl)
-        with prof("interaction_fwd"):
-            ops.interact_forward(cfg.arch_interaction_op, x, feats,
-                                 cfg.arch_interaction_itself, out=bufs["R"])
-        h = bufs["R"]
-        for L, out in zip(self.top[:-1], bufs["top_act"]):
-            self._gemm([self._fwd(L, h, out)])
-            h = out
-        last = self.top[-1]
-        hin = h
-        # ---------------- head: last layer + sigmoid + loss + dz + input grad + [dw | db]
-        # (bias folded: [hin | 1] . [w | b]) in two launches; the weight update (fused SGD on
-        # one GPU) follows every read of the weights
-        G = bufs["g"]
-        gi = 0
-        gview = G[gi][:, :last.Kp]
-        prev_is_relu = len(self.top) > 1
-        with prof("head"):
-            ops.head_step(hin[:, :last.Kp], last.W[0, :last.Kp], batch.target, cfg.loss_function,
-                          cfg.loss_threshold, 1.0, prob=bufs["prob"], dz=bufs["dz"],
-                          loss_out=bufs["loss"], dX=gview, relu_mask=prev_is_relu,
-                          dw=None if fused_opt else last.gW[0, :last.Kp],
-                          lr=lr if fused_opt else 0.0, workspace=self._ws_head_step(Bl, last.Kp))
-        g = gview
-        # top hidden layers, last to first.  Each layer's weight gradient is split-K into a
-        # per-layer partial buffer; its reduction (+ fused SGD) is a REDUCE job inside the
-        # NEXT GEMM launch (the kernel boundary publishes the partials; no reduce launch,
-        # no in-launch hand-off).  dgrad(l) reads W_l, never W_{l+1} which that job writes.
-        # G rotates over three buffers.
-        rq = []  # reduce jobs riding on the next launch
-        for li in range(len(self.top) - 2, -1, -1):
-            L = self.top[li]
-            inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
-            gn = (gi + 1) % 3
-            self._gemm([self._dgrad(L, g, inp if li > 0 else None, G[gn])] + rq)
-            w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li))
-            self._gemm([w])
-            rq = [r] if r is not None else []
-            g, gi = G[gn], gn
-        # ---------------- backward: interaction -> dR = g
-        xg, gfeats = self._features(bufs, Bl, grad=True)
-        with prof("interaction_bwd"):
-            ops.interact_backward(cfg.arch_interaction_op, x, feats, g[:, :self.num_int],
-                                  cfg.arch_interaction_itself, grad_x=xg, grad_ly=gfeats)
-        work = None
-        if self.world > 1:
-            work = self._alltoall_bwd(bufs, Bl)
-        # ---------------- backward: bottom MLP; a last launch finishes the reductions
-        if c_bot:
-            if rq:
-                self._gemm(rq)
-            rq = []
-            fork()
-        with side_if(c_bot):
+
+        def fwd_single():  # one GPU: bottom MLP || lookup
+            s0, s1 = streams()
+            if c_fwd:
+                s1.wait_stream(s0)
+            lookup()
+            with side_if(c_fwd, s1):
+                bottom_fwd()
+            if c_fwd:
+                s0.wait_stream(s1)
+
+        def middle():  # interaction, top MLP, head, top backward, interaction backward
+            x, feats = self._features(bufs, Bl)
+            with prof("interaction_fwd"):
+                ops.interact_forward(cfg.arch_interaction_op, x, feats,
+                                     cfg.arch_interaction_itself, out=bufs["R"])
+            h = bufs["R"]
+            for L, out in zip(self.top[:-1], bufs["top_act"]):
+                self._gemm([self._fwd(L, h, out)])
+                h = out
+            last = self.top[-1]
+            # head: last layer + sigmoid + loss + dz + input grad + [dw | db] (bias folded:
+            # [h | 1] . [w | b]) in two launches; the update follows every read of w
+            G = bufs["g"]
+            gi = 0
+            gview = G[gi][:, :last.Kp]
+            with prof("head"):
+                ops.head_step(h[:, :last.Kp], last.W[0, :last.Kp], batch.target,
+                              cfg.loss_function, cfg.loss_threshold, 1.0, prob=bufs["prob"],
+                              dz=bufs["dz"], loss_out=bufs["loss"], dX=gview,
+                              relu_mask=len(self.top) > 1,
+                              dw=None if fused_opt else last.gW[0, :last.Kp],
+                              lr=lr if fused_opt else 0.0,
+                              workspace=self._ws_head_step(Bl, last.Kp))
+            g = gview
+            rq = []  # reduce jobs riding on the next launch; G rotates over three buffers
+            for li in range(len(self.top) - 2, -1, -1):
+                L = self.top[li]
+                inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
+                gn = (gi + 1) % 3
+                self._gemm([self._dgrad(L, g, inp if li > 0 else None, G[gn])] + rq)
+                w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li))
+                self._gemm([w])
+                rq = [r] if r is not None else []
+                g, gi = G[gn], gn
+            xg, gfeats = self._features(bufs, Bl, grad=True)
+            with prof("interaction_bwd"):
+                ops.interact_backward(cfg.arch_interaction_op, x, feats, g[:, :self.num_int],
+                                      cfg.arch_interaction_itself, grad_x=xg, grad_ly=gfeats)
+            st["rq"] = rq
+
+        def bottom_bwd(s1=None):
+            rq = st.pop("rq")
             xin = bufs["bot_act"][-1][:, :D]
             with prof("relu_bwd"):
                 g = ops.relu_backward(bufs["dx"], xin, out=bufs["gx"])
@@ -499,28 +496,33 @@ class DLRMTrainer:
                     g = bg[li % 2]
             if rq:
                 self._gemm(rq, side=c_bot)
-        ar = None
-        if self.world > 1:
-            if conc:
-                join()
-            ar = self._allreduce_dense()
-        # ---------------- backward: embeddings + fused update
-        if work is not None:
-            work.wait()
-        with prof("tbe_bwd"):
-            if self.T_local > 0:
-                mode = "rowwise_adagrad" if cfg.optimizer == "rwsadagrad" else "sgd"
-                ops.tbe_backward(mode, self.weights, self.row_base, self.T_local, B,
-                                 batch.indices, batch.offsets, bufs["dE"], lr=elr,
-                                 eps=cfg.adagrad_eps, momentum=self.momentum,
-                                 workspace=self._ws_tbe(batch.indices.numel()),
-                                 max_lookups_per_table=batch.max_per_table,
-                                 error_flag=self.tbe_error_flag)
-        if conc:
-            join()
-        if ar is not None:
-            ar.wait()
-        if not fused_opt:
+
+        def emb_bwd():  # embedding backward + fused update
+            with prof("tbe_bwd"):
+                if self.T_local > 0:
+                    mode = "rowwise_adagrad" if cfg.optimizer == "rwsadagrad" else "sgd"
+                    ops.tbe_backward(mode, self.weights, self.row_base, self.T_local, B,
+                                     batch.indices, batch.offsets, bufs["dE"], lr=elr,
+                                     eps=cfg.adagrad_eps, momentum=self.momentum,
+                                     workspace=self._ws_tbe(batch.indices.numel()),
+                                     max_lookups_per_table=batch.max_per_table,
+                                     error_flag=self.tbe_error_flag)
+
+        def backward_single():  # one GPU: bottom backward || embedding backward
+            s0, s1 = streams()
+            if c_bot:
+                rq = st["rq"]
+                if rq:
+                    self._gemm(rq)
+                st["rq"] = []
+                s1.wait_stream(s0)
+            with side_if(c_bot, s1):
+                bottom_bwd()
+            emb_bwd()
+            if c_bot:
+                s0.wait_stream(s1)
+
+        def dense_update():
             with prof("dense_update"):
                 scale = 1.0 / self.world
                 if cfg.optimizer == "sgd":
@@ -530,8 +532,65 @@ class DLRMTrainer:
                         ops.scale_(self.grads, scale)
                     ops.adagrad_update(self.params, self.grads, self.adagrad_sum, lr,
                                        cfg.adagrad_eps)
-        self.step_count += 1
-        return bufs["prob"], bufs["loss"]
+
+        def done():
+            self.step_count += 1
+
+        if not dist:
+            segs = [("gpu", fwd_single), ("gpu", middle), ("gpu", backward_single)]
+            if not fused_opt:
+                segs.append(("gpu", dense_update))
+            return segs + [("comm", done)]
+        # multi GPU (distributed_forward, dlrm_s_pytorch.py:686-730): the pooled-embedding
+        # all-to-all overlaps the bottom MLP; its reverse overlaps the bottom backward; the
+        # dense all-reduce overlaps the embedding backward
+        return [
+            ("gpu", lookup),
+            ("comm", lambda: st.__setitem__("a2a", self._alltoall_fwd(bufs, Bl))),
+            ("gpu", bottom_fwd),
+            ("comm", lambda: st.pop("a2a").wait()),
+            ("gpu", middle),
+            ("comm", lambda: st.__setitem__("a2a", self._alltoall_bwd(bufs, Bl))),
+            ("gpu", bottom_bwd),
+            ("comm", lambda: st.__setitem__("ar", self._allreduce_dense())),
+            ("comm", lambda: st.pop("a2a").wait()),
+            ("gpu", emb_bwd),
+            ("comm", lambda: st.pop("ar").wait()),
+            ("gpu", dense_update),
+            ("comm", done),
+        ]
+
+    def capture(self, batch: Batch, pool=None):
+        """A replayable step for ``batch``: its "gpu" segments captured as hipGraphs (one
+        graph on one GPU; a few graphs around the collectives on several), "comm" items run
+        eagerly between them.  Run one eager step of this batch size first (allocations).
+        Returns a callable; each call is one full training step on the captured buffers."""
+        items = []
+        pending = []
+        segs = self.segments(batch)
+
+        def flush():
+            if not pending:
+                return
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                for fn in pending:
+                    fn()
+            items.append(g.replay)
+            pending.clear()
+
+        for kind, fn in segs:
+            if kind == "gpu":
+                pending.append(fn)
+            else:
+                flush()
+                items.append(fn)
+        flush()
+
+        def run():
+            for f in items:
+                f()
+        return run
 
     def check_errors(self) -> None:
         """Raise (ops.TBEIndexError / ValueError) if any step since the last check hit an

@@ -45,7 +45,7 @@ def _batches(n, B):
     return out
 
 
-def _worker(rank, W, port, sharder, q):
+def _worker(rank, W, port, sharder, q, graph=False):
     try:
         sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd")]
         import torch.distributed as dist
@@ -57,8 +57,17 @@ def _worker(rank, W, port, sharder, q):
         tr = DLRMTrainer.from_oracle(cfg, ref, device="cuda:0", rank=rank, world_size=W,
                                      process_group=dist.group.WORLD)
         res = {"Z": [], "E": [], "local": tr.local_tables}
-        for X, lS_o, lS_i, T in _batches(3, 12):
-            Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
+        batches = [tr.make_batch(X, lS_o, lS_i, T) for X, lS_o, lS_i, T in _batches(3, 12)]
+        runs = [lambda b=b: tr.step(b) for b in batches]
+        if graph:  # step 0 eager (allocations), steps 1-2 replayed from captured segments
+            tr.step(batches[0])
+            torch.cuda.synchronize()
+            runs = [None] + [tr.capture(b) for b in batches[1:]]
+        for i, b in enumerate(batches):
+            if runs[i] is not None:
+                runs[i]()
+            bufs = tr._bufs[(b.X.shape[0], b.X.shape[0] * W)]
+            Z, E = bufs["prob"], bufs["loss"]
             res["Z"].append(Z.cpu().numpy())
             res["E"].append(float(E.cpu()))
         torch.cuda.synchronize()
@@ -72,8 +81,11 @@ def _worker(rank, W, port, sharder, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("sharder", ["naive", "greedy"])
-def test_two_ranks_match_oracle_distributed_step(sharder):
+@pytest.mark.parametrize("sharder,graph", [("naive", False), ("greedy", False),
+                                           ("greedy", True)])
+def test_two_ranks_match_oracle_distributed_step(sharder, graph):
+    """graph=True: steps replayed from trainer.capture (kernel segments as hipGraphs, the
+    exchanges eager between them), the bench's multi-GPU path."""
     import oracle as O
     from conftest import fp32_close
     from dlrm_hip.sharders import shard
@@ -81,7 +93,7 @@ def test_two_ranks_match_oracle_distributed_step(sharder):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, W, port, sharder, q)) for r in range(W)]
+    ps = [ctx.Process(target=_worker, args=(r, W, port, sharder, q, graph)) for r in range(W)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(W))
