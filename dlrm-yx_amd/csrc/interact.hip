@@ -319,6 +319,211 @@ __global__ __launch_bounds__(256) void interact_dot_fwd_v3(int B, int F, FeatArg
   }
 }
 
+// ------------------------------------ LDS-staged kernels (compile-time D) --
+// One wave per sample, four waves per workgroup stepping through the batch together.
+// Loads and stores move whole feature rows as float4 with C4 = D/4 lanes per row, so a
+// wave-instruction touches 64/C4 rows; the row pointers of an instruction are picked
+// from the (uniform) kernel arguments with v_cndmask, never lane-indexed (a lane-indexed
+// kernarg read compiles to a waterfall loop).
+template <int D>
+__device__ __forceinline__ const float* row_ptr(const FeatArgs& fa, int F, int64_t b, int i0,
+                                                int sub) {
+  constexpr int RPI = 64 / (D / 4);
+  const float* p = fa.ptr[0];
+  int64_t bs = 0;
+#pragma unroll
+  for (int j = 0; j < RPI; ++j) {
+    const int f = i0 + j;
+    const float* pj = f < F ? fa.ptr[f] : fa.ptr[0];
+    const int64_t bj = f < F ? fa.bs[f] : 0;
+    if (sub == j) p = pj, bs = bj;
+  }
+  return p + b * bs;
+}
+
+template <int D>
+__device__ __forceinline__ float* grad_row_ptr(const GradArgs& ga, int F, int64_t b, int i0,
+                                               int sub) {
+  constexpr int RPI = 64 / (D / 4);
+  float* p = ga.ptr[0];
+  int64_t bs = 0;
+#pragma unroll
+  for (int j = 0; j < RPI; ++j) {
+    const int f = i0 + j;
+    float* pj = f < F ? ga.ptr[f] : ga.ptr[0];
+    const int64_t bj = f < F ? ga.bs[f] : 0;
+    if (sub == j) p = pj, bs = bj;
+  }
+  return p + b * bs;
+}
+
+// Forward: T (F x D) -> LDS with coalesced float4 loads; lane (f, h) then feeds T[f][k] for
+// its k-half as both MFMA operands (Z = T T^T, two accumulator chains); the strict lower
+// triangle and x are staged in LDS in output order and written as whole float4 rows.
+template <int D>
+__global__ __launch_bounds__(256) void interact_dot_fwd_v4(int B, int F, FeatArgs fa, int self,
+                                                           float* __restrict__ out,
+                                                           int64_t ld_out, int width,
+                                                           int vec_out) {
+  constexpr int DP = D + 4, C4 = D / 4, RPI = 64 / C4, KH = D / 2;
+  constexpr int OUTP = D + 32 * 33 / 2 + 4;  // x + <= 528 pairs, rounded
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = lane >> 5, l32 = lane & 31;
+  float* Tl = lds + wave * (32 * DP + OUTP);
+  float* Ol = Tl + 32 * DP;
+  const int sub = lane / C4, c = lane - sub * C4;
+  const bool rowok = l32 < F;
+  for (int64_t b0 = (int64_t)blockIdx.x * 4; b0 < B; b0 += (int64_t)gridDim.x * 4) {
+    const int64_t b = b0 + wave;
+    const bool active = b < B;
+    if (active) {
+      for (int i0 = 0; i0 < F; i0 += RPI) {
+        const int f = i0 + sub;
+        const float* src = row_ptr<D>(fa, F, b, i0, sub);
+        if (f < F)
+          *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) =
+              *reinterpret_cast<const float4*>(src + 4 * c);
+      }
+    }
+    __syncthreads();
+    if (active) {
+      const float* trow = Tl + l32 * DP + h * KH;
+      f32x16 acc0, acc1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+#pragma unroll
+      for (int q = 0; q < KH / 4; ++q) {
+        float4 v = *reinterpret_cast<const float4*>(trow + 4 * q);
+        if (!rowok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, v.x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, v.y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, v.z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, v.w, acc1, 0, 0, 0);
+      }
+      for (int d = lane; d < D; d += 64) Ol[d] = Tl[d];  // x
+      const int j = l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (i < F && (self ? i >= j : i > j)) Ol[D + pair_index(i, j, self)] = acc0[r] + acc1[r];
+      }
+    }
+    __syncthreads();
+    if (active) {
+      float* orow = out + b * ld_out;
+      if (vec_out) {
+        const int w4 = width / 4;
+        for (int q = lane; q < w4; q += 64)
+          *reinterpret_cast<float4*>(orow + 4 * q) = *reinterpret_cast<const float4*>(Ol + 4 * q);
+        for (int q = 4 * w4 + lane; q < width; q += 64) orow[q] = Ol[q];
+      } else {
+        for (int q = lane; q < width; q += 64) orow[q] = Ol[q];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Backward: T and the sample's dR row -> LDS (coalesced); S = G + G^T row by row from
+// the staged dR; dT = S T per 32-column block on MFMA, each block written back over the
+// T columns it consumed, then every feature's gradient row leaves as whole float4 rows.
+// Feature 0 (the bottom-MLP output x) gets dR[0:D] added and, with relu_x, the ReLU' mask
+// of x applied (the backward of the bottom MLP's last ReLU, fused).
+template <int D>
+__global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArgs fa, int self,
+                                                           const float* __restrict__ gout,
+                                                           int64_t ld_g, GradArgs ga,
+                                                           int relu_x, int vec_g) {
+  constexpr int DP = D + 4, C4 = D / 4, RPI = 64 / C4;
+  constexpr int GP = D + 32 * 33 / 2 + 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = lane >> 5, l32 = lane & 31;
+  float* Tl = lds + wave * (32 * DP + GP);
+  float* Gl = Tl + 32 * DP;
+  const int sub = lane / C4, c = lane - sub * C4;
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  const int width = D + npairs;
+  for (int64_t b0 = (int64_t)blockIdx.x * 4; b0 < B; b0 += (int64_t)gridDim.x * 4) {
+    const int64_t b = b0 + wave;
+    const bool active = b < B;
+    if (active) {
+      for (int i0 = 0; i0 < 32; i0 += RPI) {  // rows >= F are zero (they meet S's zeros)
+        const int f = i0 + sub;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float* src = row_ptr<D>(fa, F, b, i0, sub);
+        if (f < F) v = *reinterpret_cast<const float4*>(src + 4 * c);
+        *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) = v;
+      }
+      const float* grow = gout + b * ld_g;
+      if (vec_g) {
+        const int w4 = width / 4;
+        for (int q = lane; q < w4; q += 64)
+          *reinterpret_cast<float4*>(Gl + 4 * q) = *reinterpret_cast<const float4*>(grow + 4 * q);
+        for (int q = 4 * w4 + lane; q < width; q += 64) Gl[q] = grow[q];
+      } else {
+        for (int q = lane; q < width; q += 64) Gl[q] = grow[q];
+      }
+    }
+    __syncthreads();
+    if (active) {
+      // S row l32, columns k = 16h + s: symmetric scatter of dR's pair gradients
+      float sv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = 16 * h + s, i = l32;
+        float v = 0.f;
+        if (i < F && k < F) {
+          if (i == k)
+            v = self ? 2.f * Gl[D + pair_index(i, i, true)] : 0.f;
+          else
+            v = Gl[D + (i > k ? pair_index(i, k, self) : pair_index(k, i, self))];
+        }
+        sv[s] = v;
+      }
+#pragma unroll
+      for (int n0 = 0; n0 < D; n0 += 32) {
+        const int n = n0 + l32;
+        float bv[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bv[s] = n < D ? Tl[(16 * h + s) * DP + n] : 0.f;
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sv[s], bv[s], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (n < D) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (i < F) {
+              float v = acc[r];
+              if (i == 0) {
+                v += Gl[n];
+                if (relu_x && !(Tl[n] > 0.f)) v = 0.f;
+              }
+              Tl[i * DP + n] = v;
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();
+    if (active) {
+      for (int i0 = 0; i0 < F; i0 += RPI) {
+        const int f = i0 + sub;
+        float* dst = grad_row_ptr<D>(ga, F, b, i0, sub);
+        if (f < F)
+          *reinterpret_cast<float4*>(dst + 4 * c) = *reinterpret_cast<const float4*>(Tl + f * DP + 4 * c);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------- generic VALU path (F > 32) --
 __global__ __launch_bounds__(256) void interact_dot_fwd_generic(int B, int F, int D, FeatArgs fa,
                                                                 int self, float* __restrict__ out,
@@ -392,6 +597,16 @@ __global__ __launch_bounds__(256) void interact_cat_bwd(int B, int F, int D,
   ga.ptr[f][b * ga.bs[f] + d] = gout[b * ld_g + rem];
 }
 
+// ReLU' of x applied to its gradient (fallback paths of relu_x): g0 *= (x > 0).
+__global__ __launch_bounds__(256) void relu_mask_kernel(int B, int D, const float* __restrict__ x,
+                                                        int64_t xbs, float* __restrict__ g,
+                                                        int64_t gbs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * D) return;
+  const int64_t b = i / D, d = i - b * D;
+  if (!(x[b * xbs + d] > 0.f)) g[b * gbs + d] = 0.f;
+}
+
 int fill_feat(FeatArgs& fa, int F, const float* const* ptrs, const int64_t* bs, const char* name) {
   DLRM_ARG(ptrs && bs, "%s: null feature arrays", name);
   for (int f = 0; f < F; ++f) {
@@ -442,9 +657,22 @@ extern "C" int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D,
   int rc = fill_feat(fa, F, feat_ptrs, feat_bstrides, name);
   if (rc) return rc;
   hipStream_t st = dlrm::as_stream(stream);
-  // v3 (register-only, one wave per sample) for the compile-time D; v1 otherwise
+  // v4 (LDS-staged, coalesced rows) for the compile-time D; v3 / v1 otherwise
   const bool fast = F <= 32 && (D == 16 || D == 32 || D == 64 || D == 128) &&
                     aligned_feats(fa, F) && !getenv("DLRM_INTERACT_V1");
+  if (fast && !getenv("DLRM_INTERACT_V3")) {
+    const int width = D + npairs;
+    const int vec_out = ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 4 == 0) ? 1 : 0;
+    const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
+    const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
+#define L4(DD)                                                                                \
+  hipLaunchKernelGGL(interact_dot_fwd_v4<DD>, dim3(grid), dim3(256), lds, st, B, F, fa,        \
+                     self_interaction ? 1 : 0, out, ld_out, width, vec_out)
+    if (D == 16) L4(16); else if (D == 32) L4(32); else if (D == 64) L4(64); else L4(128);
+#undef L4
+    DLRM_LAUNCH_CHECK(name);
+    return DLRM_OK;
+  }
   if (fast) {
     const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 4096);
 #define L3(DD)                                                                          \
@@ -475,7 +703,7 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
                                           const int64_t* feat_bstrides, int32_t self_interaction,
                                           const float* grad_out, int64_t ld_gout,
                                           float* const* grad_ptrs, const int64_t* grad_bstrides,
-                                          dlrm_stream_t stream) {
+                                          int32_t relu_x, dlrm_stream_t stream) {
   const char* name = "dlrm_interact_dot_backward";
   DLRM_ARG(B >= 0 && F >= 1 && F <= kMaxF && D > 0, "%s: need F in [1,64], D > 0", name);
   if (B == 0) return DLRM_OK;
@@ -489,9 +717,25 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
   rc = fill_grad(ga, F, grad_ptrs, grad_bstrides, name);
   if (rc) return rc;
   hipStream_t st = dlrm::as_stream(stream);
-  // v2 (LDS-staged T, S rows straight from dR) for the compile-time D; v1 otherwise
+  // v3 (LDS-staged T and dR, coalesced rows, ReLU' fused) for the compile-time D;
+  // v2 / v1 otherwise (ReLU' then as a separate pass)
   const bool fast = F <= 32 && (D == 16 || D == 32 || D == 64 || D == 128) &&
                     aligned_feats(fa, F) && !getenv("DLRM_INTERACT_V1");
+  bool grads_aligned = true;
+  for (int f = 0; f < F; ++f)
+    if ((reinterpret_cast<uintptr_t>(ga.ptr[f]) & 15) || (ga.bs[f] & 3)) grads_aligned = false;
+  if (fast && grads_aligned && !getenv("DLRM_INTERACT_V2")) {
+    const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
+    const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
+    const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
+#define L3B(DD)                                                                               \
+  hipLaunchKernelGGL(interact_dot_bwd_v3<DD>, dim3(grid), dim3(256), lds, st, B, F, fa,        \
+                     self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g)
+    if (D == 16) L3B(16); else if (D == 32) L3B(32); else if (D == 64) L3B(64); else L3B(128);
+#undef L3B
+    DLRM_LAUNCH_CHECK(name);
+    return DLRM_OK;
+  }
   if (fast) {
     const size_t lds = 4 * 32 * (size_t)(D + 4) * sizeof(float);
     const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 2048);
@@ -500,21 +744,25 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
                      self_interaction ? 1 : 0, grad_out, ld_gout, ga)
     if (D == 16) L2(16); else if (D == 32) L2(32); else if (D == 64) L2(64); else L2(128);
 #undef L2
-    DLRM_LAUNCH_CHECK(name);
-    return DLRM_OK;
-  }
-  const size_t per_wave = (size_t)(F * (D + 1) + 32 * 33) * sizeof(float);
-  const int wpb = waves_for(per_wave);
-  if (F <= 32 && wpb > 0) {
-    hipLaunchKernelGGL(interact_dot_bwd_mfma, dim3(grid_for(B, wpb)), dim3(64 * wpb),
-                       per_wave * wpb, st, B, F, D, fa,
-                       self_interaction ? 1 : 0, grad_out, ld_gout, ga);
   } else {
-    const int64_t n = (int64_t)B * F * D;
-    hipLaunchKernelGGL(interact_dot_bwd_generic, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0, st,
-                       B, F, D, fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga);
+    const size_t per_wave = (size_t)(F * (D + 1) + 32 * 33) * sizeof(float);
+    const int wpb = waves_for(per_wave);
+    if (F <= 32 && wpb > 0) {
+      hipLaunchKernelGGL(interact_dot_bwd_mfma, dim3(grid_for(B, wpb)), dim3(64 * wpb),
+                         per_wave * wpb, st, B, F, D, fa,
+                         self_interaction ? 1 : 0, grad_out, ld_gout, ga);
+    } else {
+      const int64_t n = (int64_t)B * F * D;
+      hipLaunchKernelGGL(interact_dot_bwd_generic, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0, st,
+                         B, F, D, fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga);
+    }
   }
   DLRM_LAUNCH_CHECK(name);
+  if (relu_x) {
+    hipLaunchKernelGGL(relu_mask_kernel, dim3(dlrm::ceil_div((int64_t)B * D, 256)), dim3(256), 0,
+                       st, B, D, fa.ptr[0], fa.bs[0], ga.ptr[0], ga.bs[0]);
+    DLRM_LAUNCH_CHECK(name);
+  }
   return DLRM_OK;
 }
 

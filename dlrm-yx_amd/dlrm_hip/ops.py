@@ -242,8 +242,9 @@ def interact_forward(op: str, x: torch.Tensor, ly, self_interaction: bool = Fals
 
 def interact_backward(op: str, x: torch.Tensor, ly, grad_out: torch.Tensor,
                       self_interaction: bool = False, grad_x: Optional[torch.Tensor] = None,
-                      grad_ly=None):
-    """Returns (grad_x, grad_ly) with grad_ly shaped like ly ([B,T,D] or list of [B,D])."""
+                      grad_ly=None, relu_x: bool = False):
+    """Returns (grad_x, grad_ly) with grad_ly shaped like ly ([B,T,D] or list of [B,D]).
+    relu_x: grad_x also gets ReLU'(x) applied (x = output of a ReLU layer; dot only)."""
     feats, strides = feature_views(x, ly)
     B, D = x.shape
     F = len(feats)
@@ -260,10 +261,12 @@ def interact_backward(op: str, x: torch.Tensor, ly, grad_out: torch.Tensor,
     g = grad_out if grad_out.stride(1) == 1 else grad_out.contiguous()  # row stride is passed
     if op == "dot":
         _lib.call("dlrm_interact_dot_backward", B, F, D, ptrs, bs, int(self_interaction), _p(g),
-                  g.stride(0), gptrs, gbs, _stream(x.device))
+                  g.stride(0), gptrs, gbs, int(relu_x), _stream(x.device))
     else:
         _lib.call("dlrm_interact_cat_backward", B, F, D, _p(g), g.stride(0), gptrs, gbs,
                   _stream(x.device))
+        if relu_x:
+            relu_backward(grad_x, x, out=grad_x)
     return grad_x, grad_ly
 
 

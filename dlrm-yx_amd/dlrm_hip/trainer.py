@@ -471,17 +471,16 @@ class DLRMTrainer:
                 self._gemm([w])
                 rq = [r] if r is not None else []
                 g, gi = G[gn], gn
-            xg, gfeats = self._features(bufs, Bl, grad=True)
-            with prof("interaction_bwd"):
+            _, gfeats = self._features(bufs, Bl, grad=True)
+            with prof("interaction_bwd"):  # + the backward of the bottom MLP's last ReLU
                 ops.interact_backward(cfg.arch_interaction_op, x, feats, g[:, :self.num_int],
-                                      cfg.arch_interaction_itself, grad_x=xg, grad_ly=gfeats)
+                                      cfg.arch_interaction_itself, grad_x=bufs["gx"],
+                                      grad_ly=gfeats, relu_x=True)
             st["rq"] = rq
 
         def bottom_bwd(s1=None):
             rq = st.pop("rq")
-            xin = bufs["bot_act"][-1][:, :D]
-            with prof("relu_bwd"):
-                g = ops.relu_backward(bufs["dx"], xin, out=bufs["gx"])
+            g = bufs["gx"]  # dLoss/d(pre-ReLU bottom output), from the interaction backward
             bg = [bufs["gb"][0], bufs["gb"][1]]
             for li in range(self.n_bot - 1, -1, -1):
                 L = self.bot[li]

@@ -206,12 +206,15 @@ int dlrm_qr_combine_backward(int32_t op, int64_t n_rows, int64_t D, const float*
 int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D, const float* const* feat_ptrs,
                               const int64_t* feat_bstrides, int32_t self_interaction,
                               float* out, int64_t ld_out, dlrm_stream_t stream);
-/* Writes (overwrites) grad of every feature: grad_ptrs[f] + b*grad_bstrides[f]. */
+/* Writes (overwrites) grad of every feature: grad_ptrs[f] + b*grad_bstrides[f].
+ * relu_x != 0 also applies ReLU'(x) to feature 0's gradient (x = the bottom MLP's ReLU
+ * output: the backward of that ReLU, fused). */
 int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
                                const float* const* feat_ptrs, const int64_t* feat_bstrides,
                                int32_t self_interaction, const float* grad_out,
                                int64_t ld_gout, float* const* grad_ptrs,
-                               const int64_t* grad_bstrides, dlrm_stream_t stream);
+                               const int64_t* grad_bstrides, int32_t relu_x,
+                               dlrm_stream_t stream);
 /* Cat: out[b][f*D:(f+1)*D] = feature f. */
 int dlrm_interact_cat_forward(int32_t B, int32_t F, int32_t D, const float* const* feat_ptrs,
                               const int64_t* feat_bstrides, float* out, int64_t ld_out,

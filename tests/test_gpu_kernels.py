@@ -623,3 +623,34 @@ def test_gemm_partial_then_reduce_equals_full(ops, ones):
     ops.gemm_group([ops.reduce_problem(pp)], ws)
     torch.cuda.synchronize()
     assert torch.equal(W1, W2)
+
+
+@pytest.mark.parametrize("path", ["", "DLRM_INTERACT_V2", "DLRM_INTERACT_V1"])
+@pytest.mark.parametrize("D", [16, 128])
+def test_interact_backward_relu_x_and_paths(ops, monkeypatch, path, D):
+    """relu_x fuses ReLU'(x) into feature 0's gradient, on the LDS-staged kernel and on the
+    fallback paths (separate mask pass); all paths agree with autograd on a torch fp32
+    reference (bmm + tril gather), within the fp32 tolerance."""
+    if path:
+        monkeypatch.setenv(path, "1")
+    torch.manual_seed(D)
+    B, F = 70, 27
+    x = torch.randn(B, D)          # mixed signs: the mask matters
+    ly = torch.randn(B, F - 1, D)
+    gR = torch.randn(B, D + F * (F - 1) // 2)
+    xr = x.clone().requires_grad_(True)
+    lr_ = ly.clone().requires_grad_(True)
+    T = torch.cat([xr[:, None, :], lr_], 1)
+    Z = torch.bmm(T, T.transpose(1, 2))
+    li, lj = torch.tril_indices(F, F, -1)
+    R = torch.cat([xr, Z[:, li, lj]], 1)
+    (R * gR).sum().backward()
+    gx, gly = ops.interact_backward("dot", x.to(dev), ly.to(dev), gR.to(dev), relu_x=True)
+    ok, msg = fp32_close(gx.cpu().numpy(), (xr.grad * (x > 0)).numpy())
+    assert ok, msg
+    ok, msg = fp32_close(gly.cpu().numpy(), lr_.grad.numpy())
+    assert ok, msg
+    # forward on every path vs the same reference
+    out = ops.interact_forward("dot", x.to(dev), ly.to(dev))
+    ok, msg = fp32_close(out.cpu().numpy(), R.detach().numpy())
+    assert ok, msg
