@@ -21,6 +21,8 @@
 // batch) are thus split over many lane-groups instead of serialising one of them, and
 // the summation order is fixed by the sort: bitwise reproducible run to run.
 #include <hipcub/hipcub.hpp>
+#include <cstdio>
+#include <cstdlib>
 
 #include "tbe_common.hpp"
 
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
 
 // Per-table sort (replaces keys + device radix sort when every table's lookups fit in
 // one workgroup): workgroup t builds table t's local row keys (out-of-range rows ->
-// rows_t) and sorts (key, position) with a stable block radix sort over only
+// rows_t) and sorts (key, position) with a stable LDS radix sort over only
 // bit_width(rows_t) bits, then writes global rows / positions into the table's own range
 // of the output.  Stable on positions, so the order equals the device-wide stable sort.
 // Tables own disjoint row ranges and consecutive lookup ranges, so the concatenation is
@@ -75,17 +77,108 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
 // (the caller's max_lookups_per_table was an underestimate) is not sorted: all its lookups
 // become sentinels (no update, no stale keys, no out-of-bounds row) and bit
 // DLRM_TBE_ERR_TABLE_CAP is raised in *err.
-constexpr int kSegThreads = 512;
-constexpr int kSegItems = 8;
-constexpr int kSegCap = kSegThreads * kSegItems;  // 4096 lookups per table
+constexpr int kSegThreads = 512, kSegItems = 8;
+constexpr int kSegCap = kSegThreads * kSegItems;  // lookups per table
+constexpr int kSegWaves = kSegThreads / 64;
+constexpr int kDigitBits = 8;
+
+struct SegSortLds {
+  uint32_t key[kSegCap];
+  int32_t pos[kSegCap];
+  uint32_t cnt[(1 << kDigitBits) * (kSegWaves + 1)];  // per (digit, wave): count, then offset
+  uint32_t wsum[kSegWaves];
+  int32_t bag[kSegCap];  // bag of each local position
+};
+
+// Stable LSD radix sort of kSegCap (key, pos) pairs, 8-bit digits.  Items sit in a
+// wave-striped arrangement: item u of lane l in wave w is element w*512 + u*64 + l.  A
+// digit's rank inside a wave comes from ballots (lanes holding the same digit, those below
+// this lane) plus the wave's running count of that digit in LDS; one scan over the
+// (digit, wave) counts gives every element its destination.  Order inside a digit is
+// (wave, item, lane) = element order: stable.
+__device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
+                                               int32_t (&pos)[kSegItems], int bits,
+                                               SegSortLds& sm) {
+  constexpr int NB = 1 << kDigitBits;
+  constexpr int NC = NB * kSegWaves;
+  constexpr int CPT = NC / kSegThreads;  // counters per thread in the scan
+  constexpr int CS = kSegWaves + 1;      // counter row stride: digits of one wave's lanes
+                                         // land in distinct LDS banks
+  static_assert(kSegWaves % CPT == 0, "scan entries of one thread share a digit");
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  const uint64_t below = (1ull << l) - 1;
+  for (int s = 0; s < bits; s += kDigitBits) {
+    for (int i = tid; i < NB * CS; i += kSegThreads) sm.cnt[i] = 0;
+    __syncthreads();
+    uint32_t rank[kSegItems];
+    uint32_t dig[kSegItems];
+#pragma unroll
+    for (int u = 0; u < kSegItems; ++u) {
+      const uint32_t d = (key[u] >> s) & (NB - 1);
+      uint64_t peers = ~0ull;
+#pragma unroll
+      for (int b = 0; b < kDigitBits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? bal : ~bal;
+      }
+      const uint32_t r = __popcll(peers & below);
+      const uint32_t c = __popcll(peers);
+      const uint32_t base = sm.cnt[d * CS + w];
+      rank[u] = base + r;
+      dig[u] = d;
+      if (r == c - 1) sm.cnt[d * CS + w] = base + c;  // last peer publishes
+    }
+    __syncthreads();
+    // exclusive scan of cnt in (digit, wave) order
+    uint32_t v[CPT];
+    uint32_t tsum = 0;
+    // logical entries tid*CPT .. +CPT-1 = digit jd, waves jw .. jw+CPT-1
+    const int jd = (tid * CPT) / kSegWaves, jw = (tid * CPT) % kSegWaves;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      v[k] = sm.cnt[jd * CS + jw + k];
+      tsum += v[k];
+    }
+    uint32_t inc = tsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (l >= o) inc += y;
+    }
+    if (l == 63) sm.wsum[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - tsum;
+    for (int k = 0; k < w; ++k) run += sm.wsum[k];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      sm.cnt[jd * CS + jw + k] = run;
+      run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kSegItems; ++u) {
+      const uint32_t dst = sm.cnt[dig[u] * CS + w] + rank[u];
+      sm.key[dst] = key[u];
+      sm.pos[dst] = pos[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kSegItems; ++u) {
+      const int e = w * (kSegItems * 64) + u * 64 + l;
+      key[u] = sm.key[e];
+      pos[u] = sm.pos[e];
+    }
+    __syncthreads();
+  }
+}
+
 template <typename IdxT, typename OffT>
-__global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
+__device__ __forceinline__ void segsort_body(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
-    int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
-  using BRS = hipcub::BlockRadixSort<uint32_t, kSegThreads, kSegItems, int32_t>;
-  __shared__ typename BRS::TempStorage temp;
-  const int t = blockIdx.x;
+    int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err, int t,
+    SegSortLds& sm) {
   const int tid = threadIdx.x;
   if (t == T) {  // lookups outside every bag
     const int64_t a = (int64_t)off[0], e = (int64_t)off[(int64_t)T * B];
@@ -101,11 +194,11 @@ __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
   const int64_t n64 = (int64_t)off[(int64_t)(t + 1) * B] - s0;  // <= kSegCap (contract)
   const int64_t rb = row_base[t];
   const int64_t nrows = row_base[t + 1] - rb;
-  for (int b = tid; b < B; b += blockDim.x) {
-    const int64_t a = (int64_t)off[(int64_t)t * B + b], e = (int64_t)off[(int64_t)t * B + b + 1];
-    for (int64_t p = a; p < e; ++p) bag_of[p] = t * B + b;
-  }
   if (n64 > kSegCap) {  // contract violated: skip the table, report
+    for (int b = tid; b < B; b += blockDim.x) {
+      const int64_t a = (int64_t)off[(int64_t)t * B + b], e = (int64_t)off[(int64_t)t * B + b + 1];
+      for (int64_t p = a; p < e; ++p) bag_of[p] = t * B + b;
+    }
     for (int64_t i = tid; i < n64; i += blockDim.x) {
       keys_out[s0 + i] = sentinel;
       pos_out[s0 + i] = (int32_t)(s0 + i);
@@ -117,28 +210,89 @@ __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) <= nrows) ++bits;  // keys in [0, nrows]
   const uint32_t pad = bits >= 32 ? 0xffffffffu : (uint32_t)(((uint64_t)1 << bits) - 1);
+  const int w = tid >> 6, l = tid & 63;
+  // all global loads of the table are issued before the first one is consumed (one
+  // memory latency, not one per loop trip): the lookup rows, then the bag offsets
+  IdxT rv[kSegItems];
+#pragma unroll
+  for (int u = 0; u < kSegItems; ++u) {
+    const int i = w * (kSegItems * 64) + u * 64 + l;  // wave-striped element order
+    rv[u] = i < n ? idx[s0 + i] : (IdxT)0;
+  }
+  // bag of each local position, in LDS; written out below in SORTED order (bag_of[i] =
+  // bag of the i-th sorted lookup), which spares the block kernel a dependent load
+  const OffT* toff = off + (int64_t)t * B;
+  constexpr int kBU = 4;  // bags per thread per round, loads in flight
+  for (int b0 = 0; b0 < B; b0 += kBU * kSegThreads) {
+    int64_t ba[kBU], be[kBU];
+#pragma unroll
+    for (int k = 0; k < kBU; ++k) {
+      const int b = b0 + k * kSegThreads + tid;
+      ba[k] = b < B ? (int64_t)toff[b] : 0;
+      be[k] = b < B ? (int64_t)toff[b + 1] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kBU; ++k) {
+      const int32_t bag = t * B + b0 + k * kSegThreads + tid;
+      for (int64_t p = ba[k]; p < be[k]; ++p) sm.bag[p - s0] = bag;
+    }
+  }
   uint32_t key[kSegItems];
   int32_t pos[kSegItems];
 #pragma unroll
   for (int u = 0; u < kSegItems; ++u) {
-    const int i = tid * kSegItems + u;  // blocked arrangement = position order
+    const int i = w * (kSegItems * 64) + u * 64 + l;
     key[u] = pad;
     pos[u] = i;
     if (i < n) {
-      const int64_t r = (int64_t)idx[s0 + i];
+      const int64_t r = (int64_t)rv[u];
       key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
       if (key[u] == (uint32_t)nrows && err) atomicOr(err, DLRM_TBE_ERR_INDEX);
     }
   }
-  BRS(temp).Sort(key, pos, 0, bits);
+  __syncthreads();  // bags complete
+  seg_radix_sort(key, pos, bits, sm);
 #pragma unroll
   for (int u = 0; u < kSegItems; ++u) {
-    const int i = tid * kSegItems + u;
+    const int i = w * (kSegItems * 64) + u * 64 + l;
     if (i < n) {
       keys_out[s0 + i] = key[u] < (uint32_t)nrows ? (uint32_t)(rb + key[u]) : sentinel;
       pos_out[s0 + i] = (int32_t)(s0 + pos[u]);
+      bag_of[s0 + i] = sm.bag[pos[u]];
     }
   }
+}
+
+template <typename IdxT, typename OffT>
+__global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
+    int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
+    int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
+  __shared__ SegSortLds sm;
+  segsort_body<IdxT, OffT>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of, err,
+                           blockIdx.x, sm);
+}
+
+// The forward gather and the backward's per-table sort in ONE launch: the sort depends only
+// on the indices, and its T+1 latency-bound workgroups (LDS radix passes on T CUs) run beside
+// the bandwidth-bound gather instead of as a separate launch in the backward.  Blocks
+// [0, T] sort (started first), the rest gather.  512 threads per workgroup.
+constexpr int kPreThreads = kSegThreads;
+template <int LPB, int VW, int MAXV, typename IdxT, typename OffT>
+__global__ __launch_bounds__(kPreThreads) void tbe_fwd_presort_kernel(
+    const float* __restrict__ W, int64_t D, const int64_t* __restrict__ row_base, int T, int B,
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const float* __restrict__ psw,
+    float* __restrict__ out, int64_t out_bs, int32_t* __restrict__ err, int64_t N,
+    uint32_t sentinel, uint32_t* __restrict__ keys_out, int32_t* __restrict__ pos_out,
+    int32_t* __restrict__ bag_of) {
+  __shared__ SegSortLds sm;
+  if ((int)blockIdx.x <= T) {
+    segsort_body<IdxT, OffT>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of,
+                             err, blockIdx.x, sm);
+    return;
+  }
+  tbe_fwd_body<LPB, VW, MAXV, IdxT, OffT>(W, D, row_base, T, B, idx, off, psw, out, out_bs, err,
+                                          (int64_t)blockIdx.x - (T + 1), (int64_t)gridDim.x - (T + 1));
 }
 
 enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2 };
@@ -202,7 +356,69 @@ __device__ __forceinline__ void finalize_row(float* __restrict__ W, float* __res
   }
 }
 
-template <int LPB, int VW, int MAXV, typename KeyT, int MODE>
+// finalize_row with the row's weights (and momentum) already in registers: the load was
+// issued with the gradient rows, so the read-modify-write costs no extra HBM round trip.
+template <int LPB, int VW, int MAXV, int MODE>
+__device__ __forceinline__ void finalize_row_pf(float* __restrict__ W, float* __restrict__ mom,
+                                                int64_t D, int64_t row,
+                                                typename VecT<VW>::T (&g)[MAXV],
+                                                typename VecT<VW>::T (&w)[MAXV], float m0,
+                                                int gl, int nchunks, float lr, float eps) {
+  using V = typename VecT<VW>::T;
+  V* wrow = reinterpret_cast<V*>(W + row * D);
+  if (MODE == MODE_SGD) {
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int chunk = gl + c * LPB;
+      if (chunk < nchunks) {
+        V x = w[c];
+        vfma(x, -lr, g[c]);
+        wrow[chunk] = x;
+      }
+    }
+  } else if (MODE == MODE_DENSE) {
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int chunk = gl + c * LPB;
+      if (chunk < nchunks) {
+        V x = w[c];
+        vadd(x, g[c]);
+        wrow[chunk] = x;
+      }
+    }
+  } else {
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c)
+      if (gl + c * LPB < nchunks) sq += vdot(g[c]);
+#pragma unroll
+    for (int m = LPB / 2; m >= 1; m >>= 1) sq += __shfl_xor(sq, m, kWave);
+    const float mnew = m0 + sq / (float)D;
+    if (gl == 0) mom[row] = mnew;
+    const float denom = sqrtf(mnew) + eps;
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int chunk = gl + c * LPB;
+      if (chunk < nchunks) {
+        V x = w[c];
+        V u = g[c];
+        if constexpr (VW == 4) {
+          u.x /= denom;
+          u.y /= denom;
+          u.z /= denom;
+          u.w /= denom;
+        } else {
+          u /= denom;
+        }
+        vfma(x, -lr, u);
+        wrow[chunk] = x;
+      }
+    }
+  }
+}
+
+// SB: bag_of is indexed by sorted position (per-table sort) instead of by lookup position
+template <int LPB, int VW, int MAXV, typename KeyT, int MODE, bool SB>
 __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
     float* __restrict__ W, float* __restrict__ mom, int64_t D, int B,
     const KeyT* __restrict__ keys, const int32_t* __restrict__ pos,
@@ -236,12 +452,24 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
     int64_t seg_a = i0;
     bool have = false;
 
+    // PF: the weight row (and momentum) of every run start in a chunk is loaded together
+    // with the chunk's gradient rows (MAXV == 1 keeps that within the register budget)
+    constexpr bool PF = MAXV == 1;
+    V wcur[MAXV];
+    float mcur = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) vzero(wcur[c]);
+
     auto flush = [&](int64_t b_end) {
       if (cur == sentinel) return;
       const bool starts = (seg_a > i0) || !has_prev || (prev_key != cur);
       const bool ends = (b_end < i1) || !has_next || (next_key != cur);
       if (starts && ends) {
-        finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)cur, acc, gl, nchunks, lr, eps);
+        if constexpr (PF)
+          finalize_row_pf<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)cur, acc, wcur, mcur, gl,
+                                               nchunks, lr, eps);
+        else
+          finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)cur, acc, gl, nchunks, lr, eps);
       } else {
         V* dst = reinterpret_cast<V*>(partial + (2 * k + (seg_a == i0 ? 0 : 1)) * D);
 #pragma unroll
@@ -257,14 +485,20 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
       float my_w = 1.f;
       if (gl < n) {
         my_key = keys[base + gl];
-        const int32_t p = pos[base + gl];
-        const int32_t bag = bag_of[p];
+        int32_t bag;
+        if constexpr (SB) {
+          bag = bag_of[base + gl];
+          if (psw) my_w = psw[pos[base + gl]];
+        } else {
+          const int32_t p = pos[base + gl];
+          bag = bag_of[p];
+          if (psw) my_w = psw[p];
+        }
         if (bag >= 0) {
           const int t = bag / B;
           const int b = bag - t * B;
           my_off = (int64_t)b * gbs + (int64_t)t * D;
         }
-        if (psw) my_w = psw[p];
       }
       constexpr int U = LPB < CH ? LPB : CH;  // gradient rows in flight per group
       for (int j = 0; j < n; j += U) {
@@ -283,6 +517,8 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
           if (j + u >= n) ou[u] = -1;
         }
         V gv[U][MAXV];
+        V wv[PF ? U : 1][MAXV];
+        float mv[PF ? U : 1];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -295,6 +531,20 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
               vzero(gv[u][c]);
             }
           }
+          if constexpr (PF) {
+            // rows starting a run inside the chunk (repeats of one row load it once)
+            const bool lead = (j + u < n) && ku[u] != sentinel && (u == 0 || ku[u] != ku[u - 1]);
+            const V* wrow = reinterpret_cast<const V*>(W + (int64_t)ku[u] * D);
+#pragma unroll
+            for (int c = 0; c < MAXV; ++c) {
+              const int chunk = gl + c * LPB;
+              if (lead && chunk < nchunks)
+                wv[u][c] = wrow[chunk];
+              else
+                vzero(wv[u][c]);
+            }
+            mv[u] = (MODE == MODE_ADAGRAD && lead) ? mom[ku[u]] : 0.f;
+          }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -306,6 +556,11 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
               seg_a = base + j + u;
 #pragma unroll
               for (int c = 0; c < MAXV; ++c) vzero(acc[c]);
+              if constexpr (PF) {
+#pragma unroll
+                for (int c = 0; c < MAXV; ++c) wcur[c] = wv[u][c];
+                mcur = mv[u];
+              }
             }
 #pragma unroll
             for (int c = 0; c < MAXV; ++c) vadd(acc[c], gv[u][c]);
@@ -378,11 +633,12 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
       else
         vzero(acc[c]);
     }
-    // partials of blocks k+1 .. kend in block order, 8 loads in flight
-    for (int64_t kk0 = k + 1; kk0 <= kend; kk0 += 8) {
-      V pv[8][MAXV];
+    // partials of blocks k+1 .. kend in block order, NF loads in flight
+    constexpr int NF = MAXV <= 2 ? 16 : 8;
+    for (int64_t kk0 = k + 1; kk0 <= kend; kk0 += NF) {
+      V pv[NF][MAXV];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < NF; ++u) {
         const int64_t kk = kk0 + u;
         const V* s2 = reinterpret_cast<const V*>(partial + (2 * kk) * D);
 #pragma unroll
@@ -394,7 +650,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < NF; ++u)
         if (kk0 + u <= kend) {
 #pragma unroll
           for (int c = 0; c < MAXV; ++c) vadd(acc[c], pv[u][c]);
@@ -402,6 +658,11 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
     }
     finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)last, acc, gl, nchunks, lr, eps);
   }
+}
+
+// The per-table LDS sort applies (and dlrm_tbe_forward_presort can run it early).
+inline bool presort_applies(size_t key_bytes, int64_t max_seg, int64_t N) {
+  return key_bytes == 4 && max_seg > 0 && max_seg <= kSegCap && N < (int64_t)0x7fffffff;
 }
 
 inline int bit_width_u64(uint64_t v) {
@@ -450,17 +711,20 @@ template <typename KeyT, typename IdxT, typename OffT>
 int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
                const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
                const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
-               int64_t max_seg, int32_t* err, hipStream_t st, const char* name) {
+               int64_t max_seg, int32_t* err, int presorted, hipStream_t st, const char* name) {
   if (N == 0) return DLRM_OK;
   const KeyT sentinel = (KeyT)total_rows;
   const int end_bit = bit_width_u64((uint64_t)total_rows);
   BwdWs<KeyT> w = carve_bwd_ws<KeyT>(ws, N, D, end_bit);
   DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
                name, ws_bytes, w.total);
-  if (sizeof(KeyT) == 4 && max_seg > 0 && max_seg <= kSegCap && N < (int64_t)0x7fffffff) {
-    hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(kSegThreads), 0, st,
-                       static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base, T,
-                       B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),
+  const bool per_table = presort_applies(sizeof(KeyT), max_seg, N);
+  if (per_table && presorted) {
+    // this batch's per-table sort already ran inside dlrm_tbe_forward_presort
+  } else if (per_table) {
+    hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(kSegThreads), 0,
+                       st, static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base,
+                       T, B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),
                        w.pos_out, w.bag_of, err);
     DLRM_LAUNCH_CHECK(name);
   } else {
@@ -489,9 +753,14 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   if (blocks < 1) blocks = 1;
 #define LAUNCH2(LPB, VW, MV, MODE)                                                             \
   do {                                                                                         \
-    hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE>), dim3(blocks),          \
-                       dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw,   \
-                       gout, gbs, N, lr, eps, sentinel, w.partial);                            \
+    if (per_table)                                                                             \
+      hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE, true>), dim3(blocks),  \
+                         dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw, \
+                         gout, gbs, N, lr, eps, sentinel, w.partial);                          \
+    else                                                                                       \
+      hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE, false>), dim3(blocks), \
+                         dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw, \
+                         gout, gbs, N, lr, eps, sentinel, w.partial);                          \
     hipLaunchKernelGGL((tbe_bwd_combine_kernel<LPB, VW, MV, KeyT, MODE>), dim3(blocks),        \
                        dim3(256), 0, st, W, mom, D, w.keys_out, N, lr, eps, sentinel,          \
                        w.partial);                                                             \
@@ -534,7 +803,7 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
                  int B, const void* idx, int ib, const void* off, int ob, int64_t N,
                  int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
                  float eps, void* ws, size_t ws_bytes, int64_t max_seg, int32_t* err,
-                 dlrm_stream_t stream, const char* name) {
+                 int presorted, dlrm_stream_t stream, const char* name) {
   DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
@@ -547,7 +816,7 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
   const bool k32 = (uint64_t)total_rows < 0xFFFFFFFFull;
 #define BWD(K, I, O)                                                                     \
   return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
-                             gout, gbs, lr, eps, ws, ws_bytes, max_seg, err, st, name)
+                             gout, gbs, lr, eps, ws, ws_bytes, max_seg, err, presorted, st, name)
   if (k32) {
     if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
     if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
@@ -582,11 +851,12 @@ extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* r
                                      const float* grad_out, int64_t grad_batch_stride, float lr,
                                      int64_t max_lookups_per_table, void* workspace,
                                      size_t workspace_bytes, int32_t* error_flag,
-                                     dlrm_stream_t stream) {
+                                     int32_t presorted, dlrm_stream_t stream) {
   return bwd_dispatch(MODE_SGD, weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes,
-                      max_lookups_per_table, error_flag, stream, "dlrm_tbe_backward_sgd");
+                      max_lookups_per_table, error_flag, presorted, stream,
+                      "dlrm_tbe_backward_sgd");
 }
 
 extern "C" int dlrm_tbe_backward_rowwise_adagrad(
@@ -595,12 +865,12 @@ extern "C" int dlrm_tbe_backward_rowwise_adagrad(
     int64_t num_lookups, int64_t total_rows, const float* per_sample_weights,
     const float* grad_out, int64_t grad_batch_stride, float lr, float eps,
     int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes, int32_t* error_flag,
-    dlrm_stream_t stream) {
+    int32_t presorted, dlrm_stream_t stream) {
   DLRM_ARG(momentum, "dlrm_tbe_backward_rowwise_adagrad: null momentum");
   return bwd_dispatch(MODE_ADAGRAD, weights, momentum, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes,
-                      max_lookups_per_table, error_flag, stream,
+                      max_lookups_per_table, error_flag, presorted, stream,
                       "dlrm_tbe_backward_rowwise_adagrad");
 }
 
@@ -612,9 +882,101 @@ extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int
                                        const float* grad_out, int64_t grad_batch_stride,
                                        int64_t max_lookups_per_table, void* workspace,
                                        size_t workspace_bytes, int32_t* error_flag,
-                                       dlrm_stream_t stream) {
+                                       int32_t presorted, dlrm_stream_t stream) {
   return bwd_dispatch(MODE_DENSE, grad_weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes,
-                      max_lookups_per_table, error_flag, stream, "dlrm_tbe_backward_dense");
+                      max_lookups_per_table, error_flag, presorted, stream,
+                      "dlrm_tbe_backward_dense");
+}
+
+namespace {
+
+template <typename IdxT, typename OffT>
+int launch_fwd_presort(const float* W, int64_t D, const int64_t* row_base, int T, int B,
+                       const void* idx, const void* off, const float* psw, float* out,
+                       int64_t out_bs, int64_t N, int64_t total_rows, void* ws, size_t ws_bytes,
+                       int32_t* err, hipStream_t st) {
+  const char* name = "dlrm_tbe_forward_presort";
+  const int end_bit = bit_width_u64((uint64_t)total_rows);
+  BwdWs<uint32_t> w = carve_bwd_ws<uint32_t>(ws, N, D, end_bit);
+  DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu", name,
+               ws_bytes, w.total);
+  const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
+                    ((reinterpret_cast<uintptr_t>(out) & 15) == 0) && (out_bs % 4 == 0);
+  const int64_t nchunks = vec4 ? D / 4 : D;
+  int lpb = 1;
+  while (lpb < nchunks && lpb < 64) lpb <<= 1;
+  const int64_t maxv = dlrm::ceil_div(nchunks, lpb);
+  DLRM_REQUIRE(maxv <= 8, DLRM_ERR_UNSUPPORTED, "%s: D=%lld too large", name, (long long)D);
+  const int64_t nbags = (int64_t)T * B;
+  const int gpw = 64 / lpb;
+  int64_t gblocks = dlrm::ceil_div(dlrm::ceil_div(nbags, gpw), kPreThreads / 64);
+  if (gblocks > 8192) gblocks = 8192;
+  if (gblocks < 1) gblocks = 1;
+  const dim3 grid((unsigned)(T + 1 + gblocks)), block(kPreThreads);
+  const IdxT* ip = static_cast<const IdxT*>(idx);
+  const OffT* op = static_cast<const OffT*>(off);
+  const uint32_t sentinel = (uint32_t)total_rows;
+#define PRE(LPB, VW, MV)                                                                         \
+  hipLaunchKernelGGL((tbe_fwd_presort_kernel<LPB, VW, MV, IdxT, OffT>), grid, block, 0, st, W, D, \
+                     row_base, T, B, ip, op, psw, out, out_bs, err, N, sentinel,                  \
+                     reinterpret_cast<uint32_t*>(w.keys_out), w.pos_out, w.bag_of)
+#define PRE_LPB(VW)                        \
+  switch (lpb) {                           \
+    case 1: PRE(1, VW, 1); break;          \
+    case 2: PRE(2, VW, 1); break;          \
+    case 4: PRE(4, VW, 1); break;          \
+    case 8: PRE(8, VW, 1); break;          \
+    case 16: PRE(16, VW, 1); break;        \
+    case 32: PRE(32, VW, 1); break;        \
+    default:                               \
+      if (maxv == 1) PRE(64, VW, 1);       \
+      else if (maxv == 2) PRE(64, VW, 2);  \
+      else if (maxv <= 4) PRE(64, VW, 4);  \
+      else PRE(64, VW, 8);                 \
+  }
+  if (vec4) {
+    PRE_LPB(4)
+  } else {
+    PRE_LPB(1)
+  }
+#undef PRE_LPB
+#undef PRE
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+}  // namespace
+
+extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const int64_t* row_base,
+                                        int32_t T, int32_t B, const void* indices,
+                                        int32_t index_bits, const void* offsets,
+                                        int32_t offset_bits, const float* per_sample_weights,
+                                        float* out, int64_t out_batch_stride,
+                                        int64_t num_lookups, int64_t total_rows,
+                                        int64_t max_lookups_per_table, void* workspace,
+                                        size_t workspace_bytes, int32_t* error_flag,
+                                        dlrm_stream_t stream) {
+  const char* name = "dlrm_tbe_forward_presort";
+  if (!presort_applies((uint64_t)total_rows < 0xFFFFFFFFull ? 4 : 8, max_lookups_per_table,
+                       num_lookups) || num_lookups == 0 || T * (int64_t)B >= INT32_MAX)
+    return dlrm_tbe_forward(weights, D, row_base, T, B, indices, index_bits, offsets, offset_bits,
+                            per_sample_weights, out, out_batch_stride, error_flag, stream);
+  DLRM_ARG(weights && row_base && out && offsets && indices, "%s: null pointer", name);
+  DLRM_ARG(T > 0 && B > 0 && D > 0 && total_rows > 0, "%s: bad sizes", name);
+  DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: index_bits must be 32|64", name);
+  DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: offset_bits must be 32|64", name);
+  DLRM_ARG(out_batch_stride >= (int64_t)T * D, "%s: out_batch_stride < T*D", name);
+  DLRM_ARG(workspace, "%s: null workspace", name);
+  hipStream_t st = dlrm::as_stream(stream);
+#define PS(I, O)                                                                           \
+  return launch_fwd_presort<I, O>(weights, D, row_base, T, B, indices, offsets,            \
+                                  per_sample_weights, out, out_batch_stride, num_lookups,  \
+                                  total_rows, workspace, workspace_bytes, error_flag, st)
+  if (index_bits == 32 && offset_bits == 32) PS(int32_t, int32_t);
+  if (index_bits == 32) PS(int32_t, int64_t);
+  if (offset_bits == 32) PS(int64_t, int32_t);
+  PS(int64_t, int64_t);
+#undef PS
 }

@@ -45,5 +45,103 @@ __device__ __forceinline__ float vdot(const float4& a) {
 }
 __device__ __forceinline__ float vdot(const float& a) { return a * a; }
 
+// ------------------------------------------------------ forward gather --
+// Gather-reduce body over this workgroup's bags: `blk` / `nblk` = this workgroup's index and
+// the number of gather workgroups (a launch may also hold other roles, tbe_bwd.hip).
+template <int LPB, int VW, int MAXV, typename IdxT, typename OffT>
+__device__ __forceinline__ void tbe_fwd_body(
+    const float* __restrict__ W, int64_t D, const int64_t* __restrict__ row_base, int T, int B,
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const float* __restrict__ psw,
+    float* __restrict__ out, int64_t out_bs, int32_t* __restrict__ err, int64_t blk,
+    int64_t nblk) {
+  using V = typename VecT<VW>::T;
+  constexpr int GPW = kWave / LPB;  // bags per wave
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPB;
+  const int gl = lane - g * LPB;
+  const int nchunks = (int)(D / VW);
+  const int64_t nbags = (int64_t)T * B;
+  const int64_t wave_id = blk * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nwaves = nblk * (blockDim.x / kWave);
+
+  for (int64_t bag0 = wave_id * GPW; bag0 < nbags; bag0 += nwaves * GPW) {
+    const int64_t bag = bag0 + g;
+    const bool active = bag < nbags;
+    int t = 0, b = 0;
+    int64_t start = 0, end = 0, base = 0, nrows = 0;
+    if (active) {
+      t = (int)(bag / B);
+      b = (int)(bag - (int64_t)t * B);
+      start = (int64_t)off[bag];
+      end = (int64_t)off[bag + 1];
+      base = row_base[t];
+      nrows = row_base[t + 1] - base;
+    }
+    V acc[MAXV];
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) vzero(acc[c]);
+
+    for (int64_t l0 = start; l0 < end; l0 += LPB) {
+      const int n = (int)((end - l0) < LPB ? (end - l0) : LPB);
+      int64_t my_row = -1;
+      float my_w = 1.f;
+      if (gl < n) {
+        int64_t r = (int64_t)idx[l0 + gl];
+        if (r < 0 || r >= nrows) {
+          if (err) atomicOr(err, DLRM_TBE_ERR_INDEX);
+          r = -1;
+        }
+        my_row = r;
+        if (psw) my_w = psw[l0 + gl];
+      }
+      for (int j = 0; j < n; j += 4) {
+        int64_t r[4];
+        float w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = g * LPB + ((j + u) < LPB ? (j + u) : 0);
+          r[u] = __shfl(my_row, src, kWave);
+          w[u] = __shfl(my_w, src, kWave);
+          if (j + u >= n) r[u] = -1;
+        }
+        V v[4][MAXV];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int c = 0; c < MAXV; ++c) {
+            const int chunk = gl + c * LPB;
+            if (r[u] >= 0 && chunk < nchunks) {
+              v[u][c] = reinterpret_cast<const V*>(W + (base + r[u]) * D)[chunk];
+            } else {
+              vzero(v[u][c]);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (r[u] >= 0) {
+#pragma unroll
+            for (int c = 0; c < MAXV; ++c) {
+              if (psw)
+                vfma(acc[c], w[u], v[u][c]);
+              else
+                vadd(acc[c], v[u][c]);
+            }
+          }
+        }
+      }
+    }
+    if (active) {
+      V* o = reinterpret_cast<V*>(out + (int64_t)b * out_bs + (int64_t)t * D);
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c) {
+        const int chunk = gl + c * LPB;
+        if (chunk < nchunks) o[chunk] = acc[c];
+      }
+    }
+  }
+}
+
+
 
 }  // namespace

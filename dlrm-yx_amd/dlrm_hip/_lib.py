@@ -46,14 +46,17 @@ SIGNATURES = {
     "dlrm_tbe_backward_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
     "dlrm_tbe_backward_sgd": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32,
                                         c_int64, c_int64, P, P, c_int64, c_float, c_int64, P,
-                                        c_size_t, P, P]),
+                                        c_size_t, P, c_int32, P]),
     "dlrm_tbe_backward_rowwise_adagrad": (c_int32, [P, P, c_int64, P, c_int32, c_int32, P,
                                                     c_int32, P, c_int32, c_int64, c_int64, P, P,
                                                     c_int64, c_float, c_float, c_int64, P,
-                                                    c_size_t, P, P]),
+                                                    c_size_t, P, c_int32, P]),
     "dlrm_tbe_backward_dense": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P,
                                           c_int32, c_int64, c_int64, P, P, c_int64, c_int64, P,
-                                          c_size_t, P, P]),
+                                          c_size_t, P, c_int32, P]),
+    "dlrm_tbe_forward_presort": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P,
+                                           c_int32, P, P, c_int64, c_int64, c_int64, c_int64, P,
+                                           c_size_t, P, P]),
     "dlrm_tbe_expand_grad": (c_int32, [c_int64, c_int32, c_int32, P, c_int32, c_int64, P, P,
                                        c_int64, P, P]),
     "dlrm_qr_split_indices": (c_int32, [P, c_int32, c_int64, c_int64, P, P, P]),

@@ -103,6 +103,28 @@ def tbe_forward(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
     return out
 
 
+def tbe_forward_presort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
+                        indices: torch.Tensor, offsets: torch.Tensor, workspace: torch.Tensor,
+                        max_lookups_per_table: int, out: Optional[torch.Tensor] = None,
+                        out_batch_stride: Optional[int] = None,
+                        per_sample_weights: Optional[torch.Tensor] = None,
+                        error_flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """tbe_forward + this batch's backward sort in one launch (dlrm_tbe_forward_presort);
+    follow with tbe_backward(..., workspace, presorted=True)."""
+    _check_cuda(weights, row_base, indices, offsets, workspace, per_sample_weights)
+    D = weights.shape[1]
+    if out is None:
+        out = torch.empty((B, T, D), dtype=torch.float32, device=weights.device)
+        out_batch_stride = T * D
+    elif out_batch_stride is None:
+        out_batch_stride = T * D
+    _lib.call("dlrm_tbe_forward_presort", _p(weights), D, _p(row_base), T, B, _p(indices),
+              _bits(indices), _p(offsets), _bits(offsets), _p(per_sample_weights), _p(out),
+              out_batch_stride, indices.numel(), weights.shape[0], int(max_lookups_per_table),
+              _p(workspace), workspace.numel(), _p(error_flag), _stream(weights.device))
+    return out
+
+
 def tbe_backward_workspace_size(num_lookups: int, total_rows: int, D: int) -> int:
     return _lib.query("dlrm_tbe_backward_workspace_size", num_lookups, total_rows, D)
 
@@ -114,7 +136,7 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
                  grad_batch_stride: Optional[int] = None,
                  workspace: Optional[torch.Tensor] = None,
                  max_lookups_per_table: int = 0,
-                 error_flag: Optional[torch.Tensor] = None) -> None:
+                 error_flag: Optional[torch.Tensor] = None, presorted: bool = False) -> None:
     """mode: 'sgd' (fused exact SGD), 'rowwise_adagrad' (fused RWSAdagrad) or
     'dense' (weights is a gradient buffer to accumulate into).  max_lookups_per_table:
     upper bound on any table's lookups (0 = unknown); <= 4096 selects the per-table LDS
@@ -136,13 +158,14 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
     mx = int(max_lookups_per_table)
     if mode == "sgd":
         _lib.call("dlrm_tbe_backward_sgd", _p(weights), *args_common, lr, mx, _p(workspace),
-                  workspace.numel(), _p(error_flag), st)
+                  workspace.numel(), _p(error_flag), int(presorted), st)
     elif mode == "rowwise_adagrad":
         _lib.call("dlrm_tbe_backward_rowwise_adagrad", _p(weights), _p(momentum), *args_common,
-                  lr, eps, mx, _p(workspace), workspace.numel(), _p(error_flag), st)
+                  lr, eps, mx, _p(workspace), workspace.numel(), _p(error_flag), int(presorted),
+                  st)
     elif mode == "dense":
         _lib.call("dlrm_tbe_backward_dense", _p(weights), *args_common, mx, _p(workspace),
-                  workspace.numel(), _p(error_flag), st)
+                  workspace.numel(), _p(error_flag), int(presorted), st)
     else:
         raise ValueError(mode)
 

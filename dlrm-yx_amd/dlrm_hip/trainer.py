@@ -169,6 +169,9 @@ class DLRMTrainer:
         self.overlaps = set(os.environ.get("DLRM_OVERLAPS", "").split(","))
         self._side = torch.cuda.Stream(device=self.dev)
         self._tbe_ws: Optional[torch.Tensor] = None
+        # run the embedding backward's per-table sort inside the lookup launch
+        # (dlrm_tbe_forward_presort); DLRM_TBE_PRESORT=0 sorts in the backward instead
+        self.tbe_presort = os.environ.get("DLRM_TBE_PRESORT", "1") != "0"
         # device TBE error bits (ops.TBE_ERR_*): out-of-range indices are skipped by the
         # kernels and flagged here; check_errors() reads it (the step never syncs)
         self.tbe_error_flag = torch.zeros(1, dtype=torch.int32, device=self.dev)
@@ -406,6 +409,7 @@ class DLRMTrainer:
         c_fwd = conc and "fwd" in self.overlaps and not dist
         c_bot = conc and "bot" in self.overlaps and not dist
         st = {}  # state shared by the segments (collective handles, pending reductions)
+        presort = self.tbe_presort
 
         def streams():
             s0 = torch.cuda.current_stream(self.dev)
@@ -416,7 +420,14 @@ class DLRMTrainer:
 
         def lookup():  # embeddings (full batch, local tables)
             with prof("tbe_fwd"):
-                if self.T_local > 0:
+                if self.T_local > 0 and presort:
+                    # the backward's per-table sort runs inside the lookup launch
+                    ops.tbe_forward_presort(self.weights, self.row_base, self.T_local, B,
+                                            batch.indices, batch.offsets,
+                                            self._ws_tbe(batch.indices.numel()),
+                                            batch.max_per_table, out=bufs["E"],
+                                            error_flag=self.tbe_error_flag)
+                elif self.T_local > 0:
                     ops.tbe_forward(self.weights, self.row_base, self.T_local, B, batch.indices,
                                     batch.offsets, out=bufs["E"],
                                     error_flag=self.tbe_error_flag)
@@ -505,7 +516,7 @@ class DLRMTrainer:
                                      eps=cfg.adagrad_eps, momentum=self.momentum,
                                      workspace=self._ws_tbe(batch.indices.numel()),
                                      max_lookups_per_table=batch.max_per_table,
-                                     error_flag=self.tbe_error_flag)
+                                     error_flag=self.tbe_error_flag, presorted=presort)
 
         def backward_single():  # one GPU: bottom backward || embedding backward
             s0, s1 = streams()

@@ -113,6 +113,22 @@ int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base, i
                      int32_t offset_bits, const float* per_sample_weights, float* out,
                      int64_t out_batch_stride, int32_t* error_flag, dlrm_stream_t stream);
 
+/*
+ * dlrm_tbe_forward + the per-table sort of the backward (which depends only on the
+ * indices) in ONE launch: the sort's latency-bound workgroups run beside the gather.
+ * The sort lands in `workspace` (a dlrm_tbe_backward_* workspace); call the backward of
+ * the same batch with presorted = 1.  When the per-table sort does not apply (64-bit row
+ * ids, max_lookups_per_table 0 or > 4096) this is dlrm_tbe_forward and the backward
+ * sorts as usual.
+ */
+int dlrm_tbe_forward_presort(const float* weights, int64_t D, const int64_t* row_base, int32_t T,
+                             int32_t B, const void* indices, int32_t index_bits,
+                             const void* offsets, int32_t offset_bits,
+                             const float* per_sample_weights, float* out,
+                             int64_t out_batch_stride, int64_t num_lookups, int64_t total_rows,
+                             int64_t max_lookups_per_table, void* workspace,
+                             size_t workspace_bytes, int32_t* error_flag, dlrm_stream_t stream);
+
 /* Workspace for the deterministic (sorted, segment-reduced) backward. */
 size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows, int64_t D);
 
@@ -130,6 +146,9 @@ size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows,
  * offending table is skipped and DLRM_TBE_ERR_TABLE_CAP is set in *error_flag.
  * Out-of-range indices are skipped and set DLRM_TBE_ERR_INDEX (the reference's
  * EmbeddingBag raises IndexError there).  error_flag may be NULL.
+ * presorted != 0: the per-table sort of THIS batch (same indices, offsets, workspace)
+ * already ran inside dlrm_tbe_forward_presort and is skipped here (ignored when the
+ * per-table sort does not apply: 32-bit row ids, bound <= 4096).
  * (The same applies to the two functions below.)
  */
 int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, int32_t T,
@@ -138,7 +157,8 @@ int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, in
                           int64_t total_rows, const float* per_sample_weights,
                           const float* grad_out, int64_t grad_batch_stride, float lr,
                           int64_t max_lookups_per_table, void* workspace,
-                          size_t workspace_bytes, int32_t* error_flag, dlrm_stream_t stream);
+                          size_t workspace_bytes, int32_t* error_flag, int32_t presorted,
+                          dlrm_stream_t stream);
 
 /*
  * Row-wise sparse Adagrad (RWSAdagrad, optim/rwsadagrad.py:92-115) fused into the
@@ -155,7 +175,7 @@ int dlrm_tbe_backward_rowwise_adagrad(float* weights, float* momentum, int64_t D
                                       int64_t grad_batch_stride, float lr, float eps,
                                       int64_t max_lookups_per_table, void* workspace,
                                       size_t workspace_bytes, int32_t* error_flag,
-                                      dlrm_stream_t stream);
+                                      int32_t presorted, dlrm_stream_t stream);
 
 /*
  * Dense (non-fused) embedding-bag gradient scatter: grad_weights[row] += w_l * g
@@ -168,7 +188,8 @@ int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_b
                             int64_t total_rows, const float* per_sample_weights,
                             const float* grad_out, int64_t grad_batch_stride,
                             int64_t max_lookups_per_table, void* workspace,
-                            size_t workspace_bytes, int32_t* error_flag, dlrm_stream_t stream);
+                            size_t workspace_bytes, int32_t* error_flag, int32_t presorted,
+                            dlrm_stream_t stream);
 
 /*
  * Sparse-gradient values of an EmbeddingBag(sparse=True) backward

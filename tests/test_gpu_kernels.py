@@ -155,6 +155,54 @@ def test_tbe_backward_per_table_sort_vs_global_sort(ops, mode, invalid):
         assert ok, msg
 
 
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad", "dense"])
+@pytest.mark.parametrize("invalid", [False, True])
+@pytest.mark.parametrize("idx_dtype", [torch.int32, torch.int64])
+@pytest.mark.parametrize("mx_kind", ["cap", "none"])
+def test_tbe_forward_presort_matches_separate_sort(ops, mode, invalid, idx_dtype, mx_kind):
+    """dlrm_tbe_forward_presort (gather + the backward's per-table sort in one launch)
+    followed by the backward with presorted=1 is bitwise identical to tbe_forward + the
+    self-sorting backward; with no per-table bound (mx 0) presort degrades to the plain
+    forward and the backward sorts itself."""
+    torch.manual_seed(11)
+    rows, D, B, L = [3, 5000, 4, 700, 1, 90000], 64, 512, 3
+    T = len(rows)
+    lo = [torch.arange(B) * L for _ in rows]
+    li = [torch.randint(0, n, (B * L,)) for n in rows]
+    if invalid:
+        li[1][5] = 999999
+    off, idx = O.batched_csr(lo, li)
+    idx, off = idx.to(idx_dtype).to(dev), off.to(dev)
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    G = torch.randn(B, T, D, device=dev)
+    W0 = torch.randn(sum(rows), D, device=dev)
+    mom0 = torch.rand(sum(rows), device=dev)
+    psw = torch.rand(idx.numel(), device=dev) if mode == "dense" else None
+    mx = B * L if mx_kind == "cap" else 0
+    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), sum(rows), D),
+                     dtype=torch.uint8, device=dev)
+    res = []
+    for pre in (False, True):
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ws.zero_()
+        if pre:
+            out = ops.tbe_forward_presort(W0, row_base, T, B, idx, off, ws, mx,
+                                          per_sample_weights=psw, error_flag=flag)
+        else:
+            out = ops.tbe_forward(W0, row_base, T, B, idx, off, per_sample_weights=psw,
+                                  error_flag=flag)
+        W = W0.clone() if mode != "dense" else torch.zeros_like(W0)
+        mom = mom0.clone()
+        ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8, momentum=mom,
+                         per_sample_weights=psw, workspace=ws, max_lookups_per_table=mx,
+                         error_flag=flag, presorted=pre)
+        res.append((out.cpu(), W.cpu(), mom.cpu(), flag.item()))
+    (o0, w0, m0, f0), (o1, w1, m1, f1) = res
+    assert torch.equal(o0, o1)
+    assert torch.equal(w0, w1) and torch.equal(m0, m1)
+    assert f0 == f1 == (ops.TBE_ERR_INDEX if invalid else 0)
+
+
 def test_tbe_out_of_range_flag(ops):
     W = torch.randn(10, 8, device=dev)
     row_base = torch.tensor([0, 10], dtype=torch.int64, device=dev)

@@ -1,4 +1,5 @@
-"""Time the TBE backward (fused SGD) at C3-like sizes: per-table sort vs device radix sort."""
+"""Time the TBE backward (fused SGD) at C3-like sizes: device radix sort vs per-table sort vs
+sorted inside the forward (presort); and the forward with / without the presort."""
 import os
 import sys
 
@@ -24,7 +25,15 @@ for rows in (TB, TB[:1], [3]):
                      device=dev)
     res = []
     for mx in (0, B):
-        t = timeit(lambda: ops.tbe_backward("sgd", W, rb, T, B, idx, off, G, lr=1e-6, workspace=ws,
-                                            max_lookups_per_table=mx))
+        t = timeit(lambda: ops.tbe_backward("sgd", W, rb, T, B, idx, off, G, lr=1e-6,
+                                            workspace=ws, max_lookups_per_table=mx))
         res.append(f"hint={mx}: {t * 1e6:.1f} us")
+    ops.tbe_forward_presort(W, rb, T, B, idx, off, ws, B)
+    t = timeit(lambda: ops.tbe_backward("sgd", W, rb, T, B, idx, off, G, lr=1e-6, workspace=ws,
+                                        max_lookups_per_table=B, presorted=True))
+    res.append(f"presorted: {t * 1e6:.1f} us")
+    t = timeit(lambda: ops.tbe_forward(W, rb, T, B, idx, off))
+    res.append(f"fwd: {t * 1e6:.1f} us")
+    t = timeit(lambda: ops.tbe_forward_presort(W, rb, T, B, idx, off, ws, B))
+    res.append(f"fwd+presort: {t * 1e6:.1f} us")
     print(f"T={T}", "  ".join(res), flush=True)
