@@ -405,14 +405,17 @@ __device__ __forceinline__ bool splitk_reduce(const GemmParams& p, int tile, int
   return true;
 }
 
-// One output tile (and K split) of problem p: the software-pipelined 16x16x4 body.
-template <int BM, int BN, bool A_KC, bool B_KC, bool RS>
+// One output tile (and K split) of problem p: the software-pipelined 16x16x4 body.  The
+// workgroup is WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile.
+template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS>
 __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* smem) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1, "wave sub-tile");
   constexpr int KL = kBK / 4;  // k-steps per K-tile (each lane group owns KL consecutive k)
-  using SA = Stage<BM, kBK, A_KC, true, kThreads>;
-  using SB = Stage<BN, kBK, B_KC, true, kThreads>;
+  using SA = Stage<BM, kBK, A_KC, true, NT>;
+  using SB = Stage<BN, kBK, B_KC, true, NT>;
   constexpr int NS = SA::NV + SB::NV;  // staged float4 per thread per K-tile
   static_assert(NS <= KL - 1, "staging must finish before the barrier step");
 
@@ -430,8 +433,8 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   const int lane = tid & 63;
   const int kq = lane >> 4;
   const int l16 = lane & 15;
-  const int wm0 = (wave >> 1) * WM;
-  const int wn0 = (wave & 1) * WN;
+  const int wm0 = (wave / WGN) * WM;
+  const int wn0 = (wave % WGN) * WN;
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -543,7 +546,7 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
     rs[i] += __shfl_xor(rs[i], 16, 64);
     rs[i] += __shfl_xor(rs[i], 32, 64);
   }
-  const bool rs_owner = RS && tn == 0 && (wave & 1) == 0 && kq == 0;
+  const bool rs_owner = RS && tn == 0 && (wave % WGN) == 0 && kq == 0;
 
   // Register r of a 16x16 accumulator holds row 4*(lane>>4) + r, col lane&15.
   constexpr int NV = FM * FN * 4;
@@ -606,7 +609,7 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
 // thread for ones_col.  Up to 8 splits' loads in flight.
 __device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
   const int64_t MN = p.M * p.N;
-  const int64_t i = (int64_t)lb * kThreads + threadIdx.x;
+  const int64_t i = (int64_t)lb * blockDim.x + threadIdx.x;
   const int64_t n4 = MN / 4;  // N % 4 == 0 (host check)
   const int S = p.splits;
   if (i < n4) {
@@ -654,8 +657,9 @@ __host__ __device__ constexpr int kind_bit(int layout, bool rs) { return 1 << (r
 // Up to kMaxGroup independent problems; block -> (problem, tile, split) after the XCD remap.
 // KINDS is the set of body kinds compiled in (a launch uses the smallest instantiation that
 // covers its problems: fewer bodies, fewer registers).
-template <int BM, int BN, int KINDS>
-__global__ __launch_bounds__(kThreads, 2) void gemm_group_kernel(const GemmGroup g) {
+template <int BM, int BN, int WGM, int WGN, int KINDS>
+__global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
+    const GemmGroup g) {
   __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
   // Problems own consecutive PHYSICAL block ranges, so each one is dealt round-robin over
   // all eight XCDs (a remap across the whole launch would give each problem a few XCDs);
@@ -671,15 +675,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_group_kernel(const GemmGroup
   if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
   const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
   if constexpr ((KINDS & 1) != 0)
-    if (kind == 0) return pipe_body<BM, BN, true, true, false>(p, lb, smem);
+    if (kind == 0) return pipe_body<BM, BN, WGM, WGN, true, true, false>(p, lb, smem);
   if constexpr ((KINDS & 2) != 0)
-    if (kind == 1) return pipe_body<BM, BN, true, false, false>(p, lb, smem);
+    if (kind == 1) return pipe_body<BM, BN, WGM, WGN, true, false, false>(p, lb, smem);
   if constexpr ((KINDS & 4) != 0)
-    if (kind == 2) return pipe_body<BM, BN, false, false, false>(p, lb, smem);
+    if (kind == 2) return pipe_body<BM, BN, WGM, WGN, false, false, false>(p, lb, smem);
   if constexpr ((KINDS & 8) != 0)
-    if (kind == 3) return pipe_body<BM, BN, false, true, false>(p, lb, smem);
+    if (kind == 3) return pipe_body<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
   if constexpr ((KINDS & 16) != 0)
-    if (kind == 4) return pipe_body<BM, BN, false, false, true>(p, lb, smem);
+    if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
 }
 
 // Fallback for operands the pipelined body cannot take (unaligned rows, ragged float4
@@ -827,6 +831,7 @@ int layout_of(const Desc& d) {
 struct PlanEntry {
   int64_t M, N, K;
   int layout, bm, bn, split;
+  int wm = 2, wn = 2;
 };
 
 // Measured plans for the DLRM step shapes of single-problem launches (exact match), from
@@ -836,45 +841,54 @@ constexpr PlanEntry kPlans[] = {
     {0, 0, 0, 0, 64, 64, 1},  // sentinel (never matches: M = 0)
 };
 
-// Compiled tiles: 64x64, 128x64, 64x128, 32x64, 64x32.
-bool tile_ok(int bm, int bn) {
-  return (bm == 64 && bn == 64) || (bm == 128 && bn == 64) || (bm == 64 && bn == 128) ||
-         (bm == 32 && bn == 64) || (bm == 64 && bn == 32);
+// Compiled tiles (BM x BN on 2x2 waves): 64x64, 128x64, 64x128, 32x64, 64x32.  (Other
+// wave layouts of pipe_body - 64x32 on 2x1, 32x64 on 1x2, 128x32 on 4x1 - measured slower
+// on every DLRM shape: tools/gemm_cfg_ab.py, profiles/r02_gemm_cfg_ab.txt.)
+bool tile_ok(int bm, int bn, int wm, int wn) {
+  return wm == 2 && wn == 2 &&
+         ((bm == 64 && bn == 64) || (bm == 128 && bn == 64) || (bm == 64 && bn == 128) ||
+          (bm == 32 && bn == 64) || (bm == 64 && bn == 32));
 }
+
+struct Tile {
+  int bm = 64, bn = 32, wm = 2, wn = 2;
+  bool operator==(const Tile& o) const {
+    return bm == o.bm && bn == o.bn && wm == o.wm && wn == o.wn;
+  }
+};
 
 // Plan of ONE problem, independent of what it is grouped with (so a problem's result is
 // bitwise the same in any group: the split decides the summation order, the tile shape
-// does not).  Tuning overrides (read per call, for sweeps): DLRM_GEMM_CFG=<BM>x<BN>,
-// DLRM_GEMM_SPLIT=<n>.
-void plan_one(const Desc& d, int& bm, int& bn, Plan& pl) {
-  bm = bn = 64;
+// does not).  Tuning overrides (read per call, for sweeps): DLRM_GEMM_CFG=<BM>x<BN> or
+// <BM>x<BN>x<WGM>x<WGN>, DLRM_GEMM_SPLIT=<n>.
+void plan_one(const Desc& d, Tile& t, Plan& pl) {
+  t = Tile{64, 64, 2, 2};
   if (d.mode == DLRM_GEMM_REDUCE) {  // elementwise job: no tiles, no K
     pl.splits = d.splits;
     pl.kchunk = 0;
     return;
   }
   if (d.mode == DLRM_GEMM_PARTIAL && d.splits > 0) {  // caller-sized partial buffer
-    int a, b;
     Desc q = d;
     q.mode = DLRM_GEMM_FULL;
-    plan_one(q, a, b, pl);
-    bm = a, bn = b;
+    plan_one(q, t, pl);
     pl = make_plan(d.splits, d.K);
     return;
   }
   const char* cfg = getenv("DLRM_GEMM_CFG");
   const int force_split = env_int("DLRM_GEMM_SPLIT", 0);
   if (cfg && *cfg) {
-    int a = 64, b = 64;
-    if (sscanf(cfg, "%dx%d", &a, &b) == 2 && tile_ok(a, b))
-      bm = a, bn = b;
+    int a = 64, b = 64, wm = 2, wn = 2;
+    const int got = sscanf(cfg, "%dx%dx%dx%d", &a, &b, &wm, &wn);
+    if (got == 2) wm = wn = 2;
+    if (got >= 2 && tile_ok(a, b, wm, wn)) t = Tile{a, b, wm, wn};
     pl = make_plan(force_split > 0 ? force_split : 1, d.K);
     return;
   }
   if (!getenv("DLRM_GEMM_NOTABLE"))
     for (const PlanEntry& e : kPlans)
       if (e.M == d.M && e.N == d.N && e.K == d.K && e.layout == layout_of(d)) {
-        bm = e.bm, bn = e.bn;
+        t = Tile{e.bm, e.bn, e.wm, e.wn};
         pl = make_plan(e.split, d.K);
         return;
       }
@@ -882,7 +896,7 @@ void plan_one(const Desc& d, int& bm, int& bn, Plan& pl) {
   // FULL problems run unsplit unless they have fewer than one tile per CU (an in-launch
   // split costs a hand-off); PARTIAL ones split K until >= 2 blocks per CU, every K chunk
   // >= 256 (8 K-tiles).
-  bm = 64, bn = 32;
+  t = Tile{64, 32, 2, 2};
   const int64_t tiles = dlrm::ceil_div(d.M, 64) * dlrm::ceil_div(d.N, 32);
   const int target = env_int("DLRM_GEMM_TARGET", d.mode == DLRM_GEMM_PARTIAL ? 512 : 256);
   int64_t s = 1;
@@ -892,24 +906,25 @@ void plan_one(const Desc& d, int& bm, int& bn, Plan& pl) {
 
 // Tile config of a launch: the GEMM problems' common choice, else 64x32 (REDUCE jobs have
 // no tiles and do not vote).
-void plan_launch(int n, const Desc* d, int& bm, int& bn, Plan* pl) {
+void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   bool first = true;
-  bm = bn = 64;
+  t = Tile{64, 64, 2, 2};
   for (int i = 0; i < n; ++i) {
-    int a, b;
-    plan_one(d[i], a, b, pl[i]);
+    Tile a;
+    plan_one(d[i], a, pl[i]);
     if (d[i].mode == DLRM_GEMM_REDUCE) continue;
     if (first) {
-      bm = a, bn = b;
+      t = a;
       first = false;
-    } else if (a != bm || b != bn) {
-      bm = 64, bn = 32;
+    } else if (!(a == t)) {
+      t = Tile{64, 32, 2, 2};
     }
   }
 }
 
 // Split-K workspace: the fixed 64 KiB ticket head, then each problem's records.
-size_t group_ws_bytes(int n, const Desc* d, int bm, int bn, const Plan* pl) {
+size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
+  const int bm = t.bm, bn = t.bn;
   WsCarver c(nullptr);
   c.take<int>(kTicketCap);
   bool any = false;
@@ -922,8 +937,9 @@ size_t group_ws_bytes(int n, const Desc* d, int bm, int bn, const Plan* pl) {
   return any ? c.used + 256 : 0;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WGM = 2, int WGN = 2>
 int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes, hipStream_t st) {
+  constexpr int NT = WGM * WGN * 64;
   GemmGroup g{};
   g.n = n;
   const int pub = env_int("DLRM_GEMM_PUB", 1);
@@ -946,7 +962,7 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
     p.kchunk = pl[i].kchunk > 0 ? pl[i].kchunk : kBK;
     p.block0 = (int)blocks;
     if (p.mode == DLRM_GEMM_REDUCE) {
-      blocks += dlrm::ceil_div(p.M * p.N / 4 + (p.ones_col >= 0 ? p.M : 0), kThreads);
+      blocks += dlrm::ceil_div(p.M * p.N / 4 + (p.ones_col >= 0 ? p.M : 0), NT);
       continue;
     }
     if (p.splits > 1 && p.mode == DLRM_GEMM_FULL) {
@@ -966,18 +982,18 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   for (int i = 0; i < n; ++i)
     if (g.p[i].mode != DLRM_GEMM_REDUCE)
       kinds |= kind_bit(g.p[i].layout, g.p[i].layout == 2 && g.p[i].ones_col >= 0);
-  const dim3 grid(g.total), block(kThreads);
+  const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
   // row sums, two wgrads), else all kinds
   switch (kinds) {
 #define K_(M_)                                                                          \
   case M_:                                                                             \
-    hipLaunchKernelGGL((gemm_group_kernel<BM, BN, M_>), grid, block, 0, st, g);         \
+    hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g); \
     break;
     K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
 #undef K_
     default:
-      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, 31>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
   }
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32");
   return DLRM_OK;
@@ -1050,10 +1066,10 @@ size_t ws_for(int n, const Desc* d) {
   for (int i = 0; i < n; ++i)
     if (d[i].M > 0 && d[i].N > 0 && d[i].K > 0 && pipe_ok(d[i])) q[m++] = d[i];
   if (m == 0) return 0;
-  int bm, bn;
+  Tile t;
   Plan pl[kMaxGroup];
-  plan_launch(m, q, bm, bn, pl);
-  return group_ws_bytes(m, q, bm, bn, pl);
+  plan_launch(m, q, t, pl);
+  return group_ws_bytes(m, q, t, pl);
 }
 
 int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -1076,17 +1092,17 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
     q[m++] = d[i];
   }
   if (m == 0) return DLRM_OK;
-  int bm, bn;
+  Tile t;
   Plan pl[kMaxGroup];
-  plan_launch(m, q, bm, bn, pl);
-  const size_t need = group_ws_bytes(m, q, bm, bn, pl);
+  plan_launch(m, q, t, pl);
+  const size_t need = group_ws_bytes(m, q, t, pl);
   if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: every problem unsplit
     for (int i = 0; i < m; ++i) pl[i] = make_plan(1, q[i].K);
   }
-  if (bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, st);
-  if (bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, st);
-  if (bm == 32) return launch_group<32, 64>(m, q, pl, ws, ws_bytes, st);
-  if (bn == 32) return launch_group<64, 32>(m, q, pl, ws, ws_bytes, st);
+  if (t.bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, st);
+  if (t.bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, st);
+  if (t.bm == 32) return launch_group<32, 64>(m, q, pl, ws, ws_bytes, st);
+  if (t.bn == 32) return launch_group<64, 32>(m, q, pl, ws, ws_bytes, st);
   return launch_group<64, 64>(m, q, pl, ws, ws_bytes, st);
 }
 
@@ -1148,9 +1164,9 @@ extern "C" int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem) {
   if (d.mode == DLRM_GEMM_REDUCE) d.mode = DLRM_GEMM_FULL;
   d.splits = 0;
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) return 1;
-  int bm, bn;
+  Tile t;
   Plan pl;
-  plan_one(d, bm, bn, pl);
+  plan_one(d, t, pl);
   return pl.splits;
 }
 

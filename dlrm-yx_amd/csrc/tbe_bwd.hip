@@ -96,6 +96,8 @@ struct SegSortLds {
 // this lane) plus the wave's running count of that digit in LDS; one scan over the
 // (digit, wave) counts gives every element its destination.  Order inside a digit is
 // (wave, item, lane) = element order: stable.
+// PRB (timing probes, tools/tbe_bwd_bench.py): 1 = ranking only, 2 = ranking + scan
+template <int PRB = 0>
 __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
                                                int32_t (&pos)[kSegItems], int bits,
                                                SegSortLds& sm) {
@@ -130,6 +132,11 @@ __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
       if (r == c - 1) sm.cnt[d * CS + w] = base + c;  // last peer publishes
     }
     __syncthreads();
+    if constexpr (PRB == 1) {
+#pragma unroll
+      for (int u = 0; u < kSegItems; ++u) key[u] ^= rank[u] & 1 ? 0u : 0u;
+      continue;
+    }
     // exclusive scan of cnt in (digit, wave) order
     uint32_t v[CPT];
     uint32_t tsum = 0;
@@ -149,13 +156,16 @@ __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
     if (l == 63) sm.wsum[w] = inc;
     __syncthreads();
     uint32_t run = inc - tsum;
-    for (int k = 0; k < w; ++k) run += sm.wsum[k];
+    // waves before this one: all wave totals read at once (independent LDS reads)
+#pragma unroll
+    for (int k = 0; k < kSegWaves; ++k) run += k < w ? sm.wsum[k] : 0u;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       sm.cnt[jd * CS + jw + k] = run;
       run += v[k];
     }
     __syncthreads();
+    if constexpr (PRB == 2) continue;
 #pragma unroll
     for (int u = 0; u < kSegItems; ++u) {
       const uint32_t dst = sm.cnt[dig[u] * CS + w] + rank[u];
@@ -173,7 +183,7 @@ __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
   }
 }
 
-template <typename IdxT, typename OffT>
+template <typename IdxT, typename OffT, int PRB = 0>
 __device__ __forceinline__ void segsort_body(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
@@ -251,7 +261,7 @@ __device__ __forceinline__ void segsort_body(
     }
   }
   __syncthreads();  // bags complete
-  seg_radix_sort(key, pos, bits, sm);
+  seg_radix_sort<PRB>(key, pos, bits, sm);
 #pragma unroll
   for (int u = 0; u < kSegItems; ++u) {
     const int i = w * (kSegItems * 64) + u * 64 + l;
@@ -263,14 +273,14 @@ __device__ __forceinline__ void segsort_body(
   }
 }
 
-template <typename IdxT, typename OffT>
+template <typename IdxT, typename OffT, int PRB = 0>
 __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
     int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
   __shared__ SegSortLds sm;
-  segsort_body<IdxT, OffT>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of, err,
-                           blockIdx.x, sm);
+  segsort_body<IdxT, OffT, PRB>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of,
+                                err, blockIdx.x, sm);
 }
 
 // The forward gather and the backward's per-table sort in ONE launch: the sort depends only
@@ -660,6 +670,12 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
   }
 }
 
+// DLRM_SEGSORT_PROBE (timing probes of the per-table sort; tools/tbe_bwd_bench.py only)
+inline int env_probe() {
+  const char* e = getenv("DLRM_SEGSORT_PROBE");
+  return e ? atoi(e) : 0;
+}
+
 // The per-table LDS sort applies (and dlrm_tbe_forward_presort can run it early).
 inline bool presort_applies(size_t key_bytes, int64_t max_seg, int64_t N) {
   return key_bytes == 4 && max_seg > 0 && max_seg <= kSegCap && N < (int64_t)0x7fffffff;
@@ -722,10 +738,16 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   if (per_table && presorted) {
     // this batch's per-table sort already ran inside dlrm_tbe_forward_presort
   } else if (per_table) {
-    hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(kSegThreads), 0,
-                       st, static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base,
-                       T, B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),
-                       w.pos_out, w.bag_of, err);
+    const int prb = env_probe();
+#define SEG(P)                                                                                  \
+  hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT, P>), dim3(T + 1), dim3(kSegThreads), 0, \
+                     st, static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base,   \
+                     T, B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),         \
+                     w.pos_out, w.bag_of, err)
+    if (prb == 1) SEG(1);
+    else if (prb == 2) SEG(2);
+    else SEG(0);
+#undef SEG
     DLRM_LAUNCH_CHECK(name);
   } else {
     hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(dlrm::ceil_div(N, 256)),

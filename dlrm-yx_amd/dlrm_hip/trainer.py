@@ -172,6 +172,9 @@ class DLRMTrainer:
         # run the embedding backward's per-table sort inside the lookup launch
         # (dlrm_tbe_forward_presort); DLRM_TBE_PRESORT=0 sorts in the backward instead
         self.tbe_presort = os.environ.get("DLRM_TBE_PRESORT", "1") != "0"
+        # MLP backward: a layer's split wgrad (partials only) in the same launch as its dgrad
+        self.group_wgrad = os.environ.get("DLRM_GROUP_WGRAD", "1") != "0"
+        self.full_last_wgrad = os.environ.get("DLRM_FULL_LAST_WGRAD", "0") == "1"
         # device TBE error bits (ops.TBE_ERR_*): out-of-range indices are skipped by the
         # kernels and flagged here; check_errors() reads it (the step never syncs)
         self.tbe_error_flag = torch.zeros(1, dtype=torch.int32, device=self.dev)
@@ -477,9 +480,15 @@ class DLRMTrainer:
                 L = self.top[li]
                 inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
                 gn = (gi + 1) % 3
-                self._gemm([self._dgrad(L, g, inp if li > 0 else None, G[gn])] + rq)
+                dg = self._dgrad(L, g, inp if li > 0 else None, G[gn])
                 w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li))
-                self._gemm([w])
+                if r is not None and self.group_wgrad:
+                    # the split wgrad only writes partials (its update rides on the next
+                    # launch's reduce job), so it may run beside the dgrad reading W
+                    self._gemm([dg, w] + rq)
+                else:
+                    self._gemm([dg] + rq)
+                    self._gemm([w])
                 rq = [r] if r is not None else []
                 g, gi = G[gn], gn
             _, gfeats = self._features(bufs, Bl, grad=True)
@@ -496,11 +505,14 @@ class DLRMTrainer:
             for li in range(self.n_bot - 1, -1, -1):
                 L = self.bot[li]
                 inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
-                if li > 0:
-                    self._gemm([self._dgrad(L, g, inp, bg[li % 2])] + rq, side=c_bot)
-                    rq = []
-                w, r = self._wg(L, g, inp, fused_opt, lr, ("bot", li))
-                self._gemm([w] + rq, side=c_bot)
+                w, r = self._wg(L, g, inp, fused_opt, lr, ("bot", li), last=li == 0)
+                if li > 0 and r is not None and self.group_wgrad:
+                    self._gemm([self._dgrad(L, g, inp, bg[li % 2]), w] + rq, side=c_bot)
+                else:
+                    if li > 0:
+                        self._gemm([self._dgrad(L, g, inp, bg[li % 2])] + rq, side=c_bot)
+                        rq = []
+                    self._gemm([w] + rq, side=c_bot)
                 rq = [r] if r is not None else []
                 if li > 0:
                     g = bg[li % 2]
@@ -636,9 +648,13 @@ class DLRMTrainer:
                                     **kw, **part)[0]
         return ops.gemm_problem(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=C, **kw, **part)[0]
 
-    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key):
+    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key, last=False):
         """The wgrad of L as (problem, reduce job or None): split-K wgrads write partials
-        into a per-layer buffer and their reduction (+ SGD) runs in the NEXT launch."""
+        into a per-layer buffer and their reduction (+ SGD) runs in the NEXT launch.  The
+        last GEMM of the step (last=True) has no next launch to carry a reduce job: its
+        K split, if any, is reduced inside its own launch (FULL mode)."""
+        if last and self.full_last_wgrad:
+            return self._wgrad(L, g, inp, fused_opt, lr), None
         bufs = self._cur
         sp = bufs.setdefault("splits", {})
         if key not in sp:

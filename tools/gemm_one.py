@@ -1,5 +1,11 @@
-"""Run one GEMM shape/config N times (for rocprofv3 counter passes).
-    DLRM_GEMM_CFG=64x64x32 python tools/gemm_one.py M,N,K,ta,tb [reps]"""
+"""Run one trainer-shaped GEMM back to back (for rocprofv3 PMC / kernel-trace passes).
+
+    python tools/gemm_one.py --kind fwd --B 2048 --K 1024 --N 1024 [--iters 200] [--cfg 64x32]
+
+kind: fwd (X[B,Kp] . W[N,Kp]^T -> Y, ReLU), dgrad (G[B,N] . W[N,K] -> dX, ReLU'),
+wgrad (G^T[N,B] . X[B,K] -> W, fused SGD, PARTIAL + REDUCE as in the trainer).
+"""
+import argparse
 import os
 import sys
 
@@ -8,20 +14,65 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dlrm-yx_amd"))
 from dlrm_hip import ops  # noqa: E402
 
-M, N, K, ta, tb = (int(v) for v in sys.argv[1].split(","))
-reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-dev = "cuda"
-A = torch.randn((K, M) if ta else (M, K), device=dev)
-B = torch.randn((N, K) if tb else (K, N), device=dev)
-C = torch.empty(M, N, device=dev)
-ws = torch.zeros(256 << 20, dtype=torch.uint8, device=dev)  # split-K tickets start at 0
-blas = os.environ.get("GEMM_ONE_BLAS") == "1"
-At = A.t() if ta else A
-Bt = B.t() if tb else B
-for _ in range(reps):
-    if blas:
-        torch.matmul(At, Bt, out=C)
+
+def pad4(n):
+    return (n + 3) // 4 * 4
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kind", default="fwd")
+    ap.add_argument("--B", type=int, default=2048)
+    ap.add_argument("--K", type=int, default=1024)
+    ap.add_argument("--N", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--cfg", default="")
+    ap.add_argument("--split", default="")
+    args = ap.parse_args()
+    if args.cfg:
+        os.environ["DLRM_GEMM_CFG"] = args.cfg
+    if args.split:
+        os.environ["DLRM_GEMM_SPLIT"] = args.split
+    dev = "cuda"
+    B, K, N = args.B, args.K, args.N
+    Kp = pad4(K + 1)
+    torch.manual_seed(0)
+    X = torch.randn(B, Kp, device=dev)
+    W = torch.randn(N, Kp, device=dev) * 0.01
+    Y = torch.empty(B, pad4(N + 1), device=dev)
+    G = torch.randn(B, N, device=dev)
+    dX = torch.empty(B, Kp, device=dev)
+    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
+    if args.kind == "fwd":
+        probs = [[ops.gemm_problem(X, W, trans_b=True, C=Y, epilogue=ops.EPI_RELU)[0]]]
+    elif args.kind == "dgrad":
+        nd = K if K % 4 == 0 else Kp
+        probs = [[ops.gemm_problem(G, W[:, :nd], C=dX[:, :nd], epilogue=ops.EPI_DRELU, aux=X)[0]]]
     else:
-        ops.gemm(A, B, trans_a=bool(ta), trans_b=bool(tb), C=C, workspace=ws)
-torch.cuda.synchronize()
-print("done")
+        part = torch.empty(ops.gemm_partial_bytes(N, Kp, 32) // 4 + 64, device=dev)
+        pr = ops.gemm_problem(G, X[:, :K], trans_a=True, C=W, alpha=1e-9, epilogue=ops.EPI_SGD,
+                              ones_col=K, partial=part, splits=0)[0]
+        s = ops.gemm_splits(pr, partial=True)
+        pr = ops.gemm_problem(G, X[:, :K], trans_a=True, C=W, alpha=1e-9, epilogue=ops.EPI_SGD,
+                              ones_col=K, partial=part, splits=s)[0]
+        probs = [[pr]]
+        if s > 1:
+            probs.append([ops.reduce_problem(pr)])
+    for _ in range(args.iters):
+        for p in probs:
+            ops.gemm_group(p, ws)
+    torch.cuda.synchronize()
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_.record()
+    for _ in range(args.iters):
+        for p in probs:
+            ops.gemm_group(p, ws)
+    e_.record()
+    torch.cuda.synchronize()
+    t = s_.elapsed_time(e_) / args.iters * 1e-3
+    print(f"{args.kind} B{B} K{K} N{N}: {t * 1e6:.1f} us/iter (eager), "
+          f"{2 * B * N * K / t / 1e12:.1f} TF")
+
+
+if __name__ == "__main__":
+    main()
