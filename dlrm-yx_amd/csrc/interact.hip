@@ -374,17 +374,26 @@ __global__ __launch_bounds__(256) void interact_dot_fwd_v4(int B, int F, FeatArg
   float* Ol = Tl + 32 * DP;
   const int sub = lane / C4, c = lane - sub * C4;
   const bool rowok = l32 < F;
+  constexpr int NI = 32 / RPI;  // row-load instructions covering F <= 32 rows
   for (int64_t b0 = (int64_t)blockIdx.x * 4; b0 < B; b0 += (int64_t)gridDim.x * 4) {
     const int64_t b = b0 + wave;
     const bool active = b < B;
-    if (active) {
-      for (int i0 = 0; i0 < F; i0 += RPI) {
-        const int f = i0 + sub;
-        const float* src = row_ptr<D>(fa, F, b, i0, sub);
-        if (f < F)
-          *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) =
-              *reinterpret_cast<const float4*>(src + 4 * c);
+    {
+      // every row load of the sample is issued before the first LDS write (one memory
+      // latency per sample, not one per row group); rows >= F / inactive waves read a
+      // valid row (feature 0 of sample 0) and store nothing
+      const int64_t bl = active ? b : 0;
+      float4 v[NI];
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const float* src = row_ptr<D>(fa, F, bl, q * RPI, sub);
+        v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
       }
+      // unconditional stores (rows >= F are masked by rowok below; inactive waves' rows are
+      // never read), so no load sinks into a branch and waits alone
+#pragma unroll
+      for (int q = 0; q < NI; ++q)
+        *reinterpret_cast<float4*>(Tl + (q * RPI + sub) * DP + 4 * c) = v[q];
     }
     __syncthreads();
     if (active) {
@@ -445,26 +454,43 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArg
   const int sub = lane / C4, c = lane - sub * C4;
   const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
   const int width = D + npairs;
+  constexpr int NI = 32 / RPI;          // row-load instructions covering 32 rows
+  constexpr int NG = (GP / 4 + 63) / 64;  // float4 of the dR row per lane (vec_g)
   for (int64_t b0 = (int64_t)blockIdx.x * 4; b0 < B; b0 += (int64_t)gridDim.x * 4) {
     const int64_t b = b0 + wave;
     const bool active = b < B;
-    if (active) {
-      for (int i0 = 0; i0 < 32; i0 += RPI) {  // rows >= F are zero (they meet S's zeros)
-        const int f = i0 + sub;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float* src = row_ptr<D>(fa, F, b, i0, sub);
-        if (f < F) v = *reinterpret_cast<const float4*>(src + 4 * c);
-        *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) = v;
+    {
+      // all loads of the sample in flight at once (rows >= F are zero: they meet S's zeros)
+      const int64_t bl = active ? b : 0;
+      float4 v[NI];
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const float* src = row_ptr<D>(fa, F, bl, q * RPI, sub);
+        v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
       }
-      const float* grow = gout + b * ld_g;
-      if (vec_g) {
-        const int w4 = width / 4;
-        for (int q = lane; q < w4; q += 64)
-          *reinterpret_cast<float4*>(Gl + 4 * q) = *reinterpret_cast<const float4*>(grow + 4 * q);
+      const float* grow = gout + bl * ld_g;
+      const int w4 = vec_g ? width / 4 : 0;
+      float4 gv[NG];
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        const int q = lane + 64 * u;
+        gv[u] = q < w4 ? *reinterpret_cast<const float4*>(grow + 4 * q)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      // unconditional stores into this wave's own LDS region (no load sinks into a branch)
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const int f = q * RPI + sub;
+        *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) =
+            f < F ? v[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        const int q = lane + 64 * u;
+        if (4 * (lane + 64 * u) < GP) *reinterpret_cast<float4*>(Gl + 4 * q) = gv[u];
+      }
+      if (active)
         for (int q = 4 * w4 + lane; q < width; q += 64) Gl[q] = grow[q];
-      } else {
-        for (int q = lane; q < width; q += 64) Gl[q] = grow[q];
-      }
     }
     __syncthreads();
     if (active) {
