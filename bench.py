@@ -56,9 +56,10 @@ def num_int(T, D):
     return D + F * (F - 1) // 2
 
 
-def algorithmic_work(c, B_local, B_global, T_local, world):
+def algorithmic_work(c, B_local, B_global, T_local, world, bottom_fused=False):
     """Per-step algorithmic FLOPs of the GEMM launches and bytes of the TBE kernels
-    (SURVEY.md §8d formulas)."""
+    (SURVEY.md §8d formulas).  bottom_fused: the bottom MLP forward
+    ran inside the lookup launch, so its FLOPs are not GEMM-launch work."""
     D, L, T = c["D"], c["L"], len(c["rows"])
     bot = c["bot"]
     top = [num_int(T, D)] + c["top"]
@@ -66,7 +67,8 @@ def algorithmic_work(c, B_local, B_global, T_local, world):
              [(top[i], top[i + 1]) for i in range(len(top) - 2)]  # head (K->1) is not a GEMM
     fl = 0
     for li, (k, n) in enumerate(layers):
-        fl += 2 * B_local * n * k          # forward
+        if not (bottom_fused and li < len(bot) - 1):
+            fl += 2 * B_local * n * k      # forward
         fl += 2 * B_local * n * k          # wgrad
         if li != 0:
             fl += 2 * B_local * n * k      # dgrad (no dgrad for the bottom input layer)
@@ -302,7 +304,8 @@ def main():
     # ---- per-kernel HIP-event timing pass (same step, eager launches) for the roofline
     roofline, emb_roof, groups = None, None, None
     Bl = B // world
-    flops, fwd_bytes, bwd_bytes = algorithmic_work(c, Bl, B, tr.T_local, world)
+    flops, fwd_bytes, bwd_bytes = algorithmic_work(c, Bl, B, tr.T_local, world,
+                                                   bottom_fused=tr.bottom_fused)
     if not args.no_kernel_timing:
         # capture one eager step's launches per kernel group (after the timed region: the
         # captured groups run on stale data, which does not change their timing)

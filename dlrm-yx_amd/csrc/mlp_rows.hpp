@@ -1,0 +1,181 @@
+// Row-block MLP forward: the bottom MLP of the DLRM step (DLRM_Net.apply_mlp over
+// create_mlp's Linear+ReLU stack, dlrm_s_pytorch.py:227-265, 518-524) for 16 samples per
+// workgroup, every layer in one pass with the activations kept in LDS.
+//
+// The bottom MLP is short and narrow (C3: 13 -> 512 -> 256 -> 128 on 2048 samples), so as
+// three GEMM launches it is latency-bound (~25 us for 0.7 GFLOP).  Here a workgroup owns 16
+// rows: it stages their inputs in LDS, and each of its 8 waves computes 16-column tiles of
+// the next activation on v_mfma_f32_16x16x4_f32 (A = the LDS rows, B = weight rows read
+// straight from global/L2 as float4, three 16-k chunks ahead), applies ReLU, writes the tile
+// to the layer's activation buffer (needed by the backward) and into the other LDS
+// buffer as the next layer's input (bias column = 1, zero padding).  No inter-workgroup
+// traffic: the role runs beside the TBE lookup and the backward's index sort inside one
+// launch (tbe_bwd.hip), or alone (dlrm_mlp_chain_forward).
+//
+// Bias folding as in the trainer: layer l's input has in_width[l] columns; for l > 0,
+// column out_width[l-1] is the constant 1 and the rest of the padding is 0; W_l is
+// [out_width[l], >= in_width[l]] with the bias in the bias column.
+#pragma once
+#include "common.hpp"
+#include "dlrm_hip.h"
+
+namespace {
+
+constexpr int kMlpRows = 16;      // samples per workgroup
+constexpr int kMlpWaves = 8;      // waves per workgroup (512 threads)
+constexpr int kMlpTiles = 4;      // 16-column tiles per wave: out_width <= 8 * 4 * 16 = 512
+constexpr int kMlpMaxK = 528;     // input width rounded to 16, LDS capacity
+constexpr int kMlpPitch = kMlpMaxK + 4;
+constexpr int kMlpLdsFloats = 2 * kMlpRows * kMlpPitch;
+
+using mlp_f32x4 = __attribute__((ext_vector_type(4))) float;
+
+struct MlpChain {
+  int layers;
+  int64_t rows;
+  const float* X;
+  int64_t ldx;
+  int kin[DLRM_MLP_MAX_LAYERS];
+  int nout[DLRM_MLP_MAX_LAYERS];
+  const float* W[DLRM_MLP_MAX_LAYERS];
+  int64_t ldw[DLRM_MLP_MAX_LAYERS];
+  float* Y[DLRM_MLP_MAX_LAYERS];
+  int64_t ldy[DLRM_MLP_MAX_LAYERS];
+};
+
+__device__ __forceinline__ void mlp_rows_body(const MlpChain& mc, int64_t blk, float* lds) {
+  constexpr int RB = kMlpRows, P = kMlpPitch, NW = kMlpWaves, MT = kMlpTiles;
+  constexpr int NT = NW * 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar tile tests
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int64_t r0 = blk * RB;
+  float* in = lds;
+  float* nx = lds + RB * P;
+  {  // layer 0 input: X rows, zero-padded to a multiple of 16 columns
+    const int kp = mc.kin[0], kr4 = ((kp + 15) & ~15) / 4;
+    for (int e = tid; e < RB * kr4; e += NT) {
+      const int r = e / kr4, c4 = e - r * kr4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r0 + r < mc.rows && 4 * c4 < kp)
+        v = *reinterpret_cast<const float4*>(mc.X + (r0 + r) * mc.ldx + 4 * c4);
+      *reinterpret_cast<float4*>(in + r * P + 4 * c4) = v;
+    }
+  }
+  __syncthreads();
+  for (int l = 0; l < mc.layers; ++l) {
+    const int kp = mc.kin[l], n = mc.nout[l];
+    const int nch = (kp + 15) / 16, ntile = (n + 15) / 16;
+    const float* W = mc.W[l];
+    const int64_t ldw = mc.ldw[l];
+    // raw buffer loads over exactly W's rows: an out-of-range float4 (column >= n or
+    // k >= in_width) gets an offset past the extent and reads as zeros, so a fetched
+    // register is never touched before its MFMA (no select, no early wait)
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)W, (short)0, (int)(((int64_t)(n - 1) * ldw + kp) * 4), 0x00020000);
+    mlp_f32x4 acc[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[j] = mlp_f32x4{0.f, 0.f, 0.f, 0.f};
+    // B operand of tile j, chunk c: W[col][16c + 4kq .. +3] (zeros past the input width:
+    // the A side is zero there too, but 0 * garbage could be NaN)
+    auto fetch = [&](int c, float4 (&bv)[MT]) {
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int col = (wave + j * NW) * 16 + l16, k = c * 16 + 4 * kq;
+        const int off = (col < n && k < kp) ? (int)((col * ldw + k) * 4) : 0x7ffffff0;
+        bv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0));
+      }
+    };
+    // A fragments: row l16, k = 16c + 4kq .. +3 (read one chunk ahead)
+    auto lda = [&](int c) {
+      return *reinterpret_cast<const float4*>(in + l16 * P + c * 16 + 4 * kq);
+    };
+    float4 a = lda(0);
+    const int nt_w = ntile > wave ? (ntile - wave + NW - 1) / NW : 0;  // this wave's tiles
+    auto step = [&](int c, const float4 (&bv)[MT]) {
+      const float4 an = lda(c + 1 < nch ? c + 1 : c);
+      // k-step outer, tile inner: consecutive MFMAs use different accumulators
+#define MLP_KSTEP(F)                                                                         \
+  _Pragma("unroll") for (int j = 0; j < MT; ++j) if (j < nt_w) acc[j] =                      \
+      __builtin_amdgcn_mfma_f32_16x16x4f32(a.F, bv[j].F, acc[j], 0, 0, 0);
+      MLP_KSTEP(x) MLP_KSTEP(y) MLP_KSTEP(z) MLP_KSTEP(w)
+#undef MLP_KSTEP
+      a = an;
+    };
+    // a ring of four register sets: chunks c+1 .. c+3 in flight under chunk c's MFMAs
+    // (one chunk is only ~512 cycles of MFMA per SIMD; an L2/MALL weight fetch takes longer)
+    float4 b0[MT], b1[MT], b2[MT], b3[MT];
+    fetch(0, b0);
+    if (1 < nch) fetch(1, b1);
+    if (2 < nch) fetch(2, b2);
+    for (int c = 0; c < nch; c += 4) {
+      if (c + 3 < nch) fetch(c + 3, b3);
+      step(c, b0);
+      if (c + 1 >= nch) break;
+      if (c + 4 < nch) fetch(c + 4, b0);
+      step(c + 1, b1);
+      if (c + 2 >= nch) break;
+      if (c + 5 < nch) fetch(c + 5, b1);
+      step(c + 2, b2);
+      if (c + 3 >= nch) break;
+      if (c + 6 < nch) fetch(c + 6, b2);
+      step(c + 3, b3);
+    }
+    // epilogue: ReLU; register r of a 16x16 accumulator = row 4*kq + r, column l16
+    float* Y = mc.Y[l];
+    const int64_t ldy = mc.ldy[l];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int col = (wave + j * NW) * 16 + l16;
+      if (col < n) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 4 * kq + r;
+          const float v = fmaxf(acc[j][r], 0.f);
+          nx[row * P + col] = v;
+          if (r0 + row < mc.rows) Y[(r0 + row) * ldy + col] = v;
+        }
+      }
+    }
+    if (l + 1 < mc.layers) {  // next input: bias column 1, zeros to the 16-column boundary
+      const int kr = (mc.kin[l + 1] + 15) & ~15, extra = kr - n;
+      for (int e = tid; e < RB * extra; e += NT) {
+        const int r = e / extra, c = n + (e - r * extra);
+        nx[r * P + c] = c == n ? 1.f : 0.f;
+      }
+    }
+    __syncthreads();
+    float* t = in;
+    in = nx;
+    nx = t;
+  }
+}
+
+// Host-side check + conversion (the ABI struct -> kernel argument).
+inline int mlp_chain_prepare(const dlrm_mlp_chain* c, MlpChain& mc) {
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!c || c->layers < 1 || c->layers > DLRM_MLP_MAX_LAYERS || c->rows < 0) return 0;
+  if (!c->X || !a16(c->X) || c->ldx % 4 != 0) return 0;
+  mc.layers = c->layers;
+  mc.rows = c->rows;
+  mc.X = c->X;
+  mc.ldx = c->ldx;
+  for (int l = 0; l < c->layers; ++l) {
+    const int64_t kin = c->in_width[l], n = c->out_width[l];
+    if (kin < 1 || kin % 4 != 0 || ((kin + 15) & ~15) > kMlpMaxK) return 0;
+    if (n < 1 || n > kMlpWaves * kMlpTiles * 16) return 0;
+    if (l == 0 ? c->ldx < kin : kin != ((c->out_width[l - 1] + 1 + 3) / 4) * 4) return 0;
+    if (!c->W[l] || !a16(c->W[l]) || c->ldw[l] % 4 != 0 || c->ldw[l] < kin) return 0;
+    if (((n - 1) * c->ldw[l] + kin) * 4 >= 0x7ff00000LL) return 0;  // 32-bit buffer offsets
+    if (!c->Y[l] || c->ldy[l] < n) return 0;
+    mc.kin[l] = (int)kin;
+    mc.nout[l] = (int)n;
+    mc.W[l] = c->W[l];
+    mc.ldw[l] = c->ldw[l];
+    mc.Y[l] = c->Y[l];
+    mc.ldy[l] = c->ldy[l];
+  }
+  return 1;
+}
+
+}  // namespace

@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "mlp_rows.hpp"
 #include "tbe_common.hpp"
 
 namespace {
@@ -287,22 +288,40 @@ __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
 // on the indices, and its T+1 latency-bound workgroups (LDS radix passes on T CUs) run beside
 // the bandwidth-bound gather instead of as a separate launch in the backward.  Blocks
 // [0, T] sort (started first), the rest gather.  512 threads per workgroup.
+// With mlp_blocks > 0 a third role, the bottom MLP forward (mlp_rows.hpp), takes blocks
+// [T+1, T+1+mlp_blocks): it reads only X and the bottom weights, independent of the rest.
 constexpr int kPreThreads = kSegThreads;
+static_assert(kPreThreads == kMlpWaves * 64, "one workgroup size for every role");
+union PresortLds {
+  SegSortLds sort;
+  float mlp[kMlpLdsFloats];
+};
 template <int LPB, int VW, int MAXV, typename IdxT, typename OffT>
 __global__ __launch_bounds__(kPreThreads) void tbe_fwd_presort_kernel(
     const float* __restrict__ W, int64_t D, const int64_t* __restrict__ row_base, int T, int B,
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const float* __restrict__ psw,
     float* __restrict__ out, int64_t out_bs, int32_t* __restrict__ err, int64_t N,
     uint32_t sentinel, uint32_t* __restrict__ keys_out, int32_t* __restrict__ pos_out,
-    int32_t* __restrict__ bag_of) {
-  __shared__ SegSortLds sm;
-  if ((int)blockIdx.x <= T) {
+    int32_t* __restrict__ bag_of, const MlpChain mc, int mlp_blocks) {
+  __shared__ __attribute__((aligned(16))) PresortLds sm;
+  const int b = blockIdx.x;
+  if (b <= T) {
     segsort_body<IdxT, OffT>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of,
-                             err, blockIdx.x, sm);
+                             err, b, sm.sort);
     return;
   }
+  if (b < T + 1 + mlp_blocks) {
+    mlp_rows_body(mc, b - (T + 1), sm.mlp);
+    return;
+  }
+  const int g0 = T + 1 + mlp_blocks;
   tbe_fwd_body<LPB, VW, MAXV, IdxT, OffT>(W, D, row_base, T, B, idx, off, psw, out, out_bs, err,
-                                          (int64_t)blockIdx.x - (T + 1), (int64_t)gridDim.x - (T + 1));
+                                          (int64_t)b - g0, (int64_t)gridDim.x - g0);
+}
+
+__global__ __launch_bounds__(kMlpWaves * 64) void mlp_chain_kernel(const MlpChain mc) {
+  __shared__ __attribute__((aligned(16))) float lds[kMlpLdsFloats];
+  mlp_rows_body(mc, blockIdx.x, lds);
 }
 
 enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2 };
@@ -918,7 +937,7 @@ template <typename IdxT, typename OffT>
 int launch_fwd_presort(const float* W, int64_t D, const int64_t* row_base, int T, int B,
                        const void* idx, const void* off, const float* psw, float* out,
                        int64_t out_bs, int64_t N, int64_t total_rows, void* ws, size_t ws_bytes,
-                       int32_t* err, hipStream_t st) {
+                       int32_t* err, const MlpChain& mc, int mlp_blocks, hipStream_t st) {
   const char* name = "dlrm_tbe_forward_presort";
   const int end_bit = bit_width_u64((uint64_t)total_rows);
   BwdWs<uint32_t> w = carve_bwd_ws<uint32_t>(ws, N, D, end_bit);
@@ -936,14 +955,15 @@ int launch_fwd_presort(const float* W, int64_t D, const int64_t* row_base, int T
   int64_t gblocks = dlrm::ceil_div(dlrm::ceil_div(nbags, gpw), kPreThreads / 64);
   if (gblocks > 8192) gblocks = 8192;
   if (gblocks < 1) gblocks = 1;
-  const dim3 grid((unsigned)(T + 1 + gblocks)), block(kPreThreads);
+  const dim3 grid((unsigned)(T + 1 + mlp_blocks + gblocks)), block(kPreThreads);
   const IdxT* ip = static_cast<const IdxT*>(idx);
   const OffT* op = static_cast<const OffT*>(off);
   const uint32_t sentinel = (uint32_t)total_rows;
 #define PRE(LPB, VW, MV)                                                                         \
   hipLaunchKernelGGL((tbe_fwd_presort_kernel<LPB, VW, MV, IdxT, OffT>), grid, block, 0, st, W, D, \
                      row_base, T, B, ip, op, psw, out, out_bs, err, N, sentinel,                  \
-                     reinterpret_cast<uint32_t*>(w.keys_out), w.pos_out, w.bag_of)
+                     reinterpret_cast<uint32_t*>(w.keys_out), w.pos_out, w.bag_of, mc,       \
+                     mlp_blocks)
 #define PRE_LPB(VW)                        \
   switch (lpb) {                           \
     case 1: PRE(1, VW, 1); break;          \
@@ -979,12 +999,22 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
                                         int64_t num_lookups, int64_t total_rows,
                                         int64_t max_lookups_per_table, void* workspace,
                                         size_t workspace_bytes, int32_t* error_flag,
-                                        dlrm_stream_t stream) {
+                                        const dlrm_mlp_chain* bottom, dlrm_stream_t stream) {
   const char* name = "dlrm_tbe_forward_presort";
+  MlpChain mc{};
+  int mlp_blocks = 0;
+  if (bottom) {
+    DLRM_ARG(mlp_chain_prepare(bottom, mc), "%s: unsupported bottom MLP chain", name);
+    mlp_blocks = (int)dlrm::ceil_div(bottom->rows, kMlpRows);
+  }
   if (!presort_applies((uint64_t)total_rows < 0xFFFFFFFFull ? 4 : 8, max_lookups_per_table,
-                       num_lookups) || num_lookups == 0 || T * (int64_t)B >= INT32_MAX)
-    return dlrm_tbe_forward(weights, D, row_base, T, B, indices, index_bits, offsets, offset_bits,
-                            per_sample_weights, out, out_batch_stride, error_flag, stream);
+                       num_lookups) || num_lookups == 0 || T * (int64_t)B >= INT32_MAX) {
+    const int rc = dlrm_tbe_forward(weights, D, row_base, T, B, indices, index_bits, offsets,
+                                    offset_bits, per_sample_weights, out, out_batch_stride,
+                                    error_flag, stream);
+    if (rc != DLRM_OK || !bottom) return rc;
+    return dlrm_mlp_chain_forward(bottom, stream);
+  }
   DLRM_ARG(weights && row_base && out && offsets && indices, "%s: null pointer", name);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: index_bits must be 32|64", name);
@@ -995,10 +1025,27 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
 #define PS(I, O)                                                                           \
   return launch_fwd_presort<I, O>(weights, D, row_base, T, B, indices, offsets,            \
                                   per_sample_weights, out, out_batch_stride, num_lookups,  \
-                                  total_rows, workspace, workspace_bytes, error_flag, st)
+                                  total_rows, workspace, workspace_bytes, error_flag, mc,  \
+                                  mlp_blocks, st)
   if (index_bits == 32 && offset_bits == 32) PS(int32_t, int32_t);
   if (index_bits == 32) PS(int32_t, int64_t);
   if (offset_bits == 32) PS(int64_t, int32_t);
   PS(int64_t, int64_t);
 #undef PS
+}
+
+extern "C" int dlrm_mlp_chain_supported(const dlrm_mlp_chain* chain) {
+  MlpChain mc{};
+  return mlp_chain_prepare(chain, mc);
+}
+
+extern "C" int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream) {
+  const char* name = "dlrm_mlp_chain_forward";
+  MlpChain mc{};
+  DLRM_ARG(mlp_chain_prepare(chain, mc), "%s: unsupported chain", name);
+  if (chain->rows == 0) return DLRM_OK;
+  hipLaunchKernelGGL(mlp_chain_kernel, dim3((unsigned)dlrm::ceil_div(chain->rows, kMlpRows)),
+                     dim3(kMlpWaves * 64), 0, dlrm::as_stream(stream), mc);
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
 }

@@ -36,6 +36,17 @@ class GemmProblem(ctypes.Structure):
                 ("splits", c_int32), ("partial", c_void_p)]
 
 
+MLP_MAX_LAYERS = 4
+
+
+class MlpChain(ctypes.Structure):
+    """struct dlrm_mlp_chain (include/dlrm_hip.h)."""
+    _fields_ = [("layers", c_int32), ("rows", c_int64), ("X", c_void_p), ("ldx", c_int64),
+                ("in_width", c_int64 * MLP_MAX_LAYERS), ("out_width", c_int64 * MLP_MAX_LAYERS),
+                ("W", c_void_p * MLP_MAX_LAYERS), ("ldw", c_int64 * MLP_MAX_LAYERS),
+                ("Y", c_void_p * MLP_MAX_LAYERS), ("ldy", c_int64 * MLP_MAX_LAYERS)]
+
+
 # name -> (restype, argtypes); mirrors include/dlrm_hip.h exactly.
 P = c_void_p
 SIGNATURES = {
@@ -56,7 +67,9 @@ SIGNATURES = {
                                           c_size_t, P, c_int32, P]),
     "dlrm_tbe_forward_presort": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P,
                                            c_int32, P, P, c_int64, c_int64, c_int64, c_int64, P,
-                                           c_size_t, P, P]),
+                                           c_size_t, P, P, P]),
+    "dlrm_mlp_chain_supported": (c_int32, [P]),
+    "dlrm_mlp_chain_forward": (c_int32, [P, P]),
     "dlrm_tbe_expand_grad": (c_int32, [c_int64, c_int32, c_int32, P, c_int32, c_int64, P, P,
                                        c_int64, P, P]),
     "dlrm_qr_split_indices": (c_int32, [P, c_int32, c_int64, c_int64, P, P, P]),

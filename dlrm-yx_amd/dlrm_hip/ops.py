@@ -103,14 +103,44 @@ def tbe_forward(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
     return out
 
 
+def mlp_chain(X: torch.Tensor, layers) -> "_lib.MlpChain":
+    """dlrm_mlp_chain for a bias-folded Linear+ReLU stack: ``X`` [rows, >= in_width[0]]
+    carries its own bias column; ``layers`` = [(W [n, >= kin], Y [rows, >= n], kin)]."""
+    c = _lib.MlpChain()
+    c.layers = len(layers)
+    c.rows = X.shape[0]
+    c.X = X.data_ptr()
+    c.ldx = X.stride(0)
+    for i, (W, Y, kin) in enumerate(layers):
+        c.in_width[i] = int(kin)
+        c.out_width[i] = W.shape[0]
+        c.W[i] = W.data_ptr()
+        c.ldw[i] = W.stride(0)
+        c.Y[i] = Y.data_ptr()
+        c.ldy[i] = Y.stride(0)
+    return c
+
+
+def mlp_chain_supported(chain) -> bool:
+    return bool(_lib.load().dlrm_mlp_chain_supported(ctypes.byref(chain)))
+
+
+def mlp_chain_forward(chain, device=None) -> None:
+    """Every layer of the chain in one launch (dlrm_mlp_chain_forward)."""
+    dev = device if device is not None else torch.cuda.current_device()
+    _lib.call("dlrm_mlp_chain_forward", ctypes.cast(ctypes.byref(chain), ctypes.c_void_p),
+              _stream(dev))
+
+
 def tbe_forward_presort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
                         indices: torch.Tensor, offsets: torch.Tensor, workspace: torch.Tensor,
                         max_lookups_per_table: int, out: Optional[torch.Tensor] = None,
                         out_batch_stride: Optional[int] = None,
                         per_sample_weights: Optional[torch.Tensor] = None,
-                        error_flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        error_flag: Optional[torch.Tensor] = None, bottom=None) -> torch.Tensor:
     """tbe_forward + this batch's backward sort in one launch (dlrm_tbe_forward_presort);
-    follow with tbe_backward(..., workspace, presorted=True)."""
+    follow with tbe_backward(..., workspace, presorted=True).  ``bottom``: an mlp_chain
+    (the bottom MLP forward) run as a third role of the same launch."""
     _check_cuda(weights, row_base, indices, offsets, workspace, per_sample_weights)
     D = weights.shape[1]
     if out is None:
@@ -121,7 +151,9 @@ def tbe_forward_presort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B
     _lib.call("dlrm_tbe_forward_presort", _p(weights), D, _p(row_base), T, B, _p(indices),
               _bits(indices), _p(offsets), _bits(offsets), _p(per_sample_weights), _p(out),
               out_batch_stride, indices.numel(), weights.shape[0], int(max_lookups_per_table),
-              _p(workspace), workspace.numel(), _p(error_flag), _stream(weights.device))
+              _p(workspace), workspace.numel(), _p(error_flag),
+              ctypes.cast(ctypes.byref(bottom), ctypes.c_void_p) if bottom is not None else None,
+              _stream(weights.device))
     return out
 
 

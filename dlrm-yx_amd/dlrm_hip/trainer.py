@@ -175,6 +175,9 @@ class DLRMTrainer:
         # MLP backward: a layer's split wgrad (partials only) in the same launch as its dgrad
         self.group_wgrad = os.environ.get("DLRM_GROUP_WGRAD", "1") != "0"
         self.full_last_wgrad = os.environ.get("DLRM_FULL_LAST_WGRAD", "0") == "1"
+        # one GPU: the bottom MLP forward as a role of the lookup launch (mlp_rows.hpp)
+        self.fuse_bottom = os.environ.get("DLRM_FUSE_BOTTOM", "1") != "0"
+        self.bottom_fused = False  # set by the last step
         # device TBE error bits (ops.TBE_ERR_*): out-of-range indices are skipped by the
         # kernels and flagged here; check_errors() reads it (the step never syncs)
         self.tbe_error_flag = torch.zeros(1, dtype=torch.int32, device=self.dev)
@@ -442,6 +445,17 @@ class DLRMTrainer:
                 h = out
 
         def fwd_single():  # one GPU: bottom MLP || lookup
+            chain = self._bottom_chain(batch, bufs) if presort and not c_fwd else None
+            self.bottom_fused = chain is not None
+            if chain is not None:
+                # the bottom MLP forward runs as a role of the lookup launch
+                with prof("tbe_fwd"):
+                    ops.tbe_forward_presort(self.weights, self.row_base, self.T_local, B,
+                                            batch.indices, batch.offsets,
+                                            self._ws_tbe(batch.indices.numel()),
+                                            batch.max_per_table, out=bufs["E"],
+                                            error_flag=self.tbe_error_flag, bottom=chain)
+                return
             s0, s1 = streams()
             if c_fwd:
                 s1.wait_stream(s0)
@@ -692,6 +706,15 @@ class DLRMTrainer:
         else:
             self._colsum(hin[:, :last.Kp], scale=dz, out=last.gW[0],
                          workspace=self._ws_colsum(Bl, last.Kp))
+
+    def _bottom_chain(self, batch: Batch, bufs):
+        """The bottom MLP forward as a dlrm_mlp_chain (None when disabled or unsupported,
+        or when there are no local tables to share a launch with)."""
+        if not self.fuse_bottom or self.T_local == 0:
+            return None
+        chain = ops.mlp_chain(batch.X, [(L.W, out, L.Kp)
+                                        for L, out in zip(self.bot, bufs["bot_act"])])
+        return chain if ops.mlp_chain_supported(chain) else None
 
     def _ws_tbe(self, n: int) -> torch.Tensor:
         need = ops.tbe_backward_workspace_size(n, self.total_rows, self.D)

@@ -114,12 +114,45 @@ int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base, i
                      int64_t out_batch_stride, int32_t* error_flag, dlrm_stream_t stream);
 
 /*
+ * A Linear+ReLU stack with the bias folded into the weights (the trainer's layout of the
+ * bottom MLP, DLRM_Net.create_mlp / apply_mlp, dlrm_s_pytorch.py:227-265, 518-524):
+ *   Y_l[r][c] = relu(sum_{k < in_width[l]} In_l[r][k] * W_l[c][k]),  c < out_width[l]
+ * with In_0 = X (which carries its own bias column) and, for l > 0, In_l = Y_{l-1} with
+ * column out_width[l-1] = 1 and the remaining padding 0; in_width[l] =
+ * pad4(out_width[l-1] + 1).  Only columns < out_width[l] of Y_l are written.  Supported
+ * (dlrm_mlp_chain_supported): 1..4 layers, out_width <= 512, in_width rounded up to 16
+ * <= 528, X and W 16-byte aligned with row strides % 4 == 0.
+ */
+#define DLRM_MLP_MAX_LAYERS 4
+typedef struct dlrm_mlp_chain {
+  int32_t layers;
+  int64_t rows;
+  const float* X;
+  int64_t ldx;
+  int64_t in_width[DLRM_MLP_MAX_LAYERS];
+  int64_t out_width[DLRM_MLP_MAX_LAYERS];
+  const float* W[DLRM_MLP_MAX_LAYERS];
+  int64_t ldw[DLRM_MLP_MAX_LAYERS];
+  float* Y[DLRM_MLP_MAX_LAYERS];
+  int64_t ldy[DLRM_MLP_MAX_LAYERS];
+} dlrm_mlp_chain;
+
+/* 1 when dlrm_mlp_chain_forward / the fused forward can take this chain, else 0. */
+int dlrm_mlp_chain_supported(const dlrm_mlp_chain* chain);
+
+/* The chain on its own: 16 rows per workgroup, every layer in one launch. */
+int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream);
+
+/*
  * dlrm_tbe_forward + the per-table sort of the backward (which depends only on the
  * indices) in ONE launch: the sort's latency-bound workgroups run beside the gather.
  * The sort lands in `workspace` (a dlrm_tbe_backward_* workspace); call the backward of
  * the same batch with presorted = 1.  When the per-table sort does not apply (64-bit row
  * ids, max_lookups_per_table 0 or > 4096) this is dlrm_tbe_forward and the backward
  * sorts as usual.
+ * bottom != NULL: the bottom MLP forward (an independent input of the same step) runs as
+ * a third role of the same launch (dlrm_mlp_chain semantics; it must be supported); when
+ * the presort does not apply it runs as its own launch.
  */
 int dlrm_tbe_forward_presort(const float* weights, int64_t D, const int64_t* row_base, int32_t T,
                              int32_t B, const void* indices, int32_t index_bits,
@@ -127,7 +160,8 @@ int dlrm_tbe_forward_presort(const float* weights, int64_t D, const int64_t* row
                              const float* per_sample_weights, float* out,
                              int64_t out_batch_stride, int64_t num_lookups, int64_t total_rows,
                              int64_t max_lookups_per_table, void* workspace,
-                             size_t workspace_bytes, int32_t* error_flag, dlrm_stream_t stream);
+                             size_t workspace_bytes, int32_t* error_flag,
+                             const dlrm_mlp_chain* bottom, dlrm_stream_t stream);
 
 /* Workspace for the deterministic (sorted, segment-reduced) backward. */
 size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows, int64_t D);

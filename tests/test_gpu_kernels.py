@@ -702,3 +702,94 @@ def test_interact_backward_relu_x_and_paths(ops, monkeypatch, path, D):
     out = ops.interact_forward("dot", x.to(dev), ly.to(dev))
     ok, msg = fp32_close(out.cpu().numpy(), R.detach().numpy())
     assert ok, msg
+
+
+def _mlp_ref(X, layers):
+    """fp64 reference of the bias-folded ReLU chain (trainer layout)."""
+    h = X.double()
+    outs = []
+    for W, Y, kin in layers:
+        n = W.shape[0]
+        y = torch.relu(h[:, :kin] @ W[:, :kin].double().t())
+        outs.append(y)
+        h = torch.zeros(X.shape[0], (n + 1 + 3) // 4 * 4, dtype=torch.float64, device=X.device)
+        h[:, :n] = y
+        h[:, n] = 1.0
+    return outs
+
+
+def _mlp_setup(rows, dims, seed=5):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    pad4 = lambda n: (n + 3) // 4 * 4  # noqa: E731
+    k0 = dims[0]
+    X = torch.zeros(rows, pad4(k0 + 1), device=dev)
+    X[:, :k0] = torch.rand(rows, k0, generator=g, device=dev)
+    X[:, k0] = 1.0
+    layers = []
+    for k, n in zip(dims[:-1], dims[1:]):
+        W = torch.randn(n, pad4(k + 1), generator=g, device=dev) / (k ** 0.5)
+        W[:, k + 1:] = 0.0
+        Y = torch.full((rows, pad4(n + 1)), -7.0, device=dev)
+        layers.append((W, Y, pad4(k + 1)))
+    return X, layers
+
+
+@pytest.mark.parametrize("rows,dims", [(2048, [13, 512, 256, 128]), (37, [13, 512, 256, 128]),
+                                       (100, [3, 64, 16]), (48, [200, 120, 500, 33, 7])])
+def test_mlp_chain_forward_matches_reference(ops, rows, dims):
+    """The row-block bottom-MLP kernel (every layer in one launch, activations in LDS) vs an
+    fp64 chain; ragged batch (37 rows), widths that are not multiples of 16 or 64, 4 layers.
+    Only columns < out_width of each output are written."""
+    X, layers = _mlp_setup(rows, dims)
+    chain = ops.mlp_chain(X, layers)
+    assert ops.mlp_chain_supported(chain)
+    ops.mlp_chain_forward(chain)
+    torch.cuda.synchronize()
+    ref = _mlp_ref(X, layers)
+    for (W, Y, kin), r in zip(layers, ref):
+        n = W.shape[0]
+        got = Y[:, :n].double()
+        err = (got - r).abs().max().item()
+        scale = max(1.0, r.abs().max().item())
+        assert err <= 1e-5 * scale, err
+        assert torch.all(Y[:, n:] == -7.0)  # padding / bias column untouched
+
+
+def test_mlp_chain_unsupported_is_refused(ops):
+    X, layers = _mlp_setup(16, [13, 1024, 8])  # out_width 1024 > 512
+    chain = ops.mlp_chain(X, layers)
+    assert not ops.mlp_chain_supported(chain)
+    with pytest.raises(Exception):
+        ops.mlp_chain_forward(chain)
+
+
+def test_tbe_forward_presort_with_bottom_chain(ops):
+    """The fused launch (sort + gather + bottom MLP) gives the plain forward's E bitwise and
+    the standalone chain's activations bitwise; the presorted backward still matches."""
+    torch.manual_seed(3)
+    rows, D, B, L = [3, 5000, 700, 90000], 128, 2048, 1
+    T = len(rows)
+    lo = [torch.arange(B) * L for _ in rows]
+    li = [torch.randint(0, n, (B * L,)) for n in rows]
+    off, idx = O.batched_csr(lo, li)
+    idx, off = idx.to(dev), off.to(dev)
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    W = torch.randn(sum(rows), D, device=dev)
+    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), sum(rows), D),
+                     dtype=torch.uint8, device=dev)
+    X, layers = _mlp_setup(B, [13, 512, 256, 128])
+    X2, layers2 = X.clone(), [(w, y.clone(), k) for w, y, k in layers]
+    E0 = ops.tbe_forward(W, row_base, T, B, idx, off)
+    E1 = ops.tbe_forward_presort(W, row_base, T, B, idx, off, ws, B,
+                                 bottom=ops.mlp_chain(X, layers))
+    ops.mlp_chain_forward(ops.mlp_chain(X2, layers2))
+    torch.cuda.synchronize()
+    assert torch.equal(E0, E1)
+    for (_, y1, _), (_, y2, _) in zip(layers, layers2):
+        assert torch.equal(y1, y2)
+    G = torch.randn(B, T, D, device=dev)
+    Wa, Wb = W.clone(), W.clone()
+    ops.tbe_backward("sgd", Wa, row_base, T, B, idx, off, G, lr=0.1, workspace=ws,
+                     max_lookups_per_table=B, presorted=True)
+    ops.tbe_backward("sgd", Wb, row_base, T, B, idx, off, G, lr=0.1, max_lookups_per_table=B)
+    assert torch.equal(Wa, Wb)

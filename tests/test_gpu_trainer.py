@@ -149,6 +149,7 @@ def test_side_stream_schedule_matches_serial(graph):
         tr = DLRMTrainer(cfg, device=dev, seed=11)
         tr.concurrent = conc
         tr.overlaps = {"fwd", "top", "bot"}
+        tr.fuse_bottom = False  # the "fwd" overlap runs the bottom MLP as GEMMs: compare alike
         batches = [tr.synthetic_batch(512, 1, seed=s) for s in range(3)]
         if graph and conc:
             tr.step(batches[0])  # allocate buffers outside capture
@@ -190,6 +191,7 @@ def test_batch_size_changes_with_overlaps_match_serial():
         tr = DLRMTrainer(cfg, device=dev, seed=13)
         tr.concurrent = conc
         tr.overlaps = {"fwd", "top", "bot"}
+        tr.fuse_bottom = False
         seq = [tr.synthetic_batch(B, 1, seed=s) for s, B in enumerate((2048, 1000, 2048, 1000))]
         for b in seq:
             tr.step(b)
@@ -218,3 +220,29 @@ def test_out_of_range_index_is_flagged():
     with pytest.raises(ops.TBEIndexError):
         tr.check_errors()
     tr.check_errors()  # the flag was reset
+
+
+def test_fused_bottom_mlp_step_matches_gemm_path():
+    """The bottom MLP forward inside the lookup launch (mlp_rows.hpp) vs the same step with
+    the bottom MLP as GEMM launches: the two sum in different orders, so the trained state
+    agrees within fp32 tolerance, not bitwise."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES["c3_small"]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function="bce",
+                        learning_rate=0.1)
+    res = []
+    for fuse in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.fuse_bottom = fuse
+        batches = [tr.synthetic_batch(512, 1, seed=s) for s in range(3)]
+        for b in batches:
+            tr.step(b)
+        assert tr.bottom_fused == fuse
+        torch.cuda.synchronize()
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
+                    tr._bufs[(512, 512)]["prob"].cpu().clone()))
+    for a, b in zip(*res):
+        ok, msg = fp32_close(b.numpy(), a.numpy(), atol=1e-4)  # 3 steps of drift
+        assert ok, msg
