@@ -22,8 +22,9 @@
 namespace {
 
 constexpr int kMlpRows = 16;      // samples per workgroup
-constexpr int kMlpWaves = 8;      // waves per workgroup (512 threads)
-constexpr int kMlpTiles = 4;      // 16-column tiles per wave: out_width <= 8 * 4 * 16 = 512
+constexpr int kMlpWaves = 16;     // waves per workgroup (1024 threads)
+constexpr int kMlpTiles = 2;      // 16-column tiles per wave: out_width <= 16 * 2 * 16 = 512
+static_assert(kMlpTiles == 2, "mlp_rows_body dispatches mlp_kloop<1..2>");
 constexpr int kMlpMaxK = 528;     // input width rounded to 16, LDS capacity
 constexpr int kMlpPitch = kMlpMaxK + 4;
 constexpr int kMlpLdsFloats = 2 * kMlpRows * kMlpPitch;
@@ -42,6 +43,66 @@ struct MlpChain {
   float* Y[DLRM_MLP_MAX_LAYERS];
   int64_t ldy[DLRM_MLP_MAX_LAYERS];
 };
+
+// K loop of one layer for this wave's NTW column tiles: acc[j] += A(16 x kp) . W_tile^T.
+// A fragments come from LDS (row l16, k = 16c + 4kq .. +3, read one chunk ahead); B
+// fragments are raw buffer loads of W[col][16c + 4kq .. +3] kept in a ring of four
+// register sets (chunks c+1 .. c+3 in flight under chunk c's MFMAs: one chunk is only a
+// few hundred cycles of MFMA, an L2/MALL weight fetch takes longer).  An out-of-range
+// float4 (column >= n or k >= in_width) gets an offset past the descriptor's extent and
+// reads as zeros, so a fetched register is never touched before its MFMA.
+template <int NTW>
+__device__ __forceinline__ void mlp_kloop(mlp_f32x4 (&acc)[kMlpTiles], const float* in,
+                                          __amdgpu_buffer_rsrc_t rw, int wave, int n, int kp,
+                                          int64_t ldw, int nch, int l16, int kq) {
+  constexpr int P = kMlpPitch, NW = kMlpWaves;
+  auto fetch = [&](int c, float4 (&bv)[NTW]) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int col = (wave + j * NW) * 16 + l16, k = c * 16 + 4 * kq;
+      const int off = (col < n && k < kp) ? (int)((col * ldw + k) * 4) : 0x7ffffff0;
+      bv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0));
+    }
+  };
+  auto lda = [&](int c) {
+    return *reinterpret_cast<const float4*>(in + l16 * P + c * 16 + 4 * kq);
+  };
+  float4 a = lda(0);
+  auto step = [&](int c, const float4 (&bv)[NTW]) {
+    const float4 an = lda(c + 1 < nch ? c + 1 : c);
+    // k-step outer, tile inner: consecutive MFMAs use different accumulators
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv[j].x, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv[j].y, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv[j].z, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv[j].w, acc[j], 0, 0, 0);
+    a = an;
+  };
+  float4 b0[NTW], b1[NTW], b2[NTW], b3[NTW];
+  fetch(0, b0);
+  if (1 < nch) fetch(1, b1);
+  if (2 < nch) fetch(2, b2);
+  for (int c = 0; c < nch; c += 4) {
+    if (c + 3 < nch) fetch(c + 3, b3);
+    step(c, b0);
+    if (c + 1 >= nch) break;
+    if (c + 4 < nch) fetch(c + 4, b0);
+    step(c + 1, b1);
+    if (c + 2 >= nch) break;
+    if (c + 5 < nch) fetch(c + 5, b1);
+    step(c + 2, b2);
+    if (c + 3 >= nch) break;
+    if (c + 6 < nch) fetch(c + 6, b2);
+    step(c + 3, b3);
+  }
+}
 
 __device__ __forceinline__ void mlp_rows_body(const MlpChain& mc, int64_t blk, float* lds) {
   constexpr int RB = kMlpRows, P = kMlpPitch, NW = kMlpWaves, MT = kMlpTiles;
@@ -68,58 +129,19 @@ __device__ __forceinline__ void mlp_rows_body(const MlpChain& mc, int64_t blk, f
     const int nch = (kp + 15) / 16, ntile = (n + 15) / 16;
     const float* W = mc.W[l];
     const int64_t ldw = mc.ldw[l];
-    // raw buffer loads over exactly W's rows: an out-of-range float4 (column >= n or
-    // k >= in_width) gets an offset past the extent and reads as zeros, so a fetched
-    // register is never touched before its MFMA (no select, no early wait)
+    // raw buffer loads over exactly W's rows (mlp_kloop)
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
         (void*)W, (short)0, (int)(((int64_t)(n - 1) * ldw + kp) * 4), 0x00020000);
     mlp_f32x4 acc[MT];
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[j] = mlp_f32x4{0.f, 0.f, 0.f, 0.f};
-    // B operand of tile j, chunk c: W[col][16c + 4kq .. +3] (zeros past the input width:
-    // the A side is zero there too, but 0 * garbage could be NaN)
-    auto fetch = [&](int c, float4 (&bv)[MT]) {
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int col = (wave + j * NW) * 16 + l16, k = c * 16 + 4 * kq;
-        const int off = (col < n && k < kp) ? (int)((col * ldw + k) * 4) : 0x7ffffff0;
-        bv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0));
-      }
-    };
-    // A fragments: row l16, k = 16c + 4kq .. +3 (read one chunk ahead)
-    auto lda = [&](int c) {
-      return *reinterpret_cast<const float4*>(in + l16 * P + c * 16 + 4 * kq);
-    };
-    float4 a = lda(0);
     const int nt_w = ntile > wave ? (ntile - wave + NW - 1) / NW : 0;  // this wave's tiles
-    auto step = [&](int c, const float4 (&bv)[MT]) {
-      const float4 an = lda(c + 1 < nch ? c + 1 : c);
-      // k-step outer, tile inner: consecutive MFMAs use different accumulators
-#define MLP_KSTEP(F)                                                                         \
-  _Pragma("unroll") for (int j = 0; j < MT; ++j) if (j < nt_w) acc[j] =                      \
-      __builtin_amdgcn_mfma_f32_16x16x4f32(a.F, bv[j].F, acc[j], 0, 0, 0);
-      MLP_KSTEP(x) MLP_KSTEP(y) MLP_KSTEP(z) MLP_KSTEP(w)
-#undef MLP_KSTEP
-      a = an;
-    };
-    // a ring of four register sets: chunks c+1 .. c+3 in flight under chunk c's MFMAs
-    // (one chunk is only ~512 cycles of MFMA per SIMD; an L2/MALL weight fetch takes longer)
-    float4 b0[MT], b1[MT], b2[MT], b3[MT];
-    fetch(0, b0);
-    if (1 < nch) fetch(1, b1);
-    if (2 < nch) fetch(2, b2);
-    for (int c = 0; c < nch; c += 4) {
-      if (c + 3 < nch) fetch(c + 3, b3);
-      step(c, b0);
-      if (c + 1 >= nch) break;
-      if (c + 4 < nch) fetch(c + 4, b0);
-      step(c + 1, b1);
-      if (c + 2 >= nch) break;
-      if (c + 5 < nch) fetch(c + 5, b1);
-      step(c + 2, b2);
-      if (c + 3 >= nch) break;
-      if (c + 6 < nch) fetch(c + 6, b2);
-      step(c + 3, b3);
+    // the tile count is a template argument of the K loop: no branch inside it, so the
+    // compiler's vmcnt accounting keeps the prefetched chunks in flight
+    switch (nt_w) {
+      case 1: mlp_kloop<1>(acc, in, rw, wave, n, kp, ldw, nch, l16, kq); break;
+      case 2: mlp_kloop<2>(acc, in, rw, wave, n, kp, ldw, nch, l16, kq); break;
+      default: break;
     }
     // epilogue: ReLU; register r of a 16x16 accumulator = row 4*kq + r, column l16
     float* Y = mc.Y[l];

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
 // (the caller's max_lookups_per_table was an underestimate) is not sorted: all its lookups
 // become sentinels (no update, no stale keys, no out-of-bounds row) and bit
 // DLRM_TBE_ERR_TABLE_CAP is raised in *err.
-constexpr int kSegThreads = 512, kSegItems = 8;
+constexpr int kSegThreads = 1024, kSegItems = 4;
 constexpr int kSegCap = kSegThreads * kSegItems;  // lookups per table
 constexpr int kSegWaves = kSegThreads / 64;
 constexpr int kDigitBits = 8;
