@@ -16,8 +16,8 @@ device buffer and apply_emb is ONE table-batched launch; the MLPs are HipMLP
 (one fused Function per MLP); the interaction is the MFMA kernel.
 
 Not on this path (documented in DESIGN.md): parallel_forward (single-process multi-GPU;
-the MI355X path is one process per GPU), fbgemm fp16 tables, mixed-dimension tables,
-learned per-sample weights, 4/8-bit quantized inference.
+the MI355X path is one process per GPU), mixed-dimension tables, learned per-sample
+weights.  4/8-bit quantized inference (quantize_embedding) runs on dlrm_tbe_forward_rows.
 """
 from __future__ import annotations
 
@@ -197,10 +197,58 @@ class DLRM_Net(nn.Module):
     def apply_mlp(self, x, layers):
         return layers(x)
 
+    def quantize_embedding(self, bits):
+        """dlrm_s_pytorch.py:609-625: 4- or 8-bit row-wise quantization of every table with
+        the reference's own packers (torch.ops.quantized.embedding_bag_{4bit,byte}_prepack,
+        CPU, once); the packed rows are then kept on the device as ONE [sum rows, row_bytes]
+        buffer that apply_emb reads with one dlrm_tbe_forward_rows launch."""
+        n = len(self.emb_l)
+        self.emb_l_q = [None] * n
+        if bits not in (4, 8):
+            return
+        pack = (torch.ops.quantized.embedding_bag_4bit_prepack if bits == 4
+                else torch.ops.quantized.embedding_bag_byte_prepack)
+        dev = None
+        for k in range(n):
+            w = self.emb_l[k].weight
+            dev = w.device
+            self.emb_l_q[k] = pack(w.detach().float().cpu().contiguous())
+        rows = [int(q.shape[0]) for q in self.emb_l_q]
+        self._q_rows = torch.cat(self.emb_l_q, 0).to(dev)
+        self._q_row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64,
+                                        device=dev)
+        self._q_fmt = ops.ROWS_Q4 if bits == 4 else ops.ROWS_Q8
+        self.emb_l = None
+        self.quantize_emb = True
+        self.quantize_bits = bits
+
+    def _apply_emb_quantized(self, lS_o, lS_i):
+        """apply_emb's quantized branch (dlrm_s_pytorch.py:554-567) for all tables in one
+        launch: embedding_bag_{4bit,byte}_rowwise_offsets semantics, per-sample weights
+        from v_W_l as in the reference."""
+        T = len(self.emb_l_q)
+        dev = self._q_rows.device
+        offs = [lS_o[k].to(dev) for k in range(T)]
+        idxs = [lS_i[k].reshape(-1).to(dev) for k in range(T)]
+        B = int(offs[0].numel())
+        counts = [int(i.numel()) for i in idxs]
+        offsets = ops.csr_from_tables(offs, counts, B, out_dtype=torch.int64)
+        indices = torch.cat(idxs) if T > 1 else idxs[0]
+        psw = None
+        if any(w is not None for w in self.v_W_l):
+            psw = torch.cat([(self.v_W_l[k].to(dev).gather(0, idxs[k]) if self.v_W_l[k] is not None
+                              else torch.ones(counts[k], device=dev)) for k in range(T)])
+        D = int(self.m_spa)
+        out = ops.tbe_forward_rows(self._q_rows, self._q_fmt, D, self._q_row_base, T, B, indices,
+                                   offsets, per_sample_weights=psw)
+        return [out[:, k, :] for k in range(T)]
+
     def apply_emb(self, lS_o, lS_i):
         """dlrm_s_pytorch.py:526-587.  lS_o: [T, B] tensor or T tensors of B bag starts;
         lS_i: [T, N] tensor or T index tensors (table-local rows).  Plain tables run as ONE
         table-batched kernel (device CSR build + pooled sum); QR tables per table."""
+        if self.quantize_emb:
+            return self._apply_emb_quantized(lS_o, lS_i)
         emb_l = self.emb_l
         T = len(emb_l)
         offs = [lS_o[k] for k in range(T)]

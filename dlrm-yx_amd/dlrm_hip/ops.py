@@ -157,6 +157,38 @@ def tbe_forward_presort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B
     return out
 
 
+ROWS_F32, ROWS_F16, ROWS_Q8, ROWS_Q4 = 0, 1, 2, 3
+
+
+def tbe_row_bytes(fmt: int, D: int) -> int:
+    return int(_lib.load().dlrm_tbe_row_bytes(fmt, D))
+
+
+def tbe_forward_rows(weights: torch.Tensor, fmt: int, D: int, row_base: torch.Tensor, T: int,
+                     B: int, indices: torch.Tensor, offsets: torch.Tensor,
+                     per_sample_weights: Optional[torch.Tensor] = None,
+                     out: Optional[torch.Tensor] = None, out_batch_stride: Optional[int] = None,
+                     error_flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dlrm_tbe_forward_rows: table-batched pooled lookup over F16 rows ([rows, D] half) or
+    row-wise quantized rows ([rows, row_bytes] uint8, torch.ops.quantized prepack layout)."""
+    _check_cuda(weights, row_base, indices, offsets, per_sample_weights)
+    if fmt == ROWS_F16:
+        assert weights.dtype == torch.float16 and weights.shape[1] == D
+        row_bytes = 2 * weights.stride(0)
+    else:
+        assert weights.dtype == torch.uint8 and weights.dim() == 2
+        row_bytes = weights.stride(0)
+    if out is None:
+        out = torch.empty((B, T, D), dtype=torch.float32, device=weights.device)
+        out_batch_stride = T * D
+    elif out_batch_stride is None:
+        out_batch_stride = T * D
+    _lib.call("dlrm_tbe_forward_rows", _p(weights), fmt, row_bytes, D, _p(row_base), T, B,
+              _p(indices), _bits(indices), _p(offsets), _bits(offsets), _p(per_sample_weights),
+              _p(out), out_batch_stride, _p(error_flag), _stream(weights.device))
+    return out
+
+
 def tbe_backward_workspace_size(num_lookups: int, total_rows: int, D: int) -> int:
     return _lib.query("dlrm_tbe_backward_workspace_size", num_lookups, total_rows, D)
 

@@ -163,6 +163,37 @@ int dlrm_tbe_forward_presort(const float* weights, int64_t D, const int64_t* row
                              size_t workspace_bytes, int32_t* error_flag,
                              const dlrm_mlp_chain* bottom, dlrm_stream_t stream);
 
+/*
+ * Reduced-precision rows.  Row layouts, fixed row_bytes per buffer:
+ *   DLRM_ROWS_F16 : D fp16 (the fbgemm TBE's FP16 weights, dlrm_s_pytorch.py:337-366)
+ *   DLRM_ROWS_Q8  : D uint8, fp32 scale, fp32 bias (torch.ops.quantized
+ *                   .embedding_bag_byte_prepack, dlrm_s_pytorch.py:609-625)
+ *   DLRM_ROWS_Q4  : ceil(D/2) bytes (element 2i = low nibble of byte i), fp16 scale, fp16
+ *                   bias (embedding_bag_4bit_prepack)
+ * value = q * scale + bias.
+ */
+enum dlrm_rows_format {
+  DLRM_ROWS_F32 = 0,
+  DLRM_ROWS_F16 = 1,
+  DLRM_ROWS_Q8 = 2,
+  DLRM_ROWS_Q4 = 3
+};
+
+/* Minimum row size in bytes of a format at dimension D (-1 for an unknown format). */
+int64_t dlrm_tbe_row_bytes(int32_t format, int64_t D);
+
+/*
+ * dlrm_tbe_forward over F16 / Q8 / Q4 rows (embedding_bag_{byte,4bit}_rowwise_offsets
+ * semantics, dlrm_s_pytorch.py:554-567, table-batched like dlrm_tbe_forward): each bag
+ * sums fma(w*scale, q, acc + w*bias) in fp32.  weights: [total_rows][row_bytes] bytes;
+ * D % 4 == 0, D <= 512; rows 8- (F16), 4- (Q8) or 2-byte (Q4) aligned.
+ */
+int dlrm_tbe_forward_rows(const void* weights, int32_t format, int64_t row_bytes, int64_t D,
+                          const int64_t* row_base, int32_t T, int32_t B, const void* indices,
+                          int32_t index_bits, const void* offsets, int32_t offset_bits,
+                          const float* per_sample_weights, float* out, int64_t out_batch_stride,
+                          int32_t* error_flag, dlrm_stream_t stream);
+
 /* Workspace for the deterministic (sorted, segment-reduced) backward. */
 size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows, int64_t D);
 

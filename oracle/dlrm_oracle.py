@@ -21,7 +21,8 @@ __all__ = [
     "generate_uniform_input_batch", "generate_random_output_batch", "batched_csr",
     "distribute_batched", "init_emb_tables", "init_mlp", "embedding_bag_sum", "interact",
     "OracleDLRM", "QREmbeddingBagOracle", "RWSAdagradOracle", "distributed_step",
-    "criteo_transform", "KAGGLE_ROWS", "TERABYTE_ROWS",
+    "criteo_transform", "KAGGLE_ROWS", "TERABYTE_ROWS", "dequantize_rows",
+    "embedding_bag_rows",
 ]
 
 # tools/visualize.py:949 (Kaggle) and :964 (Terabyte) row counts; Terabyte capped at 1e7
@@ -173,6 +174,46 @@ def embedding_bag_sum(W: torch.Tensor, idx: torch.Tensor, off: torch.Tensor,
     """nn.EmbeddingBag(mode='sum') as DLRM_Net.apply_emb calls it (dlrm_s_pytorch.py:571-576):
     off = B bag starts, the last bag ends at len(idx)."""
     return F.embedding_bag(idx, W, off, mode="sum", per_sample_weights=psw)
+
+
+def dequantize_rows(packed: np.ndarray, bits: int, D: int) -> np.ndarray:
+    """Row-wise quantized rows -> fp32 [rows, D] (the layout of
+    torch.ops.quantized.embedding_bag_{byte,4bit}_prepack that DLRM_Net.quantize_embedding
+    uses, dlrm_s_pytorch.py:609-625): 8-bit = D uint8 | fp32 scale | fp32 bias; 4-bit =
+    ceil(D/2) bytes (element 2i = low nibble of byte i) | fp16 scale | fp16 bias.
+    Returns (q, scale, bias) with q as float levels."""
+    packed = np.ascontiguousarray(packed, dtype=np.uint8)
+    if bits == 8:
+        q = packed[:, :D].astype(np.float32)
+        sb = packed[:, D:D + 8].copy().view(np.float32)
+    else:
+        nb = (D + 1) // 2
+        by = packed[:, :nb]
+        q = np.empty((packed.shape[0], 2 * nb), dtype=np.float32)
+        q[:, 0::2] = by & 0xF
+        q[:, 1::2] = by >> 4
+        q = q[:, :D]
+        sb = packed[:, nb:nb + 4].copy().view(np.float16).astype(np.float32)
+    return q, sb[:, 0].copy(), sb[:, 1].copy()
+
+
+def embedding_bag_rows(packed: np.ndarray, bits: int, D: int, idx: np.ndarray,
+                       off: np.ndarray, psw: Optional[np.ndarray] = None) -> np.ndarray:
+    """embedding_bag_{byte,4bit}_rowwise_offsets (dlrm_s_pytorch.py:554-567) restated in
+    float32: per lookup, acc = fma(w*scale, q, acc + w*bias), in lookup order (off = B bag
+    starts; the last bag ends at len(idx)).  Within fp32 rounding of the torch op."""
+    q, sc, bi = dequantize_rows(packed, bits, D)
+    B = len(off)
+    out = np.zeros((B, D), dtype=np.float32)
+    ends = list(off[1:]) + [len(idx)]
+    for b in range(B):
+        acc = np.zeros(D, dtype=np.float32)
+        for l in range(int(off[b]), int(ends[b])):
+            r = int(idx[l])
+            w = np.float32(1.0 if psw is None else psw[l])
+            acc = (np.float32(w * sc[r]) * q[r] + (acc + np.float32(w * bi[r]))).astype(np.float32)
+        out[b] = acc
+    return out
 
 
 def interact(x: torch.Tensor, ly: Sequence[torch.Tensor], op: str = "dot",
