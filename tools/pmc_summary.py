@@ -12,8 +12,9 @@ import sys
 from collections import defaultdict
 
 GROUPS = [
-    ("gemm", ("gemm_f32_", "gemm_splitk_reduce_kernel")),
-    ("tbe_fwd", ("tbe_fwd_kernel",)),
+    ("gemm", ("gemm_group_kernel", "gemm_generic_kernel", "gemm_rowsum_kernel",
+              "gemm_f32_", "gemm_splitk_reduce_kernel")),
+    ("tbe_fwd", ("tbe_fwd_kernel", "tbe_fwd_presort_kernel")),  # presort: + sort + bottom MLP
     ("tbe_bwd", ("tbe_bwd_", "rocprim")),
     ("interaction", ("interact_",)),
     ("colsum", ("colsum_",)),
@@ -59,7 +60,8 @@ def main():
         out[g] = {"launches": n, "read_bytes_per_launch": round(per_launch_read),
                   "write_bytes_per_launch": round(per_launch_write),
                   "hbm_bytes_per_launch": round(per_launch_read + per_launch_write),
-                  "launches_per_step_approx": round(launches_per_step, 2)}
+                  "launches_per_step_approx": round(launches_per_step, 2),
+                  "hbm_bytes_per_step": round((2.0 * f[g][0] + w[g][0]) / steps)}
     print(json.dumps(out, indent=1))
 
 
