@@ -324,7 +324,48 @@ __global__ __launch_bounds__(kMlpWaves * 64) void mlp_chain_kernel(const MlpChai
   mlp_rows_body(mc, blockIdx.x, lds);
 }
 
-enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2 };
+// MODE_SGD_F16: exact SGD on fp16 weights (the fbgemm TBE's FP16 tables): the row is read
+// as fp16, updated in fp32 and stored back rounded to nearest even.
+enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2, MODE_SGD_F16 = 3 };
+
+// Weight-row element access by mode: fp32 rows, or fp16 rows (W then points at halves).
+template <int MODE, int VW>
+__device__ __forceinline__ typename VecT<VW>::T wload(const float* __restrict__ W, int64_t row,
+                                                      int64_t D, int chunk) {
+  if constexpr (MODE == MODE_SGD_F16) {
+    const _Float16* h = reinterpret_cast<const _Float16*>(W) + row * D + (int64_t)chunk * VW;
+    if constexpr (VW == 4) {
+      const uint2 u = *reinterpret_cast<const uint2*>(h);
+      return make_float4((float)__builtin_bit_cast(_Float16, (unsigned short)(u.x & 0xffff)),
+                         (float)__builtin_bit_cast(_Float16, (unsigned short)(u.x >> 16)),
+                         (float)__builtin_bit_cast(_Float16, (unsigned short)(u.y & 0xffff)),
+                         (float)__builtin_bit_cast(_Float16, (unsigned short)(u.y >> 16)));
+    } else {
+      return (float)h[0];
+    }
+  } else {
+    return reinterpret_cast<const typename VecT<VW>::T*>(W + row * D)[chunk];
+  }
+}
+
+template <int MODE, int VW>
+__device__ __forceinline__ void wstore(float* __restrict__ W, int64_t row, int64_t D, int chunk,
+                                       const typename VecT<VW>::T& v) {
+  if constexpr (MODE == MODE_SGD_F16) {
+    _Float16* h = reinterpret_cast<_Float16*>(W) + row * D + (int64_t)chunk * VW;
+    if constexpr (VW == 4) {
+      auto bits = [](float f) { return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)f); };
+      uint2 u;
+      u.x = bits(v.x) | (bits(v.y) << 16);
+      u.y = bits(v.z) | (bits(v.w) << 16);
+      *reinterpret_cast<uint2*>(h) = u;
+    } else {
+      h[0] = (_Float16)v;
+    }
+  } else {
+    reinterpret_cast<typename VecT<VW>::T*>(W + row * D)[chunk] = v;
+  }
+}
 
 // Apply the coalesced gradient g of one row (group-uniform control flow).
 template <int LPB, int VW, int MAXV, int MODE>
@@ -334,14 +375,14 @@ __device__ __forceinline__ void finalize_row(float* __restrict__ W, float* __res
                                              int nchunks, float lr, float eps) {
   using V = typename VecT<VW>::T;
   V* wrow = reinterpret_cast<V*>(W + row * D);
-  if (MODE == MODE_SGD) {
+  if (MODE == MODE_SGD || MODE == MODE_SGD_F16) {
 #pragma unroll
     for (int c = 0; c < MAXV; ++c) {
       const int chunk = gl + c * LPB;
       if (chunk < nchunks) {
-        V w = wrow[chunk];
+        V w = wload<MODE, VW>(W, row, D, chunk);
         vfma(w, -lr, g[c]);
-        wrow[chunk] = w;
+        wstore<MODE, VW>(W, row, D, chunk, w);
       }
     }
   } else if (MODE == MODE_DENSE) {
@@ -395,14 +436,14 @@ __device__ __forceinline__ void finalize_row_pf(float* __restrict__ W, float* __
                                                 int gl, int nchunks, float lr, float eps) {
   using V = typename VecT<VW>::T;
   V* wrow = reinterpret_cast<V*>(W + row * D);
-  if (MODE == MODE_SGD) {
+  if (MODE == MODE_SGD || MODE == MODE_SGD_F16) {
 #pragma unroll
     for (int c = 0; c < MAXV; ++c) {
       const int chunk = gl + c * LPB;
       if (chunk < nchunks) {
         V x = w[c];
         vfma(x, -lr, g[c]);
-        wrow[chunk] = x;
+        wstore<MODE, VW>(W, row, D, chunk, x);
       }
     }
   } else if (MODE == MODE_DENSE) {
@@ -563,12 +604,11 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
           if constexpr (PF) {
             // rows starting a run inside the chunk (repeats of one row load it once)
             const bool lead = (j + u < n) && ku[u] != sentinel && (u == 0 || ku[u] != ku[u - 1]);
-            const V* wrow = reinterpret_cast<const V*>(W + (int64_t)ku[u] * D);
 #pragma unroll
             for (int c = 0; c < MAXV; ++c) {
               const int chunk = gl + c * LPB;
               if (lead && chunk < nchunks)
-                wv[u][c] = wrow[chunk];
+                wv[u][c] = wload<MODE, VW>(W, (int64_t)ku[u], D, chunk);
               else
                 vzero(wv[u][c]);
             }
@@ -780,7 +820,8 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
                   name);
   }
 
-  const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
+  const bool vec4 = (D % 4 == 0) &&
+                    ((reinterpret_cast<uintptr_t>(W) & (mode == MODE_SGD_F16 ? 7 : 15)) == 0) &&
                     ((reinterpret_cast<uintptr_t>(gout) & 15) == 0) && (gbs % 4 == 0);
   const int64_t nchunks = vec4 ? D / 4 : D;
   int lpb = 1;
@@ -825,6 +866,8 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
     BY_LPB(VW, MODE_SGD)               \
   } else if (mode == MODE_ADAGRAD) {   \
     BY_LPB(VW, MODE_ADAGRAD)           \
+  } else if (mode == MODE_SGD_F16) {   \
+    BY_LPB(VW, MODE_SGD_F16)           \
   } else {                             \
     BY_LPB(VW, MODE_DENSE)             \
   }
@@ -898,6 +941,23 @@ extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* r
                       grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes,
                       max_lookups_per_table, error_flag, presorted, stream,
                       "dlrm_tbe_backward_sgd");
+}
+
+extern "C" int dlrm_tbe_backward_sgd_f16(void* weights, int64_t D, const int64_t* row_base,
+                                         int32_t T, int32_t B, const void* indices,
+                                         int32_t index_bits, const void* offsets,
+                                         int32_t offset_bits, int64_t num_lookups,
+                                         int64_t total_rows, const float* per_sample_weights,
+                                         const float* grad_out, int64_t grad_batch_stride,
+                                         float lr, int64_t max_lookups_per_table,
+                                         void* workspace, size_t workspace_bytes,
+                                         int32_t* error_flag, int32_t presorted,
+                                         dlrm_stream_t stream) {
+  return bwd_dispatch(MODE_SGD_F16, static_cast<float*>(weights), nullptr, D, row_base, T, B,
+                      indices, index_bits, offsets, offset_bits, num_lookups, total_rows,
+                      per_sample_weights, grad_out, grad_batch_stride, lr, 0.f, workspace,
+                      workspace_bytes, max_lookups_per_table, error_flag, presorted, stream,
+                      "dlrm_tbe_backward_sgd_f16");
 }
 
 extern "C" int dlrm_tbe_backward_rowwise_adagrad(

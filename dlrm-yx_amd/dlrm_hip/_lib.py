@@ -58,6 +58,9 @@ SIGNATURES = {
     "dlrm_tbe_backward_sgd": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32,
                                         c_int64, c_int64, P, P, c_int64, c_float, c_int64, P,
                                         c_size_t, P, c_int32, P]),
+    "dlrm_tbe_backward_sgd_f16": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P,
+                                            c_int32, c_int64, c_int64, P, P, c_int64, c_float,
+                                            c_int64, P, c_size_t, P, c_int32, P]),
     "dlrm_tbe_backward_rowwise_adagrad": (c_int32, [P, P, c_int64, P, c_int32, c_int32, P,
                                                     c_int32, P, c_int32, c_int64, c_int64, P, P,
                                                     c_int64, c_float, c_float, c_int64, P,

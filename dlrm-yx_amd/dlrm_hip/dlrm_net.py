@@ -17,7 +17,8 @@ device buffer and apply_emb is ONE table-batched launch; the MLPs are HipMLP
 
 Not on this path (documented in DESIGN.md): parallel_forward (single-process multi-GPU;
 the MI355X path is one process per GPU), mixed-dimension tables, learned per-sample
-weights.  4/8-bit quantized inference (quantize_embedding) runs on dlrm_tbe_forward_rows.
+weights.  4/8-bit quantized inference (quantize_embedding) and the fp16 fbgemm TBE
+(fbgemm_emb=True) run on dlrm_tbe_forward_rows / dlrm_tbe_backward_sgd_f16.
 """
 from __future__ import annotations
 
@@ -34,7 +35,8 @@ from . import extend_distributed as ext_dist
 from . import functional as HF
 from . import ops, sharders
 from .modules import (HipEmbeddingBagList, HipMLP, HipQREmbeddingBag, Optimizer,
-                      TableBatchedEmbeddingBags, make_embedding_list)
+                      SplitTableBatchedEmbeddingBags, TableBatchedEmbeddingBags,
+                      make_embedding_list)
 
 
 class DLRM_Net(nn.Module):
@@ -106,8 +108,21 @@ class DLRM_Net(nn.Module):
                                          stochastic_rounding=False, tables=tables), [None] * T
 
     def create_emb_fbgemm(self, Ds, Es, weighted_pooling=None):
-        raise NotImplementedError("the fbgemm fp16-weight TBE (--fbgemm-emb) is not on the "
-                                  "MI355X path yet; use --batched-emb")
+        """dlrm_s_pytorch.py:337-366: one FP16-weight TBE over the local tables with exact
+        SGD fused (modules.SplitTableBatchedEmbeddingBags; fbgemm's default learning rate
+        0.01, eps 0.01 as the reference passes it)."""
+        T = len(Es)
+        emb_indices = ([i for i in range(T) if i in self.local_emb_indices]
+                       if ext_dist.my_size > 1 else list(range(T)))
+        if not self.load_processed:
+            Ds = [Ds] * T
+        rng = np.random.RandomState(torch.initial_seed() % (2 ** 32))
+        tables = [rng.uniform(low=-np.sqrt(1 / Es[i]), high=np.sqrt(1 / Es[i]),
+                              size=(int(Es[i]), int(Ds[i]))).astype(np.float32)
+                  for i in emb_indices]
+        return SplitTableBatchedEmbeddingBags([(int(Es[i]), int(Ds[i])) for i in emb_indices],
+                                              learning_rate=0.01, eps=0.01,
+                                              tables=tables), [None] * T
 
     def __init__(self, m_spa=None, ln_emb=None, ln_bot=None, ln_top=None,
                  arch_interaction_op=None, arch_interaction_itself=False, sigmoid_bot=-1,
@@ -290,7 +305,11 @@ class DLRM_Net(nn.Module):
         return [emb(lS_i[0], lS_o[0])]
 
     def apply_emb_fbgemm(self, lS_o, lS_i, device_ids=None):
-        raise NotImplementedError("--fbgemm-emb is not on the MI355X path yet")
+        """dlrm_s_pytorch.py:593-598: [B, T*D] from the fp16 TBE, viewed as [B, T, D]."""
+        emb = self.emb_l[0] if isinstance(self.emb_l, nn.ModuleList) else self.emb_l
+        y = emb(lS_i[0], lS_o[0])
+        B = y.shape[0]
+        return [y.reshape(B, -1, int(self.ln_bot[-1]))]
 
     def interact_features(self, x, ly):
         """dlrm_s_pytorch.py:627-665 on the MFMA interaction kernel."""
@@ -326,9 +345,12 @@ class DLRM_Net(nn.Module):
                              "-".join(str(s) for s in table_sizes)):
             if self.batched_emb:
                 ly = self.apply_emb_batched(lS_o, lS_i)
+            elif self.fbgemm_emb:
+                ly = self.apply_emb_fbgemm(lS_o, lS_i)
             else:
                 ly = self.apply_emb(lS_o, lS_i)
-            a2a_req = ext_dist.alltoall(ly, self.n_emb_per_rank, self.batched_emb)
+            a2a_req = ext_dist.alltoall(ly, self.n_emb_per_rank,
+                                        self.batched_emb or self.fbgemm_emb)
         with record_function("module::forward_pass::bottom_mlp"):
             x = self.apply_mlp(dense_x, self.bot_l)
             ly = list(a2a_req.wait())
@@ -345,6 +367,8 @@ class DLRM_Net(nn.Module):
         with record_function("module::forward_pass::embedding_lookup"):
             if self.batched_emb:
                 ly = self.apply_emb_batched([lS_o], [lS_i])
+            elif self.fbgemm_emb:
+                ly = self.apply_emb_fbgemm([lS_o], [lS_i])
             else:
                 ly = self.apply_emb(lS_o, lS_i)
         with record_function("module::forward_pass::interaction"):

@@ -138,8 +138,14 @@ class EmbeddingBagsFunction(torch.autograd.Function):
     def forward(ctx, module, counts, indices, offsets, per_sample_weights, *table_params):
         B = (offsets.numel() - 1) // module.T
         flag = _error_flag(module, indices.device)
-        out = ops.tbe_forward(module.weight_flat, module.row_base, module.T, B, indices, offsets,
-                              per_sample_weights=per_sample_weights, error_flag=flag)
+        fmt = getattr(module, "row_format", ops.ROWS_F32)
+        if fmt == ops.ROWS_F32:
+            out = ops.tbe_forward(module.weight_flat, module.row_base, module.T, B, indices,
+                                  offsets, per_sample_weights=per_sample_weights, error_flag=flag)
+        else:  # fp16 / quantized rows
+            out = ops.tbe_forward_rows(module.weight_flat, fmt, module.D, module.row_base,
+                                       module.T, B, indices, offsets,
+                                       per_sample_weights=per_sample_weights, error_flag=flag)
         if getattr(module, "strict_indices", True):
             # nn.EmbeddingBag raises IndexError on an out-of-range index; the kernel skips
             # and flags it, and this reads the flag (one sync, like the driver's per-step

@@ -184,6 +184,73 @@ class TableBatchedEmbeddingBags(nn.Module):
                                            self.weights)
 
 
+class SplitTableBatchedEmbeddingBags(nn.Module):
+    """FP16-weight table-batched EmbeddingBag with exact SGD fused into the backward: the
+    module DLRM_Net.create_emb_fbgemm builds (fbgemm_gpu's
+    SplitTableBatchedEmbeddingBagsCodegen with weights_precision=FP16, OptimType.EXACT_SGD,
+    dlrm_s_pytorch.py:337-366) and apply_emb_fbgemm calls (:593-598):
+    module(indices, offsets[T*B+1], per_sample_weights=None) -> [B, T*D] fp32.
+
+    Forward: dlrm_tbe_forward_rows (F16 rows, fp32 accumulation).  Backward:
+    dlrm_tbe_backward_sgd_f16 (deterministic per-row fp32 gradient sum, round-to-nearest
+    fp16 store).  fbgemm_gpu itself is not in the reference tree, so its init bound, its
+    LFU cache and its stochastic rounding are not reproduced (parity unpinned against it);
+    tables are drawn U(+-sqrt(1/n)) like the other DLRM paths."""
+
+    def __init__(self, embedding_specs, learning_rate: float = 0.01, eps: float = 1.0e-8,
+                 tables=None, seed: int = 0, device=None, **unused):
+        super().__init__()
+        Es = [int(e) for e, *_ in embedding_specs]
+        Ds = {int(d) for _, d, *_ in embedding_specs}
+        if len(Ds) != 1:
+            raise NotImplementedError("mixed embedding dims in one fp16 TBE")
+        self.T = len(Es)
+        self.D = Ds.pop()
+        self.learning_rate = float(learning_rate)
+        self.eps = float(eps)
+        self.row_format = ops.ROWS_F16
+        total = int(sum(Es))
+        w = torch.empty(total, self.D)
+        self.row_ranges = []
+        o = 0
+        g = torch.Generator().manual_seed(seed)
+        for t, n in enumerate(Es):
+            if tables is not None:
+                w[o:o + n] = torch.as_tensor(tables[t])
+            else:
+                a = float(np.sqrt(1.0 / n))
+                w[o:o + n].uniform_(-a, a, generator=g)
+            self.row_ranges.append((o, o + n))
+            o += n
+        self.weights = Parameter(w.half(), requires_grad=True)
+        self.register_buffer("table_offsets", torch.tensor([0] + [b for _, b in self.row_ranges],
+                                                           dtype=torch.int64))
+        self.grad_mode = "fused"
+        if device is not None:
+            self.to(device)
+
+    @property
+    def weight_flat(self):
+        return self.weights.data
+
+    @property
+    def row_base(self):
+        return self.table_offsets
+
+    def fused_update(self, indices, offsets, grad, psw, B):
+        ops.tbe_backward("sgd", self.weights.data, self.table_offsets, self.T, B, indices,
+                         offsets, grad, lr=self.learning_rate, per_sample_weights=psw)
+
+    def split_embedding_weights(self) -> List[torch.Tensor]:
+        return [self.weights.data[a:b] for a, b in self.row_ranges]
+
+    def forward(self, indices, offsets, per_sample_weights=None):
+        B = (offsets.numel() - 1) // self.T
+        out = EmbeddingBagsFunction.apply(self, None, indices, offsets, per_sample_weights,
+                                          self.weights)
+        return out.reshape(B, self.T * self.D)
+
+
 class _SingleTable:
     """EmbeddingBagsFunction adapter for one standalone weight matrix."""
 

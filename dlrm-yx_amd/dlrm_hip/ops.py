@@ -201,8 +201,8 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
                  workspace: Optional[torch.Tensor] = None,
                  max_lookups_per_table: int = 0,
                  error_flag: Optional[torch.Tensor] = None, presorted: bool = False) -> None:
-    """mode: 'sgd' (fused exact SGD), 'rowwise_adagrad' (fused RWSAdagrad) or
-    'dense' (weights is a gradient buffer to accumulate into).  max_lookups_per_table:
+    """mode: 'sgd' (fused exact SGD; fp32 or fp16 weights), 'rowwise_adagrad' (fused
+    RWSAdagrad) or 'dense' (weights is a gradient buffer to accumulate into).  max_lookups_per_table:
     upper bound on any table's lookups (0 = unknown); <= 4096 selects the per-table LDS
     sort (bitwise the same result as the device-wide radix sort).  ``error_flag``: device
     int32 that receives TBE_ERR_INDEX / TBE_ERR_TABLE_CAP bits (see check_tbe_errors)."""
@@ -220,7 +220,10 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
                    grad_batch_stride)
     st = _stream(weights.device)
     mx = int(max_lookups_per_table)
-    if mode == "sgd":
+    if mode == "sgd" and weights.dtype == torch.float16:
+        _lib.call("dlrm_tbe_backward_sgd_f16", _p(weights), *args_common, lr, mx,
+                  _p(workspace), workspace.numel(), _p(error_flag), int(presorted), st)
+    elif mode == "sgd":
         _lib.call("dlrm_tbe_backward_sgd", _p(weights), *args_common, lr, mx, _p(workspace),
                   workspace.numel(), _p(error_flag), int(presorted), st)
     elif mode == "rowwise_adagrad":

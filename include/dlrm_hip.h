@@ -226,6 +226,21 @@ int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, in
                           dlrm_stream_t stream);
 
 /*
+ * dlrm_tbe_backward_sgd on fp16 weights (DLRM_ROWS_F16 tables: the fbgemm TBE's FP16
+ * weights with EXACT_SGD, dlrm_s_pytorch.py:337-366): the gradient of each unique row is
+ * summed in fp32 in the same fixed order, w = float(w_fp16) - lr * g is rounded to nearest
+ * even on the store (fbgemm's optional stochastic rounding is not reproduced).
+ */
+int dlrm_tbe_backward_sgd_f16(void* weights, int64_t D, const int64_t* row_base, int32_t T,
+                              int32_t B, const void* indices, int32_t index_bits,
+                              const void* offsets, int32_t offset_bits, int64_t num_lookups,
+                              int64_t total_rows, const float* per_sample_weights,
+                              const float* grad_out, int64_t grad_batch_stride, float lr,
+                              int64_t max_lookups_per_table, void* workspace,
+                              size_t workspace_bytes, int32_t* error_flag, int32_t presorted,
+                              dlrm_stream_t stream);
+
+/*
  * Row-wise sparse Adagrad (RWSAdagrad, optim/rwsadagrad.py:92-115) fused into the
  * backward: per unique row r with coalesced gradient g_r (sum over its lookups),
  *   momentum[r] += mean_d(g_r[d]^2);  W[r] -= lr * g_r / (sqrt(momentum[r]) + eps)

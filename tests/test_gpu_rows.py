@@ -115,3 +115,75 @@ def test_dlrm_net_quantize_embedding(ops, bits):
     x = torch.rand(B, 5)
     p = net(x.to(dev), lS_o, lS_i)
     assert p.shape == (B, 1) and torch.isfinite(p).all()
+
+
+@pytest.mark.parametrize("mx_kind", ["cap", "none"])
+def test_tbe_backward_sgd_f16(ops, mx_kind):
+    """Exact SGD on fp16 rows: per-row gradient summed in fp32 (sorted, deterministic),
+    w = float(w16) - lr * g rounded to nearest fp16.  Reference: the same update in fp64
+    from the same half weights, rounded to fp16 -> equal within one fp16 ulp; skewed tables
+    exercise runs crossing blocks; bitwise reproducible run to run."""
+    torch.manual_seed(9)
+    rows, D, B, L = [3, 5000, 4, 700], 128, 512, 2
+    T = len(rows)
+    lo = [torch.arange(B) * L for _ in rows]
+    li = [torch.randint(0, n, (B * L,)) for n in rows]
+    off, idx = O.batched_csr(lo, li)
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    G = torch.randn(B, T, D, device=dev)
+    W0 = (torch.randn(sum(rows), D) * 0.5).half().to(dev)
+    mx = B * L if mx_kind == "cap" else 0
+    outs = []
+    for _ in range(2):
+        W = W0.clone()
+        ops.tbe_backward("sgd", W, row_base, T, B, idx.to(dev), off.to(dev), G, lr=0.05,
+                         max_lookups_per_table=mx)
+        outs.append(W.cpu())
+    assert torch.equal(outs[0], outs[1])
+    gsum = torch.zeros(sum(rows), D, dtype=torch.float64)
+    gt = G.cpu().double()
+    bag = torch.arange(B * L) // L
+    for t in range(T):
+        gsum.index_add_(0, int(row_base[t]) + li[t], gt[bag, t])
+    ref = (W0.cpu().double() - 0.05 * gsum).half()
+    got = outs[0]
+    ulp = torch.clamp(ref.float().abs(), min=2.0 ** -14) * 2.0 ** -10
+    assert torch.all((got.float() - ref.float()).abs() <= ulp * 1.01)
+    assert (got != W0.cpu()).any()
+
+
+def test_dlrm_net_fbgemm_fp16_path(ops):
+    """DLRM_Net(fbgemm_emb=True): the fp16 TBE module's lookup equals fp32 math on its half
+    weights, and a backward step applies exact SGD (lr 0.01) to the fp16 rows."""
+    from dlrm_hip.dlrm_net import DLRM_Net
+    np.random.seed(4)
+    torch.manual_seed(4)
+    ln_emb = np.array([60, 9, 400])
+    T, D, B = len(ln_emb), 16, 10
+    net = DLRM_Net(m_spa=D, ln_emb=ln_emb, ln_bot=np.array([5, D]),
+                   ln_top=np.array([D + T * (T + 1) // 2, 8, 1]), arch_interaction_op="dot",
+                   fbgemm_emb=True).to(dev)
+    emb = net.emb_l
+    assert emb.weights.dtype == torch.float16
+    lS_o = torch.arange(0, T * B * 2 + 1, 2, dtype=torch.int32)
+    lS_i = torch.cat([torch.randint(0, int(n), (B * 2,)) for n in ln_emb]).int()
+    W0 = emb.weights.detach().clone()
+    y = net.apply_emb_fbgemm([lS_o.to(dev)], [lS_i.to(dev)])[0]
+    Wf = W0.float().cpu()
+    rb = [0] + np.cumsum(ln_emb).tolist()
+    for t in range(T):
+        idx = lS_i[t * B * 2:(t + 1) * B * 2].long() + rb[t]
+        ref = Wf[idx].view(B, 2, D).sum(1)
+        ok, msg = fp32_close(y[:, t].detach().cpu().numpy(), ref.numpy())
+        assert ok, msg
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    torch.cuda.synchronize()
+    W1 = emb.weights.detach().cpu()
+    gsum = torch.zeros(Wf.shape, dtype=torch.float64)
+    for t in range(T):
+        idx = lS_i[t * B * 2:(t + 1) * B * 2].long() + rb[t]
+        gsum.index_add_(0, idx, g[:, t].cpu().double().repeat_interleave(2, 0))
+    ref = (Wf.double() - 0.01 * gsum).half()
+    ulp = torch.clamp(ref.float().abs(), min=2.0 ** -14) * 2.0 ** -10
+    assert torch.all((W1.float() - ref.float()).abs() <= ulp * 1.01)
