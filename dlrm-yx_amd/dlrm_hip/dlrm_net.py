@@ -16,8 +16,8 @@ device buffer and apply_emb is ONE table-batched launch; the MLPs are HipMLP
 (one fused Function per MLP); the interaction is the MFMA kernel.
 
 Not on this path (documented in DESIGN.md): parallel_forward (single-process multi-GPU;
-the MI355X path is one process per GPU), mixed-dimension tables, learned per-sample
-weights.  4/8-bit quantized inference (quantize_embedding) and the fp16 fbgemm TBE
+the MI355X path is one process per GPU), learned per-sample weights.  Mixed-dimension
+tables (md_flag) are HipPrEmbeddingBag (lookup + bias-free projection GEMM).  4/8-bit quantized inference (quantize_embedding) and the fp16 fbgemm TBE
 (fbgemm_emb=True) run on dlrm_tbe_forward_rows / dlrm_tbe_backward_sgd_f16.
 """
 from __future__ import annotations
@@ -34,8 +34,8 @@ from torch.nn.parameter import Parameter
 from . import extend_distributed as ext_dist
 from . import functional as HF
 from . import ops, sharders
-from .modules import (HipEmbeddingBagList, HipMLP, HipQREmbeddingBag, Optimizer,
-                      SplitTableBatchedEmbeddingBags, TableBatchedEmbeddingBags,
+from .modules import (HipEmbeddingBagList, HipMLP, HipPrEmbeddingBag, HipQREmbeddingBag,
+                      Optimizer, SplitTableBatchedEmbeddingBags, TableBatchedEmbeddingBags,
                       make_embedding_list)
 
 
@@ -66,24 +66,39 @@ class DLRM_Net(nn.Module):
                 continue
             local.append(i)
         ln_local = [int(ln[i]) for i in local]
+        # with --md-flag, lm is md_solver's per-table dim list (dlrm_s_pytorch.py:1510-1516)
+        md_dims = list(lm) if np.ndim(lm) > 0 else None
+        base = int(max(md_dims)) if md_dims is not None else int(lm)
         for j, n in enumerate(ln_local):
             if self.load_processed:
                 raise NotImplementedError("--load-processed per-table dims (mixed D) are not on "
                                           "the MI355X path yet")
-            m = lm
+            m = base
             if self.qr_flag and n > self.qr_threshold:
                 extra[j] = HipQREmbeddingBag(n, m, self.qr_collisions,
                                              operation=self.qr_operation, mode="sum",
                                              sparse=True)
                 tables.append(None)
             elif self.md_flag and n > self.md_threshold:
-                raise NotImplementedError("mixed-dimension embeddings (--md-flag) are not on "
-                                          "the MI355X path yet")
+                # :291-299: PrEmbeddingBag(n, m[i], max(m)), rows re-drawn from numpy
+                _m = int(md_dims[local[j]])
+                EE = HipPrEmbeddingBag(n, _m, base)
+                W = np.random.uniform(low=-np.sqrt(1 / n), high=np.sqrt(1 / n),
+                                      size=(n, _m)).astype(np.float32)
+                EE.embs.weight.data = torch.tensor(W)
+                extra[j] = EE
+                tables.append(None)
             else:
+                # (under --md-flag the reference builds nn.EmbeddingBag(n, <dim list>) here
+                # and fails; small tables get the base dim instead)
+                if self.md_flag:
+                    # nn.EmbeddingBag's own init draws from the torch RNG before the numpy
+                    # overwrite; keep that stream aligned for the projections drawn later
+                    torch.empty(n, m).normal_()
                 W = np.random.uniform(low=-np.sqrt(1 / n), high=np.sqrt(1 / n),
                                       size=(n, m)).astype(np.float32)
                 tables.append(W)
-        emb_l = make_embedding_list(ln_local, lm, tables, extra, sparse=True)
+        emb_l = make_embedding_list(ln_local, base, tables, extra, sparse=True)
         if weighted_pooling is None:
             v_W_l = [None] * len(ln_local)
         else:
@@ -287,9 +302,11 @@ class DLRM_Net(nn.Module):
             for j, t in enumerate(plain):
                 ly[t] = out[:, j, :]
         for k in range(T):
-            if ly[k] is None:
-                psw = None if self.v_W_l[k] is None else self.v_W_l[k].gather(0, idxs[k])
-                ly[k] = emb_l[k](idxs[k], offs[k], per_sample_weights=psw)
+            if ly[k] is None:  # QR / mixed-dim tables: their own module, on its device
+                dk = next(emb_l[k].parameters()).device
+                ik, ok_ = idxs[k].to(dk), offs[k].to(dk)
+                psw = None if self.v_W_l[k] is None else self.v_W_l[k].to(dk).gather(0, ik)
+                ly[k] = emb_l[k](ik, ok_, per_sample_weights=psw)
         d = int(self.ln_bot[-1])
         out_l = []
         for y in ly:

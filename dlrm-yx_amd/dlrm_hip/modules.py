@@ -325,6 +325,39 @@ class HipQREmbeddingBag(nn.Module):
         return QRCombine.apply(self.operation, eq, er)
 
 
+class HipPrEmbeddingBag(nn.Module):
+    """PrEmbeddingBag (tricks/md_embedding_bag.py:61-85): a table of dim embedding_dim
+    pooled by the TBE kernel, then projected to base_dim by a bias-free Linear on the GEMM
+    kernel (identity when the dims are equal).  The constructor builds the same torch
+    modules in the same order as the reference (nn.EmbeddingBag, xavier_uniform_,
+    nn.Linear, xavier_uniform_), so the torch RNG stream and the projection init match
+    it under a seed; state_dict keys are the reference's (embs.weight, proj.weight)."""
+
+    def __init__(self, num_embeddings, embedding_dim, base_dim):
+        super().__init__()
+        ref = nn.EmbeddingBag(num_embeddings, embedding_dim, mode="sum", sparse=True)
+        nn.init.xavier_uniform_(ref.weight)
+        self.embs = HipEmbeddingBag(num_embeddings, embedding_dim, ref.weight.data.clone(),
+                                    sparse=True)
+        self.base_dim = int(base_dim)
+        if embedding_dim < base_dim:
+            self.proj = nn.Linear(embedding_dim, base_dim, bias=False)
+            nn.init.xavier_uniform_(self.proj.weight)
+        elif embedding_dim == base_dim:
+            self.proj = nn.Identity()
+        else:
+            raise ValueError("Embedding dim " + str(embedding_dim) + " > base dim " +
+                             str(base_dim))
+
+    def forward(self, input, offsets=None, per_sample_weights=None):
+        y = single_table_lookup(self.embs.weight, input, offsets, per_sample_weights,
+                                self.embs.sparse)
+        if isinstance(self.proj, nn.Identity):
+            return y
+        zero_bias = torch.zeros(self.base_dim, dtype=y.dtype, device=y.device)
+        return MLPFunction.apply(y, ("none",), self.proj.weight, zero_bias)
+
+
 # ------------------------------------------------------------------- MLP ----
 class HipMLP(nn.Sequential):
     """The nn.Sequential[Linear, ReLU|Sigmoid]* built by create_mlp; forward runs all layers

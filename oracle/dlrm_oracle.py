@@ -22,7 +22,7 @@ __all__ = [
     "distribute_batched", "init_emb_tables", "init_mlp", "embedding_bag_sum", "interact",
     "OracleDLRM", "QREmbeddingBagOracle", "RWSAdagradOracle", "distributed_step",
     "criteo_transform", "KAGGLE_ROWS", "TERABYTE_ROWS", "dequantize_rows",
-    "embedding_bag_rows",
+    "embedding_bag_rows", "md_solver", "pr_embedding_bag",
 ]
 
 # tools/visualize.py:949 (Kaggle) and :964 (Terabyte) row counts; Terabyte capped at 1e7
@@ -214,6 +214,45 @@ def embedding_bag_rows(packed: np.ndarray, bits: int, D: int, idx: np.ndarray,
             acc = (np.float32(w * sc[r]) * q[r] + (acc + np.float32(w * bi[r]))).astype(np.float32)
         out[b] = acc
     return out
+
+
+def md_solver(n: Sequence[int], alpha: float, d0: Optional[float] = None,
+              B: Optional[float] = None, round_dim: bool = True, k=None) -> List[int]:
+    """tricks/md_embedding_bag.py:20-60 (md_solver + alpha_power_rule + pow_2_round):
+    per-table dims d_i = lambda * (n_i / k_i)^(-alpha), the smallest table (after a stable
+    ascending sort) pinned to d0, others clamped at 1, rounded, optionally to a power of 2."""
+    n_t = torch.tensor(list(n))
+    ns, idx = torch.sort(n_t)
+    kk = torch.as_tensor(k)[idx] if k is not None else torch.ones(len(ns))
+    x = ns.type(torch.float) / kk
+    if d0 is not None:
+        lamb = d0 * (x[0].type(torch.float) ** alpha)
+    elif B is not None:
+        lamb = B / torch.sum(x.type(torch.float) ** (1 - alpha))
+    else:
+        raise ValueError("Must specify either d0 or B")
+    d = torch.ones(len(x)) * lamb * (x.type(torch.float) ** (-alpha))
+    for i in range(len(d)):
+        if i == 0 and d0 is not None:
+            d[i] = d0
+        else:
+            d[i] = 1 if d[i] < 1 else d[i]
+    d = torch.round(d).type(torch.long)
+    if round_dim:
+        d = 2 ** torch.round(torch.log2(d.type(torch.float)))
+    undo = [0] * len(idx)
+    for i, v in enumerate(idx):
+        undo[v] = i
+    return [int(v) for v in d[undo].tolist()]
+
+
+def pr_embedding_bag(W: torch.Tensor, P: Optional[torch.Tensor], idx: torch.Tensor,
+                     off: torch.Tensor, psw: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """PrEmbeddingBag.forward (tricks/md_embedding_bag.py:81-85): sum pooling of the
+    dim-m_i table, then the bias-free projection to the base dim (P [base, m_i], or None
+    for the identity)."""
+    y = F.embedding_bag(idx, W, off, mode="sum", per_sample_weights=psw)
+    return y if P is None else y @ P.t()
 
 
 def interact(x: torch.Tensor, ly: Sequence[torch.Tensor], op: str = "dot",
