@@ -65,6 +65,47 @@ __global__ __launch_bounds__(256) void tbe_expand_grad_kernel(int64_t D, int T, 
   }
 }
 
+// ------------------------------------------- per-sample-weight gradient ----
+// d loss / d w_l = <grad_out[bag(l)], W[row_base[t] + indices[l]]> for every lookup l (the
+// gradient the reference's learned weighted pooling receives through
+// per_sample_weights, dlrm_s_pytorch.py:475-478, 544-545).  One wave per lookup, lanes
+// sweep D, a fixed-order wave reduction: deterministic.  Lookups outside every bag or with
+// an out-of-range index get 0.
+template <typename IdxT, typename OffT>
+__global__ __launch_bounds__(256) void tbe_psw_grad_kernel(
+    const float* __restrict__ W, int64_t D, const int64_t* __restrict__ row_base, int T, int B,
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, int64_t N,
+    const float* __restrict__ gout, int64_t gbs, float* __restrict__ gpsw) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t nb = (int64_t)T * B;
+  for (int64_t p = wave; p < N; p += nw) {
+    float s = 0.f;
+    if (p >= (int64_t)off[0] && p < (int64_t)off[nb]) {
+      int64_t lo = 0, hi = nb;
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)off[mid] <= p)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      const int t = (int)(lo / B);
+      const int b = (int)(lo - (int64_t)t * B);
+      const int64_t r = (int64_t)idx[p];
+      if (r >= 0 && r < row_base[t + 1] - row_base[t]) {
+        const float* wrow = W + (row_base[t] + r) * D;
+        const float* grow = gout + (int64_t)b * gbs + (int64_t)t * D;
+        for (int64_t d = lane; d < D; d += 64) s = fmaf(wrow[d], grow[d], s);
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if (lane == 0) gpsw[p] = s;
+  }
+}
+
 // ------------------------------------------------------------------- QR ----
 template <typename IdxT>
 __global__ __launch_bounds__(256) void qr_split_kernel(const IdxT* __restrict__ idx, int64_t n,
@@ -312,6 +353,36 @@ extern "C" int dlrm_tbe_expand_grad(int64_t D, int32_t T, int32_t B, const void*
     hipLaunchKernelGGL(tbe_expand_grad_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, D, T, B,
                        static_cast<const int64_t*>(offsets), num_lookups, per_sample_weights,
                        grad_out, grad_batch_stride, values);
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_tbe_psw_grad(const float* weights, int64_t D, const int64_t* row_base,
+                                 int32_t T, int32_t B, const void* indices, int32_t index_bits,
+                                 const void* offsets, int32_t offset_bits, int64_t num_lookups,
+                                 const float* grad_out, int64_t grad_batch_stride,
+                                 float* grad_per_sample_weights, dlrm_stream_t stream) {
+  const char* name = "dlrm_tbe_psw_grad";
+  DLRM_ARG(D > 0 && T > 0 && B > 0 && num_lookups >= 0, "%s: bad sizes", name);
+  if (num_lookups == 0) return DLRM_OK;
+  DLRM_ARG(weights && row_base && indices && offsets && grad_out && grad_per_sample_weights,
+           "%s: null pointer", name);
+  DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: bad index_bits", name);
+  DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: bad offset_bits", name);
+  DLRM_ARG(grad_batch_stride >= (int64_t)T * D, "%s: grad_batch_stride < T*D", name);
+  int64_t blocks = dlrm::ceil_div(num_lookups, 4);
+  if (blocks > 16384) blocks = 16384;
+  hipStream_t st = dlrm::as_stream(stream);
+#define PG(I, O)                                                                             \
+  hipLaunchKernelGGL((tbe_psw_grad_kernel<I, O>), dim3(blocks), dim3(256), 0, st, weights, D, \
+                     row_base, T, B, static_cast<const I*>(indices),                          \
+                     static_cast<const O*>(offsets), num_lookups, grad_out, grad_batch_stride, \
+                     grad_per_sample_weights)
+  if (index_bits == 32 && offset_bits == 32) PG(int32_t, int32_t);
+  else if (index_bits == 32) PG(int32_t, int64_t);
+  else if (offset_bits == 32) PG(int64_t, int32_t);
+  else PG(int64_t, int64_t);
+#undef PG
   DLRM_LAUNCH_CHECK(name);
   return DLRM_OK;
 }

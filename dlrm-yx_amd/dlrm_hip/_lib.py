@@ -73,6 +73,8 @@ SIGNATURES = {
                                            c_size_t, P, P, P]),
     "dlrm_mlp_chain_supported": (c_int32, [P]),
     "dlrm_tbe_row_bytes": (c_int64, [c_int32, c_int64]),
+    "dlrm_tbe_psw_grad": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32,
+                                    c_int64, P, c_int64, P, P]),
     "dlrm_tbe_forward_rows": (c_int32, [P, c_int32, c_int64, c_int64, P, c_int32, c_int32, P,
                                         c_int32, P, c_int32, P, P, c_int64, P, P]),
     "dlrm_mlp_chain_forward": (c_int32, [P, P]),

@@ -16,8 +16,9 @@ device buffer and apply_emb is ONE table-batched launch; the MLPs are HipMLP
 (one fused Function per MLP); the interaction is the MFMA kernel.
 
 Not on this path (documented in DESIGN.md): parallel_forward (single-process multi-GPU;
-the MI355X path is one process per GPU), learned per-sample weights.  Mixed-dimension
-tables (md_flag) are HipPrEmbeddingBag (lookup + bias-free projection GEMM).  4/8-bit quantized inference (quantize_embedding) and the fp16 fbgemm TBE
+the MI355X path is one process per GPU) and --load-processed per-table dims.
+Mixed-dimension tables (md_flag) are HipPrEmbeddingBag (lookup + bias-free projection
+GEMM); learned weighted pooling trains v_W_l through dlrm_tbe_psw_grad.  4/8-bit quantized inference (quantize_embedding) and the fp16 fbgemm TBE
 (fbgemm_emb=True) run on dlrm_tbe_forward_rows / dlrm_tbe_backward_sgd_f16.
 """
 from __future__ import annotations
@@ -205,9 +206,13 @@ class DLRM_Net(nn.Module):
             else:
                 self.emb_l, w_list = self.create_emb(m_spa, self.ln_emb, weighted_pooling)
             if self.weighted_pooling == "learned":
-                raise NotImplementedError("learned per-sample weights are not on the MI355X "
-                                          "path yet (use weighted_pooling='fixed')")
-            self.v_W_l = w_list
+                # :475-478: one trainable weight per row; its gradient comes from the lookup
+                # backward (dlrm_tbe_psw_grad) through the per-sample-weight gather
+                self.v_W_l = nn.ParameterList()
+                for w in w_list:
+                    self.v_W_l.append(Parameter(w))
+            else:
+                self.v_W_l = w_list
         else:
             raise NotImplementedError("single-process multi-GPU (parallel_forward) is replaced "
                                       "by one process per GPU (distributed_forward)")

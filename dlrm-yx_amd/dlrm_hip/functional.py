@@ -163,16 +163,21 @@ class EmbeddingBagsFunction(torch.autograd.Function):
         B = ctx.B
         g = gout.contiguous()
         nones = [None] * ctx.n_params
+        # learned weighted pooling: the per-sample weights' own gradient, from the weights
+        # as they were in the forward (before a fused update below changes them)
+        gpsw = None
+        if psw is not None and ctx.needs_input_grad[4]:
+            gpsw = ops.tbe_psw_grad(m.weight_flat, m.row_base, m.T, B, indices, offsets, g)
         if m.grad_mode == "fused":
             m.fused_update(indices, offsets, g, psw, B)
-            return (None, None, None, None, None, *nones)
+            return (None, None, None, None, gpsw, *nones)
         mx = max(ctx.counts) if ctx.counts else 0
         if m.grad_mode == "dense":
             gw = torch.zeros_like(m.weight_flat)
             ops.tbe_backward("dense", gw, m.row_base, m.T, B, indices, offsets, g,
                              per_sample_weights=psw, max_lookups_per_table=mx)
             grads = [gw[a:b] for a, b in m.row_ranges]
-            return (None, None, None, None, None, *grads)
+            return (None, None, None, None, gpsw, *grads)
         # sparse COO per table
         vals = ops.tbe_expand_grad(m.D, m.T, B, offsets, indices.numel(), g,
                                    per_sample_weights=psw)
@@ -187,4 +192,4 @@ class EmbeddingBagsFunction(torch.autograd.Function):
             idx_t = indices[o:o + c].to(torch.int64).view(1, -1)
             grads.append(torch.sparse_coo_tensor(idx_t, vals[o:o + c], (b - a, m.D)))
             o += c
-        return (None, None, None, None, None, *grads)
+        return (None, None, None, None, gpsw, *grads)

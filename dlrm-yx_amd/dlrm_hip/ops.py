@@ -157,6 +157,21 @@ def tbe_forward_presort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B
     return out
 
 
+def tbe_psw_grad(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
+                 indices: torch.Tensor, offsets: torch.Tensor, grad_out: torch.Tensor,
+                 grad_batch_stride: Optional[int] = None) -> torch.Tensor:
+    """d loss / d per_sample_weights of a weighted lookup (dlrm_tbe_psw_grad)."""
+    _check_cuda(weights, row_base, indices, offsets, grad_out)
+    D = weights.shape[1]
+    if grad_batch_stride is None:
+        grad_batch_stride = T * D
+    g = torch.empty(indices.numel(), dtype=torch.float32, device=weights.device)
+    _lib.call("dlrm_tbe_psw_grad", _p(weights), D, _p(row_base), T, B, _p(indices),
+              _bits(indices), _p(offsets), _bits(offsets), indices.numel(), _p(grad_out),
+              grad_batch_stride, _p(g), _stream(weights.device))
+    return g
+
+
 ROWS_F32, ROWS_F16, ROWS_Q8, ROWS_Q4 = 0, 1, 2, 3
 
 

@@ -194,6 +194,18 @@ int dlrm_tbe_forward_rows(const void* weights, int32_t format, int64_t row_bytes
                           const float* per_sample_weights, float* out, int64_t out_batch_stride,
                           int32_t* error_flag, dlrm_stream_t stream);
 
+/*
+ * Gradient of the per-sample weights of a weighted lookup (learned weighted pooling,
+ * dlrm_s_pytorch.py:475-478, 544-545): grad_per_sample_weights[l] =
+ * sum_d grad_out[b*grad_batch_stride + t*D + d] * W[row_base[t] + indices[l]][d] for the
+ * bag (t, b) holding lookup l (0 for lookups outside every bag or out of range).
+ */
+int dlrm_tbe_psw_grad(const float* weights, int64_t D, const int64_t* row_base, int32_t T,
+                      int32_t B, const void* indices, int32_t index_bits, const void* offsets,
+                      int32_t offset_bits, int64_t num_lookups, const float* grad_out,
+                      int64_t grad_batch_stride, float* grad_per_sample_weights,
+                      dlrm_stream_t stream);
+
 /* Workspace for the deterministic (sorted, segment-reduced) backward. */
 size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows, int64_t D);
 
