@@ -405,6 +405,81 @@ __device__ __forceinline__ bool splitk_reduce(const GemmParams& p, int tile, int
   return true;
 }
 
+// Tile epilogue shared by the fp32 and the split-bf16 bodies: PARTIAL slabs, or the split-K
+// hand-off then the fused epilogue.  acc is the wave's FM x FN grid of 16x16 accumulators
+// (register r: row 4*(lane>>4) + r, col lane&15 - the same map for every 16x16 MFMA form);
+// rs[i] is the full (this split's) row sum of row wm0 + 16 i + (lane&15) of op(A).
+template <int BM, int BN, int WGM, int WGN, bool RS, int FM, int FN>
+__device__ __forceinline__ void finish_tile(const GemmParams& p, const f32x4 (&acc)[FM][FN],
+                                            float (&rs)[FM], int tile, int split, int tn,
+                                            int64_t m0, int64_t n0, float* smem) {
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int kq = lane >> 4;
+  const int l16 = lane & 15;
+  const int wm0 = (wave / WGN) * WM;
+  const int wn0 = (wave % WGN) * WN;
+  // Owners of the row sums: kq == 0 lanes of the left wave column, first column of tiles.
+  const bool rs_owner = RS && tn == 0 && (wave % WGN) == 0 && kq == 0;
+
+  constexpr int NV = FM * FN * 4;
+  float v[NV];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[(i * FN + j) * 4 + r] = acc[i][j][r];
+  if (p.mode == DLRM_GEMM_PARTIAL) {
+    // raw partial sums for a REDUCE job of a later launch (the kernel boundary publishes)
+    float* slab = p.part + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t col = n0 + wn0 + j * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
+          if (row < p.M && col < p.N) slab[row * p.N + col] = v[(i * FN + j) * 4 + r];
+        }
+      }
+    if (rs_owner) {
+      float* rslab = p.part + (int64_t)p.splits * p.M * p.N + (int64_t)split * p.M;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int64_t row = m0 + wm0 + i * 16 + l16;
+        if (row < p.M) rslab[row] = rs[i];
+      }
+    }
+    return;
+  }
+  if (!splitk_reduce<BM, BN, NV, FM>(p, tile, split, v, rs, wm0 + l16, 16, rs_owner, smem))
+    return;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t col = n0 + wn0 + j * 16 + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
+        if (row < p.M && col < p.N)
+          apply_epilogue(p, row, col, p.alpha * v[(i * FN + j) * 4 + r]);
+      }
+    }
+  if (rs_owner) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int64_t row = m0 + wm0 + i * 16 + l16;
+      if (row < p.M) apply_epilogue(p, row, p.ones_col, p.alpha * rs[i]);
+    }
+  }
+}
+
+
 // One output tile (and K split) of problem p: the software-pipelined 16x16x4 body.  The
 // workgroup is WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile.
 template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS>
@@ -539,69 +614,278 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   }
 
   // Row sums: lanes l16, l16+16, l16+32, l16+48 hold the four k-quarters of row l16
-  // (fixed pairing order: deterministic).  Owners: kq == 0 lanes of the left wave column,
-  // in the first column of tiles.
+  // (fixed pairing order: deterministic).
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     rs[i] += __shfl_xor(rs[i], 16, 64);
     rs[i] += __shfl_xor(rs[i], 32, 64);
   }
-  const bool rs_owner = RS && tn == 0 && (wave % WGN) == 0 && kq == 0;
+  finish_tile<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0, smem);
+}
 
-  // Register r of a 16x16 accumulator holds row 4*(lane>>4) + r, col lane&15.
-  constexpr int NV = FM * FN * 4;
-  float v[NV];
+// ---------------------------------------------------------------- split-bf16 body --
+// fp32 GEMM on the bf16 matrix core (v_mfma_f32_16x16x32_bf16, 16x the f32 MFMA rate).
+// Every fp32 operand x is split exactly into three bf16 terms, x = h + m + l (round to
+// nearest at each level: |m| <= 2^-8 |x|, |l| <= 2^-16 |x|, and l is exact because the
+// residual after two 8-bit roundings has at most 8 significant bits).  A product is then
+//   a*b = ah*bh + (ah*bm + am*bh) + (ah*bl + al*bh + am*bm) + O(2^-24 |a*b|),
+// six bf16 products whose dropped terms (am*bl, al*bm, al*bl) are below one fp32 ulp of
+// a*b.  The products are exact in the MFMA and accumulate in fp32, 6 roundings per 32 k
+// (the f32 MFMA rounds once per k), so the result is as accurate as the exact-f32 path
+// (tests/test_gpu_kernels.py::test_gemm_x6_accuracy bounds both against fp64).
+//
+// Staging is the fp32 body's (raw buffer loads of whole float4s); the split happens once
+// per element when a thread writes its staged float4 to LDS, as three bf16 planes:
+//   k-contiguous operand  -> [mn][32 + 8]  per plane, fragments by ds_read_b128;
+//   mn-contiguous operand -> [k/8][8][MN + 16] (+32 dwords between k-octets) per plane,
+//   fragments by two ds_read_b64_tr_b16 (hardware transpose; the pitch and the octet gap
+//   put the eight rows a 32-lane half reads on eight distinct 8-bank windows).
+// One K-tile (BK = 32) is one 16x16x32 k-step: lane l holds k = 8(l>>4) .. +7 of row /
+// column l&15 for both operands, the map of the fp32 body's fragments.
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using s16x4 = __attribute__((ext_vector_type(4))) short;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ unsigned pk_bf16(float x0, float x1) {
+  using bf16x2 = __attribute__((ext_vector_type(2))) __bf16;
+  return __builtin_bit_cast(unsigned, bf16x2{(__bf16)x0, (__bf16)x1});  // v_cvt_pk_bf16_f32
+}
+__device__ __forceinline__ float lo_f(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float hi_f(unsigned u) {
+  return __builtin_bit_cast(float, u & 0xffff0000u);
+}
+// x0, x1 -> packed (h, m, l) bf16 pairs, x = h + m + l exactly.
+__device__ __forceinline__ void split2(float x0, float x1, unsigned& h, unsigned& m,
+                                       unsigned& l) {
+  h = pk_bf16(x0, x1);
+  const float r0 = x0 - lo_f(h), r1 = x1 - hi_f(h);
+  m = pk_bf16(r0, r1);
+  const float s0 = r0 - lo_f(m), s1 = r1 - hi_f(m);
+  l = pk_bf16(s0, s1);
+}
+
+// bf16 three-plane image of one operand's (MN x 32) panel (one LDS buffer).
+template <int MN, bool KC>
+struct Img6 {
+  static constexpr int BK = kBK;
+  static constexpr int PITCH = KC ? BK + 8 : MN + 16;    // bf16 per row
+  static constexpr int OCT = 8 * PITCH + 64;             // !KC: bf16 per k-octet (+32 dwords)
+  static constexpr int PLANE = KC ? MN * PITCH : (BK / 8) * OCT;
+  static constexpr int SIZE = 3 * PLANE;                 // bf16 per buffer
+  static_assert(KC || (PITCH / 16) % 2 == 1, "tr-read pitch must be an odd multiple of 8 dwords");
+
+  // staged float4 (4 consecutive k at mn if KC, 4 consecutive mn at k otherwise) -> planes
+  __device__ __forceinline__ static void store(__bf16* buf, int mn, int k, float4 f) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split2(f.x, f.y, h0, m0, l0);
+    split2(f.z, f.w, h1, m1, l1);
+    const int e = KC ? mn * PITCH + k : (k >> 3) * OCT + (k & 7) * PITCH + mn;
+    *reinterpret_cast<uint2*>(buf + e) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(buf + PLANE + e) = make_uint2(m0, m1);
+    *reinterpret_cast<uint2*>(buf + 2 * PLANE + e) = make_uint2(l0, l1);
+  }
+
+  // Fragment of the 16-wide sub-tile at mn0 for this lane: plane q, k = 8 kq .. 8 kq + 7.
+  __device__ __forceinline__ static bf16x8 frag(const __bf16* buf, int q, int mn0, int l16,
+                                                int kq) {
+    const __bf16* pl = buf + q * PLANE;
+    if constexpr (KC) {
+      return __builtin_bit_cast(
+          bf16x8, *reinterpret_cast<const uint4*>(pl + (mn0 + l16) * PITCH + kq * 8));
+    } else {
+      // ds_read_b64_tr_b16: lane 4r+c of the 16-lane group addresses row r, columns 4c..4c+3
+      // of a 4 x 16 block; lane i receives column i, row r in element r.
+      const int r = l16 >> 2, c = l16 & 3;
+      const __bf16* b0 = pl + kq * OCT + r * PITCH + mn0 + 4 * c;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0 + 4 * PITCH));
+      using s16x8 = __attribute__((ext_vector_type(8))) short;
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+template <int BM, int BN>
+constexpr int x6_smem_bytes() {
+  constexpr int a = Img6<BM, true>::SIZE > Img6<BM, false>::SIZE ? Img6<BM, true>::SIZE
+                                                                  : Img6<BM, false>::SIZE;
+  constexpr int b = Img6<BN, true>::SIZE > Img6<BN, false>::SIZE ? Img6<BN, true>::SIZE
+                                                                  : Img6<BN, false>::SIZE;
+  return 2 * (a + b) * 2;  // double-buffered, 2 B per bf16
+}
+
+template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS>
+__device__ __forceinline__ void pipe_body6(const GemmParams& p, int lb, float* smem) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1, "wave sub-tile");
+  using SA = Stage<BM, kBK, A_KC, true, NT>;
+  using SB = Stage<BN, kBK, B_KC, true, NT>;
+  using IA = Img6<BM, A_KC>;
+  using IB = Img6<BN, B_KC>;
+  constexpr int BUF = IA::SIZE + IB::SIZE;  // bf16 per LDS buffer
+  constexpr int NS = SA::NV + SB::NV;       // staged float4 per thread per K-tile
+  constexpr int NP = 6;                     // bf16 products per K-tile
+  static_assert(NS <= NP - 1, "staging must finish before the barrier step");
+  static_assert(!RS || !A_KC, "row sums are taken on the mn-contiguous A (wgrad)");
+
+  const int tile = lb / p.splits;
+  const int split = lb - tile * p.splits;
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM;
+  const int64_t n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * p.kchunk;
+  const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int kq = lane >> 4;
+  const int l16 = lane & 15;
+  const int wm0 = (wave / WGN) * WM;
+  const int wn0 = (wave % WGN) * WN;
+  __bf16* lds = reinterpret_cast<__bf16*>(smem);
+
+  f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 rsq[SA::NV];  // RS: this thread's staged A float4s summed over its k rows
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[(i * FN + j) * 4 + r] = acc[i][j][r];
-  if (p.mode == DLRM_GEMM_PARTIAL) {
-    // raw partial sums for a REDUCE job of a later launch (the kernel boundary publishes)
-    float* slab = p.part + (int64_t)split * p.M * p.N;
+  for (int v = 0; v < SA::NV; ++v) rsq[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
+  SA sa;
+  SB sb;
+  const int64_t a_ext = A_KC ? (p.M - 1) * p.lda + p.K : (p.K - 1) * p.lda + p.M;
+  const int64_t b_ext = B_KC ? (p.N - 1) * p.ldb + p.K : (p.K - 1) * p.ldb + p.N;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)(a_ext * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)(b_ext * 4), 0x00020000);
+  typename SA::Fetch fa;
+  typename SB::Fetch fb;
+  sa.fetch_init(fa, p.lda, m0, p.M, kbeg, tid);
+  sb.fetch_init(fb, p.ldb, n0, p.N, kbeg, tid);
+  const int a_step = A_KC ? kBK * 4 : (int)(kBK * p.lda * 4);
+  const int b_step = B_KC ? kBK * 4 : (int)(kBK * p.ldb * 4);
+  const int kb32 = (int)kbeg, K32 = (int)p.K;
+  auto fetch_one = [&](int c, int t) {
+    if (c < SA::NV)
+      sa.fetch4(c, fa, ra, a_step, t, kb32 + t * kBK, K32);
+    else
+      sb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * kBK, K32);
+  };
+  auto put_one = [&](int c, __bf16* buf, bool live) {  // live: the tile is < nk
+    int mn, k;
+    if (c < SA::NV) {
+      sa.coords(tid + c * NT, mn, k);
+      IA::store(buf, mn, k, sa.regs[c]);
+      if (RS && live) {
+        rsq[c].x = add_f32(rsq[c].x, sa.regs[c].x);
+        rsq[c].y = add_f32(rsq[c].y, sa.regs[c].y);
+        rsq[c].z = add_f32(rsq[c].z, sa.regs[c].z);
+        rsq[c].w = add_f32(rsq[c].w, sa.regs[c].w);
+      }
+    } else {
+      sb.coords(tid + (c - SA::NV) * NT, mn, k);
+      IB::store(buf + IA::SIZE, mn, k, sb.regs[c - SA::NV]);
+    }
+  };
+  struct Frag {
+    bf16x8 q[3];
+  };
+  auto read_frags = [&](const __bf16* buf, Frag (&a)[FM], Frag (&b)[FN]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i].q[q] = IA::frag(buf, q, wm0 + i * 16, l16, kq);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j].q[q] = IB::frag(buf + IA::SIZE, q, wn0 + j * 16, l16, kq);
+    }
+  };
+  // product s of the six: (a plane, b plane), small terms first, h*h last
+  auto products = [&](int s, const Frag (&ca)[FM], const Frag (&cb)[FN]) {
+    constexpr int PA[NP] = {0, 2, 1, 0, 1, 0};
+    constexpr int PB[NP] = {2, 0, 1, 1, 0, 0};
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int64_t col = n0 + wn0 + j * 16 + l16;
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i].q[PA[s]], cb[j].q[PB[s]],
+                                                            acc[i][j], 0, 0, 0);
+  };
+
+  Frag a[FM], b[FN];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
-          if (row < p.M && col < p.N) slab[row * p.N + col] = v[(i * FN + j) * 4 + r];
-        }
-      }
-    if (rs_owner) {
-      float* rslab = p.part + (int64_t)p.splits * p.M * p.N + (int64_t)split * p.M;
+  for (int c = 0; c < NS; ++c) fetch_one(c, 0);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int64_t row = m0 + wm0 + i * 16 + l16;
-        if (row < p.M) rslab[row] = rs[i];
+  for (int c = 0; c < NS; ++c) put_one(c, lds, true);
+#pragma unroll
+  for (int c = 0; c < NS; ++c) fetch_one(c, 1);
+  __syncthreads();
+  read_frags(lds, a, b);
+
+  auto iteration = [&](int kt, const Frag (&ca)[FM], const Frag (&cb)[FN], Frag (&na)[FM],
+                       Frag (&nb)[FN]) {
+    __bf16* nbuf = lds + ((kt + 1) & 1) * BUF;
+#pragma unroll
+    for (int s = 0; s < NP - 1; ++s) {
+      products(s, ca, cb);
+      if (s < NS) {
+        put_one(s, nbuf, kt + 1 < nk);
+        fetch_one(s, kt + 2);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    return;
+    __syncthreads();
+    read_frags(nbuf, na, nb);
+    __builtin_amdgcn_sched_barrier(0);
+    products(NP - 1, ca, cb);
+  };
+  Frag a1[FM], b1[FN];
+  for (int kt = 0; kt < nk; kt += 2) {
+    iteration(kt, a, b, a1, b1);
+    if (kt + 1 >= nk) break;
+    iteration(kt + 1, a1, b1, a, b);
   }
-  if (!splitk_reduce<BM, BN, NV, FM>(p, tile, split, v, rs, wm0 + l16, 16, rs_owner, smem))
-    return;
+
+  float rs[FM];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int i = 0; i < FM; ++i) rs[i] = 0.f;
+  if constexpr (RS) {
+    // Row sums of op(A) = A[k][m]: thread tid staged the mn quad 4*(tid % (BM/4)) at k rows
+    // tid / (BM/4) + v*R; sum its float4s (v order), then the R partials per row in order.
+    constexpr int Q = BM / 4, R = NT / Q;
+    static_assert(NT % Q == 0, "row-sum map");
+    float4 t = rsq[0];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int64_t col = n0 + wn0 + j * 16 + l16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
-        if (row < p.M && col < p.N)
-          apply_epilogue(p, row, col, p.alpha * v[(i * FN + j) * 4 + r]);
-      }
+    for (int v = 1; v < SA::NV; ++v) {
+      t.x = add_f32(t.x, rsq[v].x);
+      t.y = add_f32(t.y, rsq[v].y);
+      t.z = add_f32(t.z, rsq[v].z);
+      t.w = add_f32(t.w, rsq[v].w);
     }
-  if (rs_owner) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int64_t row = m0 + wm0 + i * 16 + l16;
-      if (row < p.M) apply_epilogue(p, row, p.ones_col, p.alpha * rs[i]);
+    __syncthreads();  // every wave is done with the LDS images
+    float* part = smem;  // [R][BM]
+    *reinterpret_cast<float4*>(part + (tid / Q) * BM + 4 * (tid % Q)) = t;
+    __syncthreads();
+    float* sums = smem + R * BM;  // [BM]
+    if (tid < BM) {
+      float s = part[tid];
+      for (int r = 1; r < R; ++r) s += part[r * BM + tid];
+      sums[tid] = s;
     }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i) rs[i] = sums[wm0 + i * 16 + l16];
+    __syncthreads();  // the split-K hand-off reuses smem[0]
   }
+  finish_tile<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0, smem);
 }
 
 // REDUCE job: C = epi(alpha * sum_s part[s]) in split order (the same additions as the
@@ -684,6 +968,32 @@ __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
     if (kind == 3) return pipe_body<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
   if constexpr ((KINDS & 16) != 0)
     if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
+}
+
+// The same grouped launch on the split-bf16 body (pipe_body6).
+template <int BM, int BN, int WGM, int WGN, int KINDS>
+__global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group6_kernel(const GemmGroup g) {
+  __shared__ __attribute__((aligned(16))) float smem[x6_smem_bytes<BM, BN>() / 4];
+  const int b = blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxGroup; ++i)
+    if (i < g.n && b >= g.p[i].block0) q = i;
+  const GemmParams& p = g.p[q];
+  const int nq = (q + 1 < g.n ? g.p[q + 1].block0 : g.total) - p.block0;
+  const int lb = xcd_remap(b - p.block0, nq);
+  if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
+  const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
+  if constexpr ((KINDS & 1) != 0)
+    if (kind == 0) return pipe_body6<BM, BN, WGM, WGN, true, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 2) != 0)
+    if (kind == 1) return pipe_body6<BM, BN, WGM, WGN, true, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 4) != 0)
+    if (kind == 2) return pipe_body6<BM, BN, WGM, WGN, false, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 8) != 0)
+    if (kind == 3) return pipe_body6<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 16) != 0)
+    if (kind == 4) return pipe_body6<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
 }
 
 // Fallback for operands the pipelined body cannot take (unaligned rows, ragged float4
@@ -778,6 +1088,13 @@ struct Plan {
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
+}
+
+// Math of the pipelined GEMMs: exact-f32 MFMA (default) or the split-bf16 body
+// (DLRM_GEMM_MATH=x6).  Read per call, like the tuning overrides.
+bool gemm_x6() {
+  const char* v = getenv("DLRM_GEMM_MATH");
+  return v && strcmp(v, "x6") == 0;
 }
 
 Plan make_plan(int64_t s, int64_t K) {
@@ -920,6 +1237,7 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
       t = Tile{64, 32, 2, 2};
     }
   }
+  if (gemm_x6() && (t.bm == 128 || t.bn == 128)) t = Tile{64, 64, 2, 2};
 }
 
 // Split-K workspace: the fixed 64 KiB ticket head, then each problem's records.
@@ -937,7 +1255,7 @@ size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
   return any ? c.used + 256 : 0;
 }
 
-template <int BM, int BN, int WGM = 2, int WGN = 2>
+template <int BM, int BN, bool X6 = false, int WGM = 2, int WGN = 2>
 int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes, hipStream_t st) {
   constexpr int NT = WGM * WGN * 64;
   GemmGroup g{};
@@ -985,15 +1303,28 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
   // row sums, two wgrads), else all kinds
-  switch (kinds) {
+  if constexpr (X6) {
+    switch (kinds) {
+#define K_(M_)                                                                           \
+  case M_:                                                                              \
+    hipLaunchKernelGGL((gemm_group6_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g); \
+    break;
+      K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
+#undef K_
+      default:
+        hipLaunchKernelGGL((gemm_group6_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
+    }
+  } else {
+    switch (kinds) {
 #define K_(M_)                                                                          \
   case M_:                                                                             \
     hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g); \
     break;
-    K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
+      K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
 #undef K_
-    default:
-      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
+      default:
+        hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
+    }
   }
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32");
   return DLRM_OK;
@@ -1098,6 +1429,11 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
   const size_t need = group_ws_bytes(m, q, t, pl);
   if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: every problem unsplit
     for (int i = 0; i < m; ++i) pl[i] = make_plan(1, q[i].K);
+  }
+  if (gemm_x6()) {  // split-bf16 body: 128-wide tiles stage too much per K-tile
+    if (t.bm == 32) return launch_group<32, 64, true>(m, q, pl, ws, ws_bytes, st);
+    if (t.bn == 32) return launch_group<64, 32, true>(m, q, pl, ws, ws_bytes, st);
+    return launch_group<64, 64, true>(m, q, pl, ws, ws_bytes, st);
   }
   if (t.bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, st);
   if (t.bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, st);

@@ -305,9 +305,12 @@ GEMM_SHAPES = [(2048, 1024, 479), (64, 64, 64), (100, 37, 13), (2, 4, 10), (1000
                (256, 512, 2048), (33, 129, 67)]
 
 
+@pytest.mark.parametrize("math", ["f32", "x6"])
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
-def test_gemm_vs_fp64(ops, M, N, K, ta, tb):
+def test_gemm_vs_fp64(ops, M, N, K, ta, tb, math, monkeypatch):
+    """Both GEMM maths (exact-f32 MFMA, split-bf16 x6) within the fp32 dot-product bound."""
+    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     torch.manual_seed(M + N + K)
     A = torch.randn(K, M) if ta else torch.randn(M, K)
     Bm = torch.randn(N, K) if tb else torch.randn(K, N)
@@ -319,13 +322,15 @@ def test_gemm_vs_fp64(ops, M, N, K, ta, tb):
     assert ok, msg
 
 
-GEMM_CFGS = ["64x64", "128x64", "64x128"]
+GEMM_CFGS = [("f32", "64x64"), ("f32", "128x64"), ("f32", "64x128"), ("f32", "64x32"),
+             ("f32", "32x64"), ("x6", "64x64"), ("x6", "64x32"), ("x6", "32x64")]
 
 
-@pytest.mark.parametrize("cfg", GEMM_CFGS)
-def test_gemm_every_kernel_config(ops, cfg, monkeypatch):
+@pytest.mark.parametrize("math,cfg", GEMM_CFGS)
+def test_gemm_every_kernel_config(ops, math, cfg, monkeypatch):
     """Every tile/BK/k-group/MFMA-shape instantiation the planner can pick, forced via the
     tuning override, on ragged shapes in all four operand layouts, with and without split-K."""
+    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     monkeypatch.setenv("DLRM_GEMM_CFG", cfg)
     ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)  # split-K tickets start at 0
     for (M, N, K) in [(130, 70, 300), (64, 128, 256), (3, 5, 1030)]:
@@ -343,7 +348,9 @@ def test_gemm_every_kernel_config(ops, cfg, monkeypatch):
                 assert ok, (cfg, M, N, K, ta, tb, split, msg)
 
 
-def test_gemm_epilogues(ops):
+@pytest.mark.parametrize("math", ["f32", "x6"])
+def test_gemm_epilogues(ops, math, monkeypatch):
+    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     torch.manual_seed(3)
     M, N, K = 300, 200, 130
     X, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
@@ -570,11 +577,12 @@ def test_gemm_splitk_in_launch_fixup_is_deterministic_and_resets(ops, monkeypatc
         assert int(ws[:4 * tiles].view(torch.int32).abs().sum()) == 0
 
 
-@pytest.mark.parametrize("cfg", GEMM_CFGS)
+@pytest.mark.parametrize("math,cfg", GEMM_CFGS)
 @pytest.mark.parametrize("split", ["1", "4"])
-def test_gemm_ones_col_bias_gradient(ops, cfg, split, monkeypatch):
+def test_gemm_ones_col_bias_gradient(ops, math, cfg, split, monkeypatch):
     """ones_col: C[:, ones_col] = epi(alpha * rowsum(op(A))) beside the GEMM - the bias
     gradient of a Linear layer whose bias is the weight column ones_col (fused SGD)."""
+    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     monkeypatch.setenv("DLRM_GEMM_CFG", cfg)
     monkeypatch.setenv("DLRM_GEMM_SPLIT", split)
     ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
@@ -598,9 +606,11 @@ def test_gemm_ones_col_bias_gradient(ops, cfg, split, monkeypatch):
         assert torch.equal(W[:, K + 1:], W0[:, K + 1:])  # untouched pad columns
 
 
-def test_gemm_group_matches_separate_launches(ops):
+@pytest.mark.parametrize("math", ["f32", "x6"])
+def test_gemm_group_matches_separate_launches(ops, math, monkeypatch):
     """A grouped launch (dgrad of layer l || wgrad+SGD of layer l+1, plus two more problems
     of other layouts) gives bitwise the results of the same problems launched one by one."""
+    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     torch.manual_seed(5)
     Bt = 1024
     g1 = torch.randn(Bt, 512, device=dev)
@@ -645,11 +655,13 @@ def test_gemm_group_matches_separate_launches(ops):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("math", ["f32", "x6"])
 @pytest.mark.parametrize("ones", [False, True])
-def test_gemm_partial_then_reduce_equals_full(ops, ones):
+def test_gemm_partial_then_reduce_equals_full(ops, ones, math, monkeypatch):
     """A PARTIAL problem (split-K partials to a buffer) finished by a REDUCE job in a later
     launch gives bitwise the in-launch split-K result (same splits, same sum order), with
     the fused SGD epilogue and the ones_col bias row sums."""
+    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     torch.manual_seed(11)
     Bt, Nout, K = 2048, 256, 512
     g = torch.randn(Bt, Nout, device=dev)
