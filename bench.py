@@ -166,6 +166,80 @@ def pmc_traffic():
             os.path.relpath(files[-1], ROOT))
 
 
+def _graph_time_us(fn, n=20, reps=5):
+    """Device time per call of ``fn``: n calls captured in one hipGraph, replayed ``reps``
+    times between HIP events on the capturing stream."""
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(n):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            g.replay()
+        e.record()
+        torch.cuda.synchronize()
+    return s.elapsed_time(e) / (n * reps) * 1000.0
+
+
+def gather_rooflines(tr, batch, B, c, dev):
+    """TBE kernels timed on their own (SURVEY.md §8d bytes):
+    * the C3 step's gather (dlrm_tbe_forward on the bench batch, without the sort and the
+      bottom MLP that share the step's lookup launch);
+    * the bandwidth regime the embedding metric is about: the C1 table shape (8 x 1e5 rows,
+      D=64, L=100, B=2048: 0.43 GB gathered per batch), forward and backward + exact SGD."""
+    from dlrm_hip import ops
+    D, L = c["D"], c["L"]
+    T = tr.T_local
+    out = {}
+    if T > 0:
+        pooled = torch.empty(B, T, D, device=dev)
+        us = _graph_time_us(lambda: ops.tbe_forward(tr.weights, tr.row_base, T, B, batch.indices,
+                                                    batch.offsets, out=pooled))
+        n = T * B * L
+        by = n * (4 * D + 4) + 4 * (T * B + 1) + 4 * T * B * D
+        out["c3_gather_only"] = {"us": round(us, 2), "bytes": by,
+                                 "achieved": round(by / us / 1e3, 1),
+                                 "frac": round(by / us / 1e3 / HBM_PEAK_GBS, 4)}
+    T1, R1, D1, L1, B1 = 8, 100000, 64, 100, 2048
+    g = torch.Generator(device=dev).manual_seed(7)
+    W1 = torch.empty(T1 * R1, D1, device=dev).uniform_(-0.003, 0.003, generator=g)
+    rb1 = torch.arange(T1 + 1, dtype=torch.int64, device=dev) * R1
+    idx1 = torch.randint(0, R1, (T1 * B1 * L1,), dtype=torch.int32, device=dev, generator=g)
+    off1 = torch.arange(T1 * B1 + 1, dtype=torch.int32, device=dev) * L1
+    pooled1 = torch.empty(B1, T1, D1, device=dev)
+    grad1 = torch.empty(B1, T1, D1, device=dev).uniform_(-1e-3, 1e-3, generator=g)
+    ws1 = torch.empty(ops.tbe_backward_workspace_size(idx1.numel(), T1 * R1, D1),
+                      dtype=torch.uint8, device=dev)
+    n1 = T1 * B1 * L1
+    fwd_by = n1 * (4 * D1 + 4) + 4 * (T1 * B1 + 1) + 4 * T1 * B1 * D1
+    bwd_by = 4 * T1 * B1 * D1 + n1 * (4 + 8 * D1)
+    fus = _graph_time_us(lambda: ops.tbe_forward(W1, rb1, T1, B1, idx1, off1, out=pooled1), n=10)
+    bus = _graph_time_us(lambda: ops.tbe_backward("sgd", W1, rb1, T1, B1, idx1, off1, grad1,
+                                                  lr=1e-9, workspace=ws1,
+                                                  max_lookups_per_table=B1 * L1), n=10)
+    uniq = int(torch.unique((idx1.view(T1, -1).long()
+                             + torch.arange(T1, device=dev).view(-1, 1) * R1)).numel())
+    out["c1_shape"] = {"tables": T1, "rows": R1, "emb_dim": D1, "lookups_per_bag": L1,
+                       "batch": B1,
+                       "fwd_us": round(fus, 2), "fwd_bytes": fwd_by,
+                       "fwd_achieved": round(fwd_by / fus / 1e3, 1),
+                       "fwd_frac": round(fwd_by / fus / 1e3 / HBM_PEAK_GBS, 4),
+                       "bwd_sgd_us": round(bus, 2), "bwd_bytes_upper": bwd_by,
+                       "unique_rows": uniq,
+                       "bwd_bytes_dedup": 4 * T1 * B1 * D1 + n1 * 4 + uniq * 8 * D1,
+                       "bwd_achieved_upper": round(bwd_by / bus / 1e3, 1),
+                       "bwd_achieved_dedup": round((4 * T1 * B1 * D1 + n1 * 4 + uniq * 8 * D1)
+                                                   / bus / 1e3, 1)}
+    return out
+
+
 def cpu_baseline(c, seconds: float):
     """The CPU oracle (a restatement of the reference step, pinned to its golden vectors)
     timed on this host's cores: bounded sample of the same workload."""
@@ -344,7 +418,11 @@ def main():
                         "fwd_frac": round(fwd_bytes / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "fwd_bytes": fwd_bytes, "fwd_us": round(f_ms * 1000.0, 2),
                         "bwd_achieved_upper": round(bwd_bytes / (b_ms * 1e-3) / 1e9, 1),
-                        "bwd_bytes_upper": bwd_bytes, "bwd_us": round(b_ms * 1000.0, 2)}
+                        "bwd_bytes_upper": bwd_bytes, "bwd_us": round(b_ms * 1000.0, 2),
+                        "fwd_note": "fwd_us is the step's lookup launch, which also runs the "
+                                    "backward's index sort and the bottom MLP forward"}
+        if rank == 0 and world == 1 and emb_roof is not None:
+            emb_roof.update(gather_rooflines(tr, batches[0], B, c, dev))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -23,6 +23,7 @@
 #include <hipcub/hipcub.hpp>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "mlp_rows.hpp"
 #include "tbe_common.hpp"
@@ -32,39 +33,54 @@ namespace {
 constexpr int CH = 16;  // sorted lookups per block (all gradient rows of a block in flight)
 
 // ---------------------------------------------------------------- backward --
-// Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags).
-template <typename IdxT, typename OffT, typename KeyT>
+// Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags),
+// its position and its bag.  One wave per bag (the lanes stride over the bag's lookups:
+// coalesced, no search); the workgroups past the bags cover the lookups outside every bag
+// (before off[0] / from off[T*B]).  KEYS = 0 (the tiled sort takes its keys from the
+// indices itself): only bag_of, plus sentinel keys / positions of the outside lookups
+// written straight into the sorted arrays (keys / pos then point at keys_out / pos_out).
+constexpr int kBagWaves = 4;     // bags per 256-thread workgroup
+constexpr int kOutsideBlocks = 16;
+template <typename IdxT, typename OffT, typename KeyT, bool KEYS>
 __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, KeyT sentinel, KeyT* __restrict__ keys, int32_t* __restrict__ pos,
     int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
   const int64_t nb = (int64_t)T * B;
-  KeyT key = sentinel;
-  int32_t bag = -1;
-  if (p >= (int64_t)off[0] && p < (int64_t)off[nb]) {
-    int64_t lo = 0, hi = nb;  // invariant off[lo] <= p < off[hi]
-    while (hi - lo > 1) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)off[mid] <= p)
-        lo = mid;
-      else
-        hi = mid;
-    }
-    const int t = (int)(lo / B);
-    const int64_t r = (int64_t)idx[p];
-    const int64_t nrows = row_base[t + 1] - row_base[t];
-    if (r >= 0 && r < nrows) {
-      key = (KeyT)(row_base[t] + r);
-      bag = (int32_t)lo;
-    } else if (err) {
-      atomicOr(err, DLRM_TBE_ERR_INDEX);
-    }
+  const int64_t bag_blocks = (nb + kBagWaves - 1) / kBagWaves;
+  const int lane = threadIdx.x & 63;
+  if ((int64_t)blockIdx.x >= bag_blocks) {  // lookups outside every bag
+    const int64_t a = (int64_t)off[0], e = (int64_t)off[nb];
+    const int64_t stride = (int64_t)kOutsideBlocks * blockDim.x;
+    const int64_t g = ((int64_t)blockIdx.x - bag_blocks) * blockDim.x + threadIdx.x;
+    auto mark = [&](int64_t p) {
+      keys[p] = sentinel;
+      pos[p] = (int32_t)p;
+      bag_of[p] = -1;
+    };
+    for (int64_t p = g; p < a && p < N; p += stride) mark(p);
+    for (int64_t p = e + g; p < N; p += stride) mark(p);
+    return;
   }
-  keys[p] = key;
-  pos[p] = (int32_t)p;
-  bag_of[p] = bag;
+  const int64_t bag = (int64_t)blockIdx.x * kBagWaves + (threadIdx.x >> 6);
+  if (bag >= nb) return;
+  const int t = (int)(bag / B);
+  const int64_t a = (int64_t)off[bag], e = (int64_t)off[bag + 1];
+  const int64_t rb = row_base[t], nrows = row_base[t + 1] - rb;
+  for (int64_t p = a + lane; p < e; p += 64) {
+    const int64_t r = (int64_t)idx[p];
+    const bool ok = r >= 0 && r < nrows;
+    if (!ok && err) atomicOr(err, DLRM_TBE_ERR_INDEX);
+    if constexpr (KEYS) {
+      keys[p] = ok ? (KeyT)(rb + r) : sentinel;
+      pos[p] = (int32_t)p;
+    }
+    bag_of[p] = ok ? (int32_t)bag : -1;
+  }
+}
+
+inline int64_t keys_grid(int T, int B) {
+  return ((int64_t)T * B + kBagWaves - 1) / kBagWaves + kOutsideBlocks;
 }
 
 // Per-table sort (replaces keys + device radix sort when every table's lookups fit in
@@ -749,6 +765,333 @@ inline int bit_width_u64(uint64_t v) {
   return b < 1 ? 1 : b;
 }
 
+// ------------------------------------------------ tiled per-table radix sort --
+// Tables with more lookups than one workgroup sorts (kSegCap: e.g. L = 100 pooling) and
+// 32-bit keys: a stable LSD radix sort of each table's (local row, position) pairs in its
+// own lookup range, DB-bit digits, tiles of kTile lookups.  Per pass, three launches:
+//   hist:    tile (t, j) counts its digits (LDS atomics) -> hist[t][d][j];
+//   scan:    per table, exclusive scan of hist in (digit, tile) order;
+//   scatter: tile (t, j) ranks its lookups by digit (wave ballots + per-(digit, wave)
+//            running counts in LDS: element order kept, so stable) and writes each to
+//            table start + hist[t][d][j] + its rank among the tile's digit-d lookups.
+// Same (row, position) order as the device-wide sort and the per-table LDS sort; no
+// memsets, no decoupled look-back.  The keys kernel has written bag_of (by lookup
+// position) and the sentinels of the lookups outside every bag.  A table with more
+// lookups than its J tiles cover (max_lookups_per_table underestimated) is not sorted: its
+// range becomes sentinels (no update) and DLRM_TBE_ERR_TABLE_CAP is raised.
+constexpr int kTileThreads = 1024, kTileItems = 4, kTile = kTileThreads * kTileItems;
+constexpr int kTileWaves = kTileThreads / 64;
+
+struct TiledPass {
+  const int64_t* row_base;
+  int T, B, J;          // tables, bags per table, tiles per table
+  int shift;            // digit shift of this pass
+  int first, last;      // pass 0 reads the indices; the last pass writes global keys
+  const uint32_t* kin;  // pass input (pass > 0)
+  const int32_t* pin;
+  uint32_t* kout;       // pass output
+  int32_t* pout;
+  uint32_t* hist;       // [T][2^DB][J]
+  uint32_t sentinel;    // global sentinel key (last pass)
+  int32_t* err;
+};
+
+template <int DB>
+struct TiledLds {
+  uint32_t cnt[(1 << DB) * (kTileWaves + 1)];  // per (digit, wave)
+  uint32_t dstart[1 << DB];                     // tile-local start of each digit
+  uint32_t wsum[kTileWaves];
+  uint32_t key[kTile];                          // the tile in digit order
+  int32_t pos[kTile];
+};
+
+// Element e of tile j of table t: wave-striped (e = w*256 + u*64 + l), position
+// s + j*kTile + e.  Loads this thread's kTileItems (key, pos, valid).
+template <typename IdxT>
+__device__ __forceinline__ void tiled_load(const TiledPass& a, const IdxT* __restrict__ idx,
+                                           int64_t s, int64_t n, int j, int64_t nrows,
+                                           uint32_t (&key)[kTileItems],
+                                           int32_t (&pos)[kTileItems], bool (&ok)[kTileItems]) {
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+#pragma unroll
+  for (int u = 0; u < kTileItems; ++u) {
+    const int64_t e = (int64_t)j * kTile + w * (kTileItems * 64) + u * 64 + l;
+    ok[u] = e < n;
+    const int64_t p = s + (ok[u] ? e : 0);
+    if (a.first) {
+      const int64_t r = (int64_t)idx[p];
+      key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
+      pos[u] = (int32_t)p;
+    } else {
+      key[u] = a.kin[p];
+      pos[u] = a.pin[p];
+    }
+  }
+}
+
+template <typename OffT>
+__device__ __forceinline__ bool tiled_range(const TiledPass& a, const OffT* __restrict__ off, int t,
+                                            int64_t& s, int64_t& n) {
+  s = (int64_t)off[(int64_t)t * a.B];
+  n = (int64_t)off[(int64_t)(t + 1) * a.B] - s;
+  return n <= (int64_t)a.J * kTile;  // false: the table overflows its tiles
+}
+
+template <typename IdxT, typename OffT, int DB>
+__global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const TiledPass a) {
+  constexpr int NB = 1 << DB;
+  __shared__ uint32_t cnt[NB];
+  const int t = blockIdx.x / a.J, j = blockIdx.x - (blockIdx.x / a.J) * a.J;
+  int64_t s, n;
+  if (!tiled_range(a, off, t, s, n)) {
+    if (a.first && j == 0 && threadIdx.x == 0 && a.err) atomicOr(a.err, DLRM_TBE_ERR_TABLE_CAP);
+    return;
+  }
+  const int64_t nrows = a.row_base[t + 1] - a.row_base[t];
+  for (int d = threadIdx.x; d < NB; d += kTileThreads) cnt[d] = 0;
+  uint32_t key[kTileItems];
+  int32_t pos[kTileItems];
+  bool ok[kTileItems];
+  tiled_load(a, idx, s, n, j, nrows, key, pos, ok);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kTileItems; ++u)
+    if (ok[u]) atomicAdd(&cnt[(key[u] >> a.shift) & (NB - 1)], 1u);
+  __syncthreads();
+  uint32_t* h = a.hist + ((int64_t)t * a.J + j) * NB;
+  for (int d = threadIdx.x; d < NB; d += kTileThreads) h[d] = cnt[d];
+}
+
+// One workgroup per table: exclusive scan of its NB * J counts in (digit, tile) order.
+// hist is [t][j][d]: thread d walks the tiles of digit d (coalesced across the threads,
+// eight loads in flight), the digit totals are scanned across the workgroup, then each
+// thread rewrites its digit's column with base + running count.
+template <int DB>
+__global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const TiledPass a,
+                                                                      const void* off_v,
+                                                                      int off_bits) {
+  constexpr int NB = 1 << DB;
+  constexpr int DPT = NB / kTileThreads > 0 ? NB / kTileThreads : 1;  // digits per thread
+  static_assert(NB % kTileThreads == 0 || kTileThreads % NB == 0, "digit map");
+  __shared__ uint32_t wsum[kTileWaves];
+  const int t = blockIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  int64_t s, n;
+  const bool fits = off_bits == 32
+                        ? tiled_range(a, static_cast<const int32_t*>(off_v), t, s, n)
+                        : tiled_range(a, static_cast<const int64_t*>(off_v), t, s, n);
+  if (!fits) {
+    if (a.last)  // the table's range holds sentinels (no update)
+      for (int64_t i = tid; i < n; i += kTileThreads) {
+        a.kout[s + i] = a.sentinel;
+        a.pout[s + i] = (int32_t)(s + i);
+      }
+    return;
+  }
+  uint32_t* h = a.hist + (int64_t)t * a.J * NB;
+  const int J = a.J;
+  constexpr int U = 8;
+  // digits d0 .. d0+DPT-1 of this thread (NB < threads: the first NB threads only)
+  const int d0 = tid * DPT;
+  const bool active = d0 < NB;
+  uint32_t tot[DPT];
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) tot[q] = 0;
+  if (active)
+    for (int j0 = 0; j0 < J; j0 += U) {
+      uint32_t v[U][DPT];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < DPT; ++q)
+          v[u][q] = (j0 + u < J) ? h[(int64_t)(j0 + u) * NB + d0 + q] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < DPT; ++q) tot[q] += v[u][q];
+    }
+  uint32_t tsum = 0;
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) tsum += tot[q];
+  uint32_t inc = tsum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (l >= o) inc += y;
+  }
+  if (l == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = inc - tsum;
+#pragma unroll
+  for (int k = 0; k < kTileWaves; ++k) base += k < w ? wsum[k] : 0u;
+  if (!active) return;
+  uint32_t run[DPT];
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) {
+    run[q] = base;
+    base += tot[q];
+  }
+  for (int j0 = 0; j0 < J; j0 += U) {
+    uint32_t v[U][DPT];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < DPT; ++q)
+        v[u][q] = (j0 + u < J) ? h[(int64_t)(j0 + u) * NB + d0 + q] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < DPT; ++q)
+        if (j0 + u < J) {
+          h[(int64_t)(j0 + u) * NB + d0 + q] = run[q];
+          run[q] += v[u][q];
+        }
+  }
+}
+
+template <typename IdxT, typename OffT, int DB>
+__global__ __launch_bounds__(kTileThreads) void tbe_tiled_scatter_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const TiledPass a) {
+  constexpr int NB = 1 << DB;
+  constexpr int CS = kTileWaves + 1;  // counter row stride
+  __shared__ TiledLds<DB> sm;
+  const int t = blockIdx.x / a.J, j = blockIdx.x - (blockIdx.x / a.J) * a.J;
+  int64_t s, n;
+  if (!tiled_range(a, off, t, s, n)) return;
+  if ((int64_t)j * kTile >= n) return;  // empty tile (uniform)
+  const int64_t rb = a.row_base[t];
+  const int64_t nrows = a.row_base[t + 1] - rb;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  uint32_t key[kTileItems];
+  int32_t pos[kTileItems];
+  bool ok[kTileItems];
+  tiled_load(a, idx, s, n, j, nrows, key, pos, ok);
+  for (int i = tid; i < NB * CS; i += kTileThreads) sm.cnt[i] = 0;
+  __syncthreads();
+  const uint64_t below = (1ull << l) - 1;
+  uint32_t rank[kTileItems], dig[kTileItems];
+#pragma unroll
+  for (int u = 0; u < kTileItems; ++u) {
+    const uint32_t d = (key[u] >> a.shift) & (NB - 1);
+    uint64_t peers = __ballot(ok[u]);
+#pragma unroll
+    for (int b = 0; b < DB; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? bal : ~bal;
+    }
+    const uint32_t r = __popcll(peers & below);
+    const uint32_t c = __popcll(peers);
+    const uint32_t base = sm.cnt[d * CS + w];
+    rank[u] = base + r;
+    dig[u] = d;
+    if (ok[u] && r == c - 1) sm.cnt[d * CS + w] = base + c;  // last peer publishes
+  }
+  __syncthreads();
+  // per digit: exclusive prefix over the waves, and the digit's tile total
+  constexpr int DPT = NB / kTileThreads > 0 ? NB / kTileThreads : 1;
+  const int d0 = tid * DPT;
+  uint32_t tot[DPT];
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) {
+    tot[q] = 0;
+    if (d0 + q < NB) {
+      uint32_t v[kTileWaves];
+#pragma unroll
+      for (int k = 0; k < kTileWaves; ++k) v[k] = sm.cnt[(d0 + q) * CS + k];
+#pragma unroll
+      for (int k = 0; k < kTileWaves; ++k) {
+        sm.cnt[(d0 + q) * CS + k] = tot[q];
+        tot[q] += v[k];
+      }
+    }
+  }
+  // tile-local digit starts: exclusive scan of the totals over the workgroup
+  uint32_t tsum = 0;
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) tsum += tot[q];
+  uint32_t inc = tsum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (l >= o) inc += y;
+  }
+  if (l == 63) sm.wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - tsum;
+#pragma unroll
+  for (int k = 0; k < kTileWaves; ++k) run += k < w ? sm.wsum[k] : 0u;
+#pragma unroll
+  for (int q = 0; q < DPT; ++q)
+    if (d0 + q < NB) {
+      sm.dstart[d0 + q] = run;
+      run += tot[q];
+    }
+  __syncthreads();
+  // stage the tile in digit order, then write it out: consecutive threads take
+  // consecutive elements, so each digit's elements go out as one contiguous run
+#pragma unroll
+  for (int u = 0; u < kTileItems; ++u) {
+    if (!ok[u]) continue;
+    const uint32_t lp = sm.dstart[dig[u]] + sm.cnt[dig[u] * CS + w] + rank[u];
+    sm.key[lp] = key[u];
+    sm.pos[lp] = pos[u];
+  }
+  __syncthreads();
+  const int nt = (int)((n - (int64_t)j * kTile) < kTile ? (n - (int64_t)j * kTile) : kTile);
+  const uint32_t* h = a.hist + ((int64_t)t * a.J + j) * NB;
+#pragma unroll
+  for (int u = 0; u < kTileItems; ++u) {
+    const int i = u * kTileThreads + tid;
+    if (i >= nt) continue;
+    const uint32_t k = sm.key[i];
+    const uint32_t d = (k >> a.shift) & (NB - 1);
+    const int64_t dst = s + h[d] + (i - sm.dstart[d]);
+    if (a.last)
+      a.kout[dst] = k < (uint32_t)nrows ? (uint32_t)(rb + k) : a.sentinel;
+    else
+      a.kout[dst] = k;
+    a.pout[dst] = sm.pos[i];
+  }
+}
+
+// DB-bit digits, passes over `bits` key bits (local rows <= total_rows): 10-bit digits when
+// they save a pass over 8-bit ones.
+inline int tiled_digit_bits(int bits) {
+  const char* e = getenv("DLRM_TBE_TILED_DB");  // A/B override: 8 or 10
+  if (e && (atoi(e) == 8 || atoi(e) == 10)) return atoi(e);
+  return (bits + 9) / 10 < (bits + 7) / 8 ? 10 : 8;
+}
+
+template <typename IdxT, typename OffT, int DB>
+void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base, int T, int B,
+                       int J, int bits, uint32_t* k_a, int32_t* p_a, uint32_t* k_out,
+                       int32_t* p_out, uint32_t* hist, uint32_t sentinel, int32_t* err,
+                       int off_bits, hipStream_t st) {
+  const int npass = (bits + DB - 1) / DB;
+  TiledPass a{};
+  a.row_base = row_base, a.T = T, a.B = B, a.J = J, a.hist = hist, a.sentinel = sentinel;
+  a.err = err;
+  // ping-pong so the last pass lands in (k_out, p_out)
+  uint32_t* kb[2] = {(npass & 1) ? k_out : k_a, (npass & 1) ? k_a : k_out};
+  int32_t* pb[2] = {(npass & 1) ? p_out : p_a, (npass & 1) ? p_a : p_out};
+  for (int ps = 0; ps < npass; ++ps) {
+    a.shift = ps * DB;
+    a.first = ps == 0;
+    a.last = ps == npass - 1;
+    a.kin = ps == 0 ? nullptr : kb[(ps - 1) & 1];
+    a.pin = ps == 0 ? nullptr : pb[(ps - 1) & 1];
+    a.kout = kb[ps & 1];
+    a.pout = pb[ps & 1];
+    hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(T * J), dim3(kTileThreads),
+                       0, st, idx, off, a);
+    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(T), dim3(kTileThreads), 0, st, a,
+                       static_cast<const void*>(off), off_bits);
+    hipLaunchKernelGGL((tbe_tiled_scatter_kernel<IdxT, OffT, DB>), dim3(T * J),
+                       dim3(kTileThreads), 0, st, idx, off, a);
+  }
+}
+
 template <typename KeyT>
 struct BwdWs {
   KeyT* keys_in;
@@ -794,6 +1137,16 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
                name, ws_bytes, w.total);
   const bool per_table = presort_applies(sizeof(KeyT), max_seg, N);
+  // large tables (> kSegCap lookups): the tiled per-table sort, its digit histograms in the
+  // block kernel's partial buffer (free until the sort is done)
+  const int64_t tiles_j = dlrm::ceil_div(max_seg > 0 ? max_seg : 1, (int64_t)kTile);
+  const int tdb = tiled_digit_bits(end_bit);
+  const char* tenv = getenv("DLRM_TBE_TILED_SORT");  // "0": device-wide sort (A/B only)
+  const bool tiled = !per_table && sizeof(KeyT) == 4 && max_seg > kSegCap &&
+                     N < (int64_t)0x7fffffff && (int64_t)T * tiles_j < (int64_t)INT32_MAX &&
+                     (int64_t)T * tiles_j * (1 << tdb) <=
+                         (int64_t)2 * dlrm::ceil_div(N, (int64_t)CH) * D &&
+                     !(tenv && strcmp(tenv, "0") == 0);
   if (per_table && presorted) {
     // this batch's per-table sort already ran inside dlrm_tbe_forward_presort
   } else if (per_table) {
@@ -808,8 +1161,28 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
     else SEG(0);
 #undef SEG
     DLRM_LAUNCH_CHECK(name);
+  } else if (tiled) {
+    hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT, false>), dim3(keys_grid(T, B)),
+                       dim3(256), 0, st, static_cast<const IdxT*>(idx),
+                       static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_out,
+                       w.pos_out, w.bag_of, err);
+    DLRM_LAUNCH_CHECK(name);
+    auto* ko = reinterpret_cast<uint32_t*>(w.keys_out);
+    auto* ki = reinterpret_cast<uint32_t*>(w.keys_in);
+    auto* hist = reinterpret_cast<uint32_t*>(w.partial);
+    if (tdb == 10)
+      launch_tiled_sort<IdxT, OffT, 10>(static_cast<const IdxT*>(idx),
+                                        static_cast<const OffT*>(off), row_base, T, B,
+                                        (int)tiles_j, end_bit, ki, w.pos_in, ko, w.pos_out, hist,
+                                        (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, st);
+    else
+      launch_tiled_sort<IdxT, OffT, 8>(static_cast<const IdxT*>(idx),
+                                       static_cast<const OffT*>(off), row_base, T, B,
+                                       (int)tiles_j, end_bit, ki, w.pos_in, ko, w.pos_out, hist,
+                                       (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, st);
+    DLRM_LAUNCH_CHECK(name);
   } else {
-    hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT>), dim3(dlrm::ceil_div(N, 256)),
+    hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT, true>), dim3(keys_grid(T, B)),
                        dim3(256), 0, st, static_cast<const IdxT*>(idx),
                        static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_in,
                        w.pos_in, w.bag_of, err);

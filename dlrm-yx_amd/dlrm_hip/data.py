@@ -128,6 +128,111 @@ class CriteoBinDataset(torch.utils.data.Dataset):
                                  batched=self.batched_or_fbgemm_emb)
 
 
+class RecordPipeline:
+    """Overlapped input pipeline for Criteo binary records (replaces
+    the reference's per-step host transform and ``.cpu()`` sync: dlrm_s_pytorch.py:1910,
+    data_loader_terabyte.py:237-252).
+
+    Three stages, each on its own resource, with ``depth`` slots in flight:
+      * a reader thread fills pinned host slots straight from the file (``readinto``: one
+        read per global batch, 160 B per sample, the GIL released during the read);
+      * a copy stream moves a filled slot to a device slot (async H2D over PCIe) one batch
+        ahead of the step that needs it;
+      * ``next()`` makes the current stream wait for that copy and enqueues one
+        ``dlrm_criteo_decode`` launch into the trainer's fixed record Batch (so a captured
+        step graph replays on it).  Nothing on the host waits for the GPU.
+    The file is read in order and, with ``loop``, wraps around (a trailing partial batch is
+    skipped, as the reference's drop-last loaders do for training).
+    """
+
+    def __init__(self, data_file, batch_size, trainer, max_ind_range=-1, depth=3, loop=True,
+                 n_dense=13, n_sparse=26):
+        import threading
+        import queue
+        self.trainer = trainer
+        self.B = batch_size
+        self.max_ind_range = max_ind_range
+        self.depth = max(2, depth)
+        self.loop = loop
+        self.nf = 1 + n_dense + n_sparse
+        self.rec_bytes = 4 * self.nf * batch_size
+        self.n_batches = os.path.getsize(data_file) // self.rec_bytes
+        if self.n_batches < 1:
+            raise ValueError("RecordPipeline: file holds less than one batch")
+        self.data_file = data_file
+        dev = trainer.dev
+        n = self.nf * batch_size
+        self.host = [torch.empty(n, dtype=torch.int32, pin_memory=True) for _ in range(self.depth)]
+        self.devs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(self.depth)]
+        self.copied = [torch.cuda.Event() for _ in range(self.depth)]
+        self.consumed = [torch.cuda.Event() for _ in range(self.depth)]
+        self.copy_stream = torch.cuda.Stream(device=dev)
+        self.batch = trainer.record_batch(batch_size)
+        self._free = [threading.Semaphore(1) for _ in range(self.depth)]  # host slot refillable
+        self._filled = queue.Queue()
+        self._stop = False
+        self._k = 0            # next batch next() returns
+        self._issued = 0       # batches whose H2D copy has been enqueued
+        self._thread = threading.Thread(target=self._reader, daemon=True)
+        self._thread.start()
+
+    def _reader(self):
+        j = 0
+        with open(self.data_file, "rb", buffering=0) as f:
+            while not self._stop:
+                b = j % self.n_batches
+                if b == 0 and j > 0 and not self.loop:
+                    self._filled.put(None)
+                    return
+                i = j % self.depth
+                self._free[i].acquire()
+                if self._stop:
+                    return
+                self.copied[i].synchronize()  # the slot's previous H2D copy has finished
+                f.seek(b * self.rec_bytes)
+                mv = memoryview(self.host[i].numpy()).cast("B")
+                got = f.readinto(mv)
+                if got != self.rec_bytes:
+                    raise IOError(f"RecordPipeline: short read ({got} of {self.rec_bytes} B)")
+                self._filled.put(i)
+                j += 1
+
+    def _issue_copy(self):
+        i = self._filled.get()
+        if i is None:
+            return False
+        cs = self.copy_stream
+        cs.wait_event(self.consumed[i])  # the device slot's previous decode is done
+        with torch.cuda.stream(cs):
+            self.devs[i].copy_(self.host[i], non_blocking=True)
+            self.copied[i].record(cs)
+        self._free[i].release()  # the reader refills after copied[i] completes
+        self._issued += 1
+        return True
+
+    def next(self):
+        """The next global batch, decoded into the trainer's fixed record Batch on the current
+        stream (the H2D copy of the batch after it is already in flight)."""
+        while self._issued <= self._k + 1:
+            if not self._issue_copy():
+                if self._issued <= self._k:
+                    raise StopIteration
+                break
+        i = self._k % self.depth
+        st = torch.cuda.current_stream(self.trainer.dev)
+        st.wait_event(self.copied[i])
+        self.trainer.decode_into(self.devs[i], self.batch, self.max_ind_range)
+        self.consumed[i].record(st)
+        self._k += 1
+        return self.batch
+
+    def close(self):
+        self._stop = True
+        for s in self._free:
+            s.release()
+        self._thread.join(timeout=5)
+
+
 def numpy_to_binary(input_files, output_file_path, split="train"):
     """Write day_*_reordered.npz files as int32 records [y | X_int | X_cat]
     (data_loader_terabyte.py:255-293): train concatenates every file; test / val take the

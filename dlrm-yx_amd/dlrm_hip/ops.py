@@ -616,13 +616,17 @@ def csr_from_tables(table_offsets: Sequence[torch.Tensor], table_nnz: Sequence[i
 
 def criteo_decode(records: torch.Tensor, n_dense: int = 13, n_sparse: int = 26,
                   max_ind_range: int = -1, batched: bool = False,
-                  dense: Optional[torch.Tensor] = None):
+                  dense: Optional[torch.Tensor] = None, label: Optional[torch.Tensor] = None,
+                  indices: Optional[torch.Tensor] = None,
+                  offsets: Optional[torch.Tensor] = None):
     """Device decode of raw Criteo binary records int32 [n, 1+n_dense+n_sparse]
     (dlrm_criteo_decode; data_loader_terabyte.py:83-114).  Returns (dense [n, n_dense]
     log(x+1), lS_o, lS_i, label [n, 1]) in the reference's layouts: batched -> int32
     offsets [T*n+1] and int32 indices [T*n]; else int64 lS_o [T, n] = arange and int64
-    lS_i [T, n].  ``dense`` may be a caller buffer (row stride >= n_dense)."""
-    _check_cuda(records, dense)
+    lS_i [T, n].  ``dense`` may be a caller buffer (row stride >= n_dense); so may
+    ``label`` (n fp32), ``indices`` and (batched) ``offsets``, e.g. the fixed buffers a
+    captured step graph reads."""
+    _check_cuda(records, dense, label, indices, offsets)
     nf = 1 + n_dense + n_sparse
     if records.dtype != torch.int32 or not records.is_contiguous() or records.numel() % nf:
         raise ValueError(f"criteo_decode: need contiguous int32 records of {nf} fields")
@@ -632,10 +636,19 @@ def criteo_decode(records: torch.Tensor, n_dense: int = 13, n_sparse: int = 26,
         dense = torch.empty((n, n_dense), dtype=torch.float32, device=dev)
     elif dense.shape[0] != n or dense.shape[1] < n_dense or dense.stride(1) != 1:
         raise ValueError("criteo_decode: dense buffer must be [n, >= n_dense] row-major")
-    label = torch.empty((n, 1), dtype=torch.float32, device=dev)
     idt = torch.int32 if batched else torch.int64
-    indices = torch.empty(n_sparse * n, dtype=idt, device=dev)
-    offsets = torch.empty(n_sparse * n + 1, dtype=torch.int32, device=dev) if batched else None
+    if label is None:
+        label = torch.empty((n, 1), dtype=torch.float32, device=dev)
+    if indices is None:
+        indices = torch.empty(n_sparse * n, dtype=idt, device=dev)
+    if offsets is None and batched:
+        offsets = torch.empty(n_sparse * n + 1, dtype=torch.int32, device=dev)
+    if (label.numel() != n or label.dtype != torch.float32 or not label.is_contiguous()
+            or indices.numel() != n_sparse * n or indices.dtype != idt
+            or not indices.is_contiguous()
+            or (batched and (offsets.numel() != n_sparse * n + 1 or offsets.dtype != torch.int32
+                             or not offsets.is_contiguous()))):
+        raise ValueError("criteo_decode: label / indices / offsets buffers of the wrong shape")
     _lib.call("dlrm_criteo_decode", _p(records), n, n_dense, n_sparse, int(max_ind_range),
               _p(dense), dense.stride(0) if n else n_dense, _p(label), _p(indices),
               32 if batched else 64, _p(offsets), 32, _stream(dev))

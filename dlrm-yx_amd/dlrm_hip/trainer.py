@@ -299,6 +299,58 @@ class DLRMTrainer:
         return Batch(dense[sl].contiguous() if Bl != B else dense, offsets, indices,
                      label.reshape(-1)[sl].contiguous(), B)
 
+    def record_batch(self, B: int) -> Batch:
+        """Fixed device buffers for global batches of B Criteo records (L = 1), filled by
+        ``decode_into`` (data.RecordPipeline): the tensors keep their addresses, so a step
+        graph captured on this Batch replays on every decoded batch."""
+        Bl = self.local_batch_size(B)
+        L0 = self.bot[0]
+        X = torch.zeros((Bl, L0.Kp), dtype=torch.float32, device=self.dev)
+        X[:, L0.K] = 1.0  # bias column
+        offsets = torch.arange(0, self.T_local * B + 1, dtype=torch.int32, device=self.dev)
+        indices = torch.zeros(self.T_local * B, dtype=torch.int32, device=self.dev)
+        target = torch.zeros(Bl, dtype=torch.float32, device=self.dev)
+        if self.world > 1 or self.T_local != self.T:  # full-batch decode scratch
+            full = torch.zeros((B, L0.Kp), dtype=torch.float32, device=self.dev)
+            self._rec_scratch = dict(
+                X=full, label=torch.empty(B, dtype=torch.float32, device=self.dev),
+                indices=torch.empty(self.T * B, dtype=torch.int32, device=self.dev),
+                offsets=torch.empty(self.T * B + 1, dtype=torch.int32, device=self.dev),
+                tables=torch.tensor(self.local_tables, dtype=torch.int64, device=self.dev))
+        return Batch(X, offsets, indices, target, B)
+
+    def decode_into(self, records: torch.Tensor, batch: Batch, max_ind_range: int = -1) -> Batch:
+        """Decode device records int32 [B * (1 + m_den + T)] into ``batch`` (from
+        ``record_batch``) on the current stream: one dlrm_criteo_decode launch (plus, on
+        several ranks, the copies of this rank's batch slice and local tables).  Enqueues
+        only; capturable."""
+        L0 = self.bot[0]
+        B = batch.max_per_table
+        Bl = batch.X.shape[0]
+        if self.world == 1 and self.T_local == self.T:
+            ops.criteo_decode(records, L0.K, self.T, max_ind_range, batched=True,
+                              dense=batch.X, label=batch.target, indices=batch.indices,
+                              offsets=self._rec_offsets(B))
+            return batch
+        sc = self._rec_scratch
+        ops.criteo_decode(records, L0.K, self.T, max_ind_range, batched=True, dense=sc["X"],
+                          label=sc["label"], indices=sc["indices"], offsets=sc["offsets"])
+        sl = slice(self.rank * Bl, (self.rank + 1) * Bl)
+        batch.X[:, :L0.K].copy_(sc["X"][sl, :L0.K])
+        batch.target.copy_(sc["label"][sl])
+        torch.index_select(sc["indices"].view(self.T, B), 0, sc["tables"],
+                           out=batch.indices.view(self.T_local, B))
+        return batch
+
+    def _rec_offsets(self, B: int) -> torch.Tensor:
+        # the decode rewrites the L = 1 CSR offsets (arange); a private buffer keeps the
+        # batch's own copy untouched while a graph may be reading it
+        t = self._rec_off.get(B) if hasattr(self, "_rec_off") else None
+        if t is None:
+            self._rec_off = getattr(self, "_rec_off", {})
+            t = self._rec_off[B] = torch.empty(self.T * B + 1, dtype=torch.int32, device=self.dev)
+        return t
+
     def synthetic_batch(self, B: int, L: int, seed: int) -> Batch:
         """Device-generated synthetic batch of the reference's shape: X ~ log(1+U[0,1))
         (dlrm_data_pytorch.py:727), L uniform indices per bag per table, targets U[0,1)

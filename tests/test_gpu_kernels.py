@@ -805,3 +805,80 @@ def test_tbe_forward_presort_with_bottom_chain(ops):
                      max_lookups_per_table=B, presorted=True)
     ops.tbe_backward("sgd", Wb, row_base, T, B, idx, off, G, lr=0.1, max_lookups_per_table=B)
     assert torch.equal(Wa, Wb)
+
+
+def _tbe_bwd_case(rows, B, L, D, seed, invalid=False, idx_dtype=torch.int32):
+    torch.manual_seed(seed)
+    T = len(rows)
+    lo = [torch.arange(B) * L for _ in rows]
+    li = [torch.randint(0, n, (B * L,)) for n in rows]
+    if invalid:
+        li[0][7] = 10 ** 9
+        li[-1][B * L - 1] = -1
+    off, idx = O.batched_csr(lo, li)
+    if invalid:  # lookups after the last bag
+        idx = torch.cat([idx, torch.tensor([1, 2, 3], dtype=idx.dtype)])
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    G = torch.randn(B, T, D, device=dev)
+    return T, lo, li, off.to(idx_dtype).to(dev), idx.to(idx_dtype).to(dev), row_base, G
+
+
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad", "dense"])
+@pytest.mark.parametrize("invalid", [False, True])
+@pytest.mark.parametrize("idx_dtype", [torch.int32, torch.int64])
+def test_tbe_backward_tiled_sort(ops, mode, invalid, idx_dtype, monkeypatch):
+    """Tables with more than 4096 lookups (L = 100 pooling): the tiled per-table radix sort
+    gives bitwise the updates of the device-wide sort when every index is valid (same
+    (row, position) order), and matches the fp64 coalesced reference either way; skewed
+    (3-row) and large tables, 10-bit digits (2^17 rows)."""
+    rows, B, L, D = [64, 130000, 700, 9000], 256, 40, 64
+    T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 5, invalid, idx_dtype)
+    W0 = torch.randn(sum(rows), D, device=dev) * 0.1
+    mom0 = torch.rand(sum(rows), device=dev)
+    res = []
+    for tiled in ("1", "0"):
+        monkeypatch.setenv("DLRM_TBE_TILED_SORT", tiled)
+        W = W0.clone() if mode != "dense" else torch.zeros_like(W0)
+        mom = mom0.clone()
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8, momentum=mom,
+                         max_lookups_per_table=B * L, error_flag=flag)
+        torch.cuda.synchronize()
+        assert (int(flag.item()) != 0) == invalid
+        res.append((W.cpu(), mom.cpu()))
+    if not invalid:
+        assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    gsum = torch.zeros(sum(rows), D, dtype=torch.float64)
+    gt = G.cpu().double()
+    bag = torch.arange(B * L) // L
+    for t in range(T):
+        r = li[t]
+        ok_ = (r >= 0) & (r < rows[t])
+        gsum.index_add_(0, int(row_base[t]) + r[ok_], gt[bag[ok_], t])
+    if mode == "dense":
+        ref = gsum
+    elif mode == "sgd":
+        ref = W0.cpu().double() - 0.3 * gsum
+    else:
+        touched = gsum.abs().sum(1) > 0
+        m = mom0.cpu().double() + torch.where(touched, (gsum ** 2).mean(1),
+                                              torch.zeros(1, dtype=torch.float64))
+        ref = W0.cpu().double() - 0.3 * gsum / (m.sqrt()[:, None] + 1e-8)
+    for W, _ in res:
+        ok, msg = fp32_close(W.numpy(), ref.numpy())
+        assert ok, msg
+
+
+def test_tbe_backward_tiled_sort_cap_violation(ops):
+    """max_lookups_per_table underestimated (tiles cover 8192 of a table's 12800 lookups):
+    that table is skipped (no update) and flagged; the others are updated."""
+    rows, B, L, D = [5000, 6000], 128, 100, 16
+    T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 9)
+    W0 = torch.randn(sum(rows), D, device=dev)
+    W = W0.clone()
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.tbe_backward("sgd", W, row_base, T, B, idx, off, G, lr=0.5,
+                     max_lookups_per_table=8000, error_flag=flag)
+    torch.cuda.synchronize()
+    assert int(flag.item()) & 2  # TBE_ERR_TABLE_CAP
+    assert torch.equal(W, W0)  # both tables overflow their 2 tiles: nothing updated
