@@ -137,3 +137,53 @@ def test_trainer_batch_from_records_matches_make_batch():
     for a, b in zip(out[0], out[1]):
         ok, msg = fp32_close(a, b)
         assert ok, msg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_record_pipeline_matches_batch_from_records(tmp_path, graph):
+    """RecordPipeline (file -> pinned slot -> copy stream -> decode into a fixed Batch) feeds
+    the same training as batch_from_records on the same blocks, bitwise: eager steps, or a
+    step graph captured once on the pipeline's Batch and replayed per decoded batch.  The
+    file wraps around (5 full batches + a partial one that is skipped) for 8 steps."""
+    from dlrm_hip.data import RecordPipeline
+    from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+    rng = np.random.RandomState(23)
+    B, mir, nb = 128, 1000, 5
+    rec = rng.randint(0, 1 << 20, (B * nb + 17, 40)).astype(np.int32)
+    rec[:, 0] = rng.randint(0, 2, rec.shape[0])
+    path = tmp_path / "train.bin"
+    rec.tofile(path)
+    cfg = TrainerConfig(m_spa=4, ln_emb=[mir] * 26, ln_bot=[13, 16, 4],
+                        ln_top=[4 + 27 * 26 // 2, 8, 1], loss_function="bce",
+                        learning_rate=0.1)
+    steps = 8
+    ref = DLRMTrainer(cfg, device="cuda:0", seed=3)
+    losses_ref = []
+    for k in range(steps):
+        blk = torch.from_numpy(rec[(k % nb) * B:(k % nb + 1) * B]).cuda()
+        _, E = ref.step(ref.batch_from_records(blk, max_ind_range=mir))
+        losses_ref.append(float(E.item()))
+    tr = DLRMTrainer(cfg, device="cuda:0", seed=3)
+    pipe = RecordPipeline(str(path), B, tr, max_ind_range=mir, depth=3)
+    assert pipe.n_batches == nb
+    losses = []
+    try:
+        if graph:
+            batch = pipe.next()
+            _, E = tr.step(batch)  # eager step of this batch size (allocations)
+            losses.append(float(E.item()))
+            run = tr.capture(batch)
+            for _ in range(steps - 1):
+                pipe.next()
+                run()
+                losses.append(float(tr._cur["loss"].item()))
+        else:
+            for _ in range(steps):
+                _, E = tr.step(pipe.next())
+                losses.append(float(E.item()))
+    finally:
+        pipe.close()
+    torch.cuda.synchronize()
+    assert losses == losses_ref
+    assert torch.equal(tr.weights, ref.weights)
