@@ -39,10 +39,13 @@ CONFIGS = {
     "terabyte": dict(workload="mlperf_terabyte_synthetic", rows=TERABYTE_ROWS, D=128,
                      bot=[13, 512, 256, 128], top=[1024, 1024, 512, 256, 1], B=2048, L=1,
                      loss="bce", lr=1.0, optimizer="sgd"),
-    "terabyte_qr_rwsadagrad": dict(workload="mlperf_terabyte_synthetic+rwsadagrad",
+    # C4: --qr-flag --qr-collisions=4 --qr-operation=mult --qr-threshold=200
+    # --optimizer=rwsadagrad
+    "terabyte_qr_rwsadagrad": dict(workload="mlperf_terabyte_synthetic+qr+rwsadagrad",
                                    rows=TERABYTE_ROWS, D=128, bot=[13, 512, 256, 128],
                                    top=[1024, 1024, 512, 256, 1], B=2048, L=1, loss="bce",
-                                   lr=1.0, optimizer="rwsadagrad"),
+                                   lr=1.0, optimizer="rwsadagrad",
+                                   qr=dict(collisions=4, operation="mult", threshold=200)),
     "small": dict(workload="synthetic_small", rows=[100000] * 8, D=64, bot=[512, 512, 64],
                   top=[1024, 1024, 1024, 1], B=2048, L=100, loss="mse", lr=0.1, optimizer="sgd"),
     "kaggle": dict(workload="criteo_kaggle_synthetic", rows=KAGGLE_ROWS, D=16,
@@ -198,7 +201,7 @@ def gather_rooflines(tr, batch, B, c, dev):
     D, L = c["D"], c["L"]
     T = tr.T_local
     out = {}
-    if T > 0:
+    if T > 0 and not tr.qr_active:  # (QR: the lookup runs on the expanded physical CSR)
         pooled = torch.empty(B, T, D, device=dev)
         us = _graph_time_us(lambda: ops.tbe_forward(tr.weights, tr.row_base, T, B, batch.indices,
                                                     batch.offsets, out=pooled))
@@ -306,6 +309,12 @@ def cpu_baseline(c, seconds: float):
         tables.append(torch.empty(n, D).uniform_(-a, a, generator=g).numpy())
     np.random.seed(0)
     m = O.OracleDLRM(D, rows, c["bot"], ln_top, loss_function=c["loss"], tables=tables)
+    qr = c.get("qr")
+    if qr:  # QR tables with the capped row counts
+        torch.manual_seed(0)
+        for k, n in enumerate(rows):
+            if n > qr["threshold"]:
+                m.emb_l[k] = O.QREmbeddingBagOracle(n, D, qr["collisions"], qr["operation"])
     rng = np.random.RandomState(1)
     batches = []
     for _ in range(4):
@@ -364,9 +373,13 @@ def main():
     B = args.batch or c["B"]
     T = len(c["rows"])
     ln_top = [num_int(T, c["D"])] + c["top"]
+    qr = c.get("qr")
     cfg = TrainerConfig(m_spa=c["D"], ln_emb=c["rows"], ln_bot=c["bot"], ln_top=ln_top,
                         loss_function=c["loss"], learning_rate=c["lr"], optimizer=c["optimizer"],
-                        sharder="greedy")
+                        sharder="greedy", qr_flag=qr is not None,
+                        qr_collisions=qr["collisions"] if qr else 4,
+                        qr_operation=qr["operation"] if qr else "mult",
+                        qr_threshold=qr["threshold"] if qr else 200)
     tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, process_group=pg, seed=1)
     nb = 10  # the reference cycles 10 pre-generated batches (dlrm_data_pytorch.py:631)
     batches = [tr.synthetic_batch(B, c["L"], seed=100 + i) for i in range(nb)]
@@ -426,7 +439,8 @@ def main():
     # ---- per-kernel HIP-event timing pass (same step, eager launches) for the roofline
     roofline, emb_roof, groups = None, None, None
     Bl = B // world
-    flops, fwd_bytes, bwd_bytes = algorithmic_work(c, Bl, B, tr.T_local, world,
+    # lookups run on the physical tables (a QR table is a quotient + a remainder table)
+    flops, fwd_bytes, bwd_bytes = algorithmic_work(c, Bl, B, tr.T_phys, world,
                                                    bottom_fused=tr.bottom_fused)
     if not args.no_kernel_timing:
         # capture one eager step's launches per kernel group (after the timed region: the
@@ -491,7 +505,8 @@ def main():
             "config": {"workload": c["workload"], "global_batch": B, "local_batch": Bl,
                        "tables": T, "rows_total": int(sum(c["rows"])), "emb_dim": c["D"],
                        "lookups_per_bag": c["L"], "bot": c["bot"], "top": ln_top,
-                       "optimizer": c["optimizer"], "parallelism": f"table-sharded emb x{world} + dp{world}",
+                       "optimizer": c["optimizer"], "qr": c.get("qr"),
+                       "parallelism": f"table-sharded emb x{world} + dp{world}",
                        "hip_graph": use_graph},
             "loss_last": loss,
             "roofline": roofline,

@@ -1090,11 +1090,14 @@ int env_int(const char* name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
-// Math of the pipelined GEMMs: exact-f32 MFMA (default) or the split-bf16 body
-// (DLRM_GEMM_MATH=x6).  Read per call, like the tuning overrides.
-bool gemm_x6() {
+// Math of the pipelined GEMMs: exact-f32 MFMA, or the split-bf16 body where the plan table
+// measured it faster and every GEMM of the launch agrees (default "auto"); DLRM_GEMM_MATH=
+// f32 / x6 forces one everywhere.  Read per call, like the tuning overrides.
+int gemm_math_env() {  // 0 f32, 1 x6, -1 auto
   const char* v = getenv("DLRM_GEMM_MATH");
-  return v && strcmp(v, "x6") == 0;
+  if (v && strcmp(v, "x6") == 0) return 1;
+  if (v && strcmp(v, "f32") == 0) return 0;
+  return -1;
 }
 
 Plan make_plan(int64_t s, int64_t K) {
@@ -1149,6 +1152,7 @@ struct PlanEntry {
   int64_t M, N, K;
   int layout, bm, bn, split;
   int wm = 2, wn = 2;
+  int x6 = 0;  // 1: the split-bf16 body measured faster (tools/gemm_x6_ab.py)
 };
 
 // Measured plans for the DLRM step shapes of single-problem launches (exact match), from
@@ -1169,6 +1173,7 @@ bool tile_ok(int bm, int bn, int wm, int wn) {
 
 struct Tile {
   int bm = 64, bn = 32, wm = 2, wn = 2;
+  int x6 = 0;  // math vote of a problem / the launch's math
   bool operator==(const Tile& o) const {
     return bm == o.bm && bn == o.bn && wm == o.wm && wn == o.wn;
   }
@@ -1205,7 +1210,7 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
   if (!getenv("DLRM_GEMM_NOTABLE"))
     for (const PlanEntry& e : kPlans)
       if (e.M == d.M && e.N == d.N && e.K == d.K && e.layout == layout_of(d)) {
-        t = Tile{e.bm, e.bn, e.wm, e.wn};
+        t = Tile{e.bm, e.bn, e.wm, e.wn, e.x6};
         pl = make_plan(e.split, d.K);
         return;
       }
@@ -1226,10 +1231,13 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
 void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   bool first = true;
   t = Tile{64, 64, 2, 2};
+  int votes = 0, gemms = 0;
   for (int i = 0; i < n; ++i) {
     Tile a;
     plan_one(d[i], a, pl[i]);
     if (d[i].mode == DLRM_GEMM_REDUCE) continue;
+    ++gemms;
+    votes += a.x6;
     if (first) {
       t = a;
       first = false;
@@ -1237,7 +1245,9 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
       t = Tile{64, 32, 2, 2};
     }
   }
-  if (gemm_x6() && (t.bm == 128 || t.bn == 128)) t = Tile{64, 64, 2, 2};
+  const int env = gemm_math_env();
+  t.x6 = env >= 0 ? env : (gemms > 0 && votes == gemms);
+  if (t.x6 && (t.bm == 128 || t.bn == 128)) t = Tile{64, 64, 2, 2, 1};
 }
 
 // Split-K workspace: the fixed 64 KiB ticket head, then each problem's records.
@@ -1430,7 +1440,7 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
   if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: every problem unsplit
     for (int i = 0; i < m; ++i) pl[i] = make_plan(1, q[i].K);
   }
-  if (gemm_x6()) {  // split-bf16 body: 128-wide tiles stage too much per K-tile
+  if (t.x6) {  // split-bf16 body: 128-wide tiles stage too much per K-tile
     if (t.bm == 32) return launch_group<32, 64, true>(m, q, pl, ws, ws_bytes, st);
     if (t.bn == 32) return launch_group<64, 32, true>(m, q, pl, ws, ws_bytes, st);
     return launch_group<64, 64, true>(m, q, pl, ws, ws_bytes, st);

@@ -259,6 +259,164 @@ extern "C" int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* 
                                       per_sample_weights, out, out_batch_stride, error_flag, st);
 }
 
+// Table-batched QR (the fused engine's QR tables): logical CSR -> physical CSR.  Physical
+// table p takes logical table src[p]'s bags; its indices are the logical ones (kind 0), the
+// quotients (kind 1) or the remainders (kind 2) by coll[p].  Grid: x over the larger of a
+// table's lookups and its bags (grid-stride), y = physical table.
+template <typename IdxT, typename OffT>
+__global__ __launch_bounds__(256) void qr_expand_kernel(
+    int T_phys, int B, const IdxT* __restrict__ idx, const OffT* __restrict__ off,
+    const int32_t* __restrict__ src, const int32_t* __restrict__ kind,
+    const int32_t* __restrict__ coll, int32_t* __restrict__ pidx, int32_t* __restrict__ poff) {
+  const int p = blockIdx.y;
+  const int j = src[p];
+  const int64_t s = (int64_t)off[(int64_t)j * B];
+  const int64_t len = (int64_t)off[(int64_t)(j + 1) * B] - s;
+  int64_t base = 0;  // lookups of the physical tables before p
+  for (int q = 0; q < p; ++q)
+    base += (int64_t)off[(int64_t)(src[q] + 1) * B] - (int64_t)off[(int64_t)src[q] * B];
+  const int k = kind[p];
+  const int64_t c = coll[p];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t lim = len > B ? len : B;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += stride) {
+    if (i < len) {
+      const int64_t v = (int64_t)idx[s + i];
+      int64_t o = v;
+      if (k == 1) {
+        o = (int64_t)((float)v / (float)c);  // (input / num_collisions).long()
+      } else if (k == 2) {
+        o = v % c;  // torch.remainder: sign of the divisor
+        if (o != 0 && ((o < 0) != (c < 0))) o += c;
+      }
+      pidx[base + i] = (int32_t)o;
+    }
+    if (i < B) poff[(int64_t)p * B + i] = (int32_t)(base + (int64_t)off[(int64_t)j * B + i] - s);
+  }
+  if (p == T_phys - 1 && blockIdx.x == 0 && threadIdx.x == 0)
+    poff[(int64_t)T_phys * B] = (int32_t)(base + len);
+}
+
+// E[b][t] = op(P[b][pq[t]], P[b][pr[t]]) for QR tables (pr[t] >= 0), P[b][pq[t]] otherwise.
+__global__ __launch_bounds__(256) void qr_pool_fwd_kernel(int op, int T, int64_t B, int64_t D4,
+                                                          const int32_t* __restrict__ pq,
+                                                          const int32_t* __restrict__ pr,
+                                                          const float4* __restrict__ P,
+                                                          int64_t pbs4, float4* __restrict__ E,
+                                                          int64_t ebs4) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per_b = (int64_t)T * D4;
+  if (i >= B * per_b) return;
+  const int64_t b = i / per_b, r = i - b * per_b, t = r / D4, d = r - t * D4;
+  const float4 a = P[b * pbs4 + (int64_t)pq[t] * D4 + d];
+  float4 o = a;
+  if (pr[t] >= 0) {
+    const float4 c = P[b * pbs4 + (int64_t)pr[t] * D4 + d];
+    if (op == DLRM_QR_MULT)
+      o = make_float4(a.x * c.x, a.y * c.y, a.z * c.z, a.w * c.w);
+    else
+      o = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w);
+  }
+  E[b * ebs4 + t * D4 + d] = o;
+}
+
+__global__ __launch_bounds__(256) void qr_pool_bwd_kernel(int op, int T, int64_t B, int64_t D4,
+                                                          const int32_t* __restrict__ pq,
+                                                          const int32_t* __restrict__ pr,
+                                                          const float4* __restrict__ P,
+                                                          int64_t pbs4,
+                                                          const float4* __restrict__ dE,
+                                                          int64_t ebs4, float4* __restrict__ dP,
+                                                          int64_t dpbs4) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per_b = (int64_t)T * D4;
+  if (i >= B * per_b) return;
+  const int64_t b = i / per_b, r = i - b * per_b, t = r / D4, d = r - t * D4;
+  const float4 g = dE[b * ebs4 + t * D4 + d];
+  const int64_t oq = (int64_t)pq[t] * D4 + d;
+  if (pr[t] < 0) {
+    dP[b * dpbs4 + oq] = g;
+    return;
+  }
+  const int64_t orr = (int64_t)pr[t] * D4 + d;
+  if (op == DLRM_QR_MULT) {
+    const float4 a = P[b * pbs4 + oq], c = P[b * pbs4 + orr];
+    dP[b * dpbs4 + oq] = make_float4(g.x * c.x, g.y * c.y, g.z * c.z, g.w * c.w);
+    dP[b * dpbs4 + orr] = make_float4(g.x * a.x, g.y * a.y, g.z * a.z, g.w * a.w);
+  } else {
+    dP[b * dpbs4 + oq] = g;
+    dP[b * dpbs4 + orr] = g;
+  }
+}
+
+extern "C" int dlrm_qr_expand_csr(int32_t T_phys, int32_t B, const void* indices,
+                                  int32_t index_bits, const void* offsets, int32_t offset_bits,
+                                  const int32_t* src, const int32_t* kind, const int32_t* coll,
+                                  int64_t max_lookups_per_table, int32_t* phys_indices,
+                                  int32_t* phys_offsets, dlrm_stream_t stream) {
+  DLRM_ARG(T_phys > 0 && B > 0, "dlrm_qr_expand_csr: bad sizes");
+  DLRM_ARG(indices && offsets && src && kind && coll && phys_indices && phys_offsets,
+           "dlrm_qr_expand_csr: null pointer");
+  DLRM_ARG(index_bits == 32 || index_bits == 64, "dlrm_qr_expand_csr: bad index_bits");
+  DLRM_ARG(offset_bits == 32 || offset_bits == 64, "dlrm_qr_expand_csr: bad offset_bits");
+  const int64_t per = max_lookups_per_table > B ? max_lookups_per_table : B;
+  int64_t bx = dlrm::ceil_div(per, 256);
+  if (bx > 4096) bx = 4096;  // grid-stride beyond
+  const dim3 grid((unsigned)bx, (unsigned)T_phys), block(256);
+  hipStream_t st = dlrm::as_stream(stream);
+#define QX(I, O)                                                                              \
+  hipLaunchKernelGGL((qr_expand_kernel<I, O>), grid, block, 0, st, T_phys, B,                  \
+                     static_cast<const I*>(indices), static_cast<const O*>(offsets), src, kind, \
+                     coll, phys_indices, phys_offsets)
+  if (index_bits == 32 && offset_bits == 32) QX(int32_t, int32_t);
+  else if (index_bits == 32) QX(int32_t, int64_t);
+  else if (offset_bits == 32) QX(int64_t, int32_t);
+  else QX(int64_t, int64_t);
+#undef QX
+  DLRM_LAUNCH_CHECK("dlrm_qr_expand_csr");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_qr_pool_combine_forward(int32_t op, int32_t T, int64_t B, int64_t D,
+                                            const int32_t* pq, const int32_t* pr, const float* P,
+                                            int64_t p_batch_stride, float* E,
+                                            int64_t e_batch_stride, dlrm_stream_t stream) {
+  DLRM_ARG(op == DLRM_QR_MULT || op == DLRM_QR_ADD, "dlrm_qr_pool_combine_forward: mult or add");
+  DLRM_ARG(T > 0 && B >= 0 && D > 0 && D % 4 == 0 && p_batch_stride % 4 == 0 &&
+               e_batch_stride % 4 == 0,
+           "dlrm_qr_pool_combine_forward: bad sizes (D and strides multiples of 4)");
+  if (B == 0) return DLRM_OK;
+  DLRM_ARG(pq && pr && P && E, "dlrm_qr_pool_combine_forward: null pointer");
+  const int64_t n = B * T * (D / 4);
+  hipLaunchKernelGGL(qr_pool_fwd_kernel, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0,
+                     dlrm::as_stream(stream), op, T, B, D / 4, pq, pr,
+                     reinterpret_cast<const float4*>(P), p_batch_stride / 4,
+                     reinterpret_cast<float4*>(E), e_batch_stride / 4);
+  DLRM_LAUNCH_CHECK("dlrm_qr_pool_combine_forward");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_qr_pool_combine_backward(int32_t op, int32_t T, int64_t B, int64_t D,
+                                             const int32_t* pq, const int32_t* pr, const float* P,
+                                             int64_t p_batch_stride, const float* dE,
+                                             int64_t e_batch_stride, float* dP,
+                                             int64_t dp_batch_stride, dlrm_stream_t stream) {
+  DLRM_ARG(op == DLRM_QR_MULT || op == DLRM_QR_ADD, "dlrm_qr_pool_combine_backward: mult or add");
+  DLRM_ARG(T > 0 && B >= 0 && D > 0 && D % 4 == 0 && p_batch_stride % 4 == 0 &&
+               e_batch_stride % 4 == 0 && dp_batch_stride % 4 == 0,
+           "dlrm_qr_pool_combine_backward: bad sizes (D and strides multiples of 4)");
+  if (B == 0) return DLRM_OK;
+  DLRM_ARG(pq && pr && P && dE && dP, "dlrm_qr_pool_combine_backward: null pointer");
+  const int64_t n = B * T * (D / 4);
+  hipLaunchKernelGGL(qr_pool_bwd_kernel, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0,
+                     dlrm::as_stream(stream), op, T, B, D / 4, pq, pr,
+                     reinterpret_cast<const float4*>(P), p_batch_stride / 4,
+                     reinterpret_cast<const float4*>(dE), e_batch_stride / 4,
+                     reinterpret_cast<float4*>(dP), dp_batch_stride / 4);
+  DLRM_LAUNCH_CHECK("dlrm_qr_pool_combine_backward");
+  return DLRM_OK;
+}
+
 extern "C" int dlrm_qr_split_indices(const void* indices, int32_t index_bits, int64_t n,
                                      int64_t collisions, int64_t* q_out, int64_t* r_out,
                                      dlrm_stream_t stream) {

@@ -293,6 +293,33 @@ def qr_combine_backward(op: str, eq: torch.Tensor, er: torch.Tensor, grad_out: t
     return geq, ger
 
 
+def qr_expand_csr(T_phys: int, B: int, indices: torch.Tensor, offsets: torch.Tensor,
+                  src: torch.Tensor, kind: torch.Tensor, coll: torch.Tensor,
+                  max_lookups_per_table: int, phys_indices: torch.Tensor,
+                  phys_offsets: torch.Tensor) -> None:
+    """Logical table-batched CSR -> the physical CSR of the QR engine (dlrm_qr_expand_csr):
+    physical table p = logical table src[p]'s bags with its indices (kind 0), quotients
+    (kind 1) or remainders (kind 2) by coll[p]; int32 outputs."""
+    _check_cuda(indices, offsets, src, kind, coll, phys_indices, phys_offsets)
+    _lib.call("dlrm_qr_expand_csr", T_phys, B, _p(indices), _bits(indices), _p(offsets),
+              _bits(offsets), _p(src), _p(kind), _p(coll), int(max_lookups_per_table),
+              _p(phys_indices), _p(phys_offsets), _stream(indices.device))
+
+
+def qr_pool_combine_forward(op: str, T: int, B: int, D: int, pq: torch.Tensor, pr: torch.Tensor,
+                            P: torch.Tensor, E: torch.Tensor) -> None:
+    """E[b, t] = op(P[b, pq[t]], P[b, pr[t]]) (or P[b, pq[t]] where pr[t] < 0)."""
+    _lib.call("dlrm_qr_pool_combine_forward", QR_OPS[op], T, B, D, _p(pq), _p(pr), _p(P),
+              P.stride(0), _p(E), E.stride(0), _stream(P.device))
+
+
+def qr_pool_combine_backward(op: str, T: int, B: int, D: int, pq: torch.Tensor,
+                             pr: torch.Tensor, P: torch.Tensor, dE: torch.Tensor,
+                             dP: torch.Tensor) -> None:
+    _lib.call("dlrm_qr_pool_combine_backward", QR_OPS[op], T, B, D, _p(pq), _p(pr), _p(P),
+              P.stride(0), _p(dE), dE.stride(0), _p(dP), dP.stride(0), _stream(P.device))
+
+
 # ---------------------------------------------------------- interaction ----
 def _feature_arrays(feats: Sequence[torch.Tensor], strides: Sequence[int]):
     F = len(feats)

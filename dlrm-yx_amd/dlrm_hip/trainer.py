@@ -55,6 +55,13 @@ class TrainerConfig:
     adagrad_eps: float = 1e-10
     sharder: str = "greedy"
     allocation: Optional[Sequence[int]] = None
+    # QR compositional embeddings (--qr-flag, dlrm_s_pytorch.py:282-290): tables with more
+    # than qr_threshold rows become a quotient table (ceil(n/c) rows) and a remainder table
+    # (c rows) combined by qr_operation (mult | add)
+    qr_flag: bool = False
+    qr_collisions: int = 4
+    qr_operation: str = "mult"
+    qr_threshold: int = 200
 
 
 @dataclass
@@ -111,6 +118,39 @@ class DLRMTrainer:
         self.T_local = len(self.local_tables)
         rows = [int(cfg.ln_emb[t]) for t in self.local_tables]
         self.rows_local = rows
+        # physical tables: the local tables, with every QR table split into its quotient and
+        # remainder tables (the lookup runs on the physical CSR, a combine kernel forms the
+        # logical features; the a2a / interaction see logical tables only)
+        self.qr = bool(cfg.qr_flag)
+        if self.qr and cfg.qr_operation not in ("mult", "add"):
+            raise NotImplementedError("trainer QR: qr_operation mult or add (concat widens "
+                                      "the feature; the module path DLRM_Net has it)")
+        prow, psrc, pkind, pcoll, pq, pr = [], [], [], [], [], []
+        for j, n in enumerate(rows):
+            if self.qr and n > cfg.qr_threshold:
+                c = int(cfg.qr_collisions)
+                pq.append(len(prow))
+                prow.append(int(math.ceil(n / c)))
+                psrc.append(j), pkind.append(1), pcoll.append(c)
+                pr.append(len(prow))
+                prow.append(c)
+                psrc.append(j), pkind.append(2), pcoll.append(c)
+            else:
+                pq.append(len(prow))
+                pr.append(-1)
+                prow.append(n)
+                psrc.append(j), pkind.append(0), pcoll.append(1)
+        self.phys_rows, self.phys_src, self.phys_kind = prow, psrc, pkind
+        self.T_phys = len(prow)
+        self.qr_active = self.T_phys != self.T_local
+        i32 = dict(dtype=torch.int32, device=self.dev)
+        self._qr_src = torch.tensor(psrc, **i32)
+        self._qr_kind = torch.tensor(pkind, **i32)
+        self._qr_coll = torch.tensor(pcoll, **i32)
+        self._qr_pq = torch.tensor(pq, **i32)
+        self._qr_pr = torch.tensor(pr, **i32)
+        self._qr_csr = {}
+        rows = prow
         self.row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64,
                                      device=self.dev)
         self.total_rows = int(sum(rows))
@@ -191,11 +231,15 @@ class DLRMTrainer:
     def init_random(self, seed: int = 0):
         """Reference-distribution random init on device: tables U(+-sqrt(1/n))
         (dlrm_s_pytorch.py:304-308), W ~ N(0, sqrt(2/(m+n))), b ~ N(0, sqrt(1/m)) (:240-247)."""
-        for j, t in enumerate(self.local_tables):
+        for p, j in enumerate(self.phys_src):
+            t = self.local_tables[j]
             n = int(self.cfg.ln_emb[t])
             a = math.sqrt(1.0 / n)
-            view = self.weights[int(self.row_base[j].item()):int(self.row_base[j + 1].item())]
-            ops.uniform_fill_(view, -a, a, seed * 1000003 + t)
+            view = self.weights[int(self.row_base[p].item()):int(self.row_base[p + 1].item())]
+            if self.phys_kind[p] == 0:
+                ops.uniform_fill_(view, -a, a, seed * 1000003 + t)
+            else:  # QR tables: uniform [sqrt(1/n), 1] (tricks/qr_embedding_bag.py:153-154)
+                ops.uniform_fill_(view, a, 1.0, seed * 1000003 + t + 7919 * self.phys_kind[p])
         g = torch.Generator(device=self.dev)
         g.manual_seed(seed + 12345)
         with torch.no_grad():
@@ -211,10 +255,14 @@ class DLRMTrainer:
                 L.W.zero_()
                 L.W[:, :L.K].copy_(torch.as_tensor(W))
                 L.b.copy_(torch.as_tensor(b))
-            if tables is not None:
-                for j, t in enumerate(self.local_tables):
-                    s, e = int(self.row_base[j].item()), int(self.row_base[j + 1].item())
-                    self.weights[s:e].copy_(torch.as_tensor(tables[t]))
+            if tables is not None:  # QR tables: (weight_q, weight_r) pairs
+                for p, j in enumerate(self.phys_src):
+                    t = self.local_tables[j]
+                    s, e = int(self.row_base[p].item()), int(self.row_base[p + 1].item())
+                    src = tables[t]
+                    if self.phys_kind[p] != 0:
+                        src = src[self.phys_kind[p] - 1]
+                    self.weights[s:e].copy_(torch.as_tensor(src))
 
     @classmethod
     def from_oracle(cls, cfg: TrainerConfig, ref, device="cuda:0", **kw):
@@ -225,15 +273,20 @@ class DLRMTrainer:
             for m in seq:
                 if isinstance(m, torch.nn.Linear):
                     mlp.append((m.weight.detach(), m.bias.detach()))
-        tr.load_dense(mlp, [e.weight.detach() for e in ref.emb_l])
+        tabs = [(e.weight_q.detach(), e.weight_r.detach()) if hasattr(e, "weight_q")
+                else e.weight.detach() for e in ref.emb_l]
+        tr.load_dense(mlp, tabs)
         return tr
 
     def dense_state(self):
         return [(L.W[:, :L.K].detach().clone(), L.b.detach().clone()) for L in self.layers]
 
-    def table(self, t: int) -> torch.Tensor:
+    def table(self, t: int):
+        """Local table t's weights (a (quotient, remainder) pair for a QR table)."""
         j = self.local_tables.index(t)
-        return self.weights[int(self.row_base[j].item()):int(self.row_base[j + 1].item())]
+        views = [self.weights[int(self.row_base[p].item()):int(self.row_base[p + 1].item())]
+                 for p, jj in enumerate(self.phys_src) if jj == j]
+        return views[0] if len(views) == 1 else tuple(views)
 
     # ------------------------------------------------------------- batches --
     @property
@@ -405,6 +458,9 @@ class DLRMTrainer:
         bufs["gx"] = torch.zeros((Bl, D), **f32)
         bufs["E"] = torch.zeros((B, max(self.T_local, 1), D), **f32)
         bufs["dE"] = torch.zeros_like(bufs["E"])
+        if self.qr_active:  # pooled physical tables (quotient / remainder halves)
+            bufs["P"] = torch.zeros((B, self.T_phys, D), **f32)
+            bufs["dP"] = torch.zeros_like(bufs["P"])
         if self.world > 1:
             bufs["recv"] = torch.zeros(self.T * Bl * D, **f32)
             bufs["drecv"] = torch.zeros_like(bufs["recv"])
@@ -478,17 +534,20 @@ class DLRMTrainer:
 
         def lookup():  # embeddings (full batch, local tables)
             with prof("tbe_fwd"):
+                if self.T_local > 0:
+                    idx, off = st["csr"] = self._phys_csr(batch, B)
+                    out = bufs["P"] if self.qr_active else bufs["E"]
                 if self.T_local > 0 and presort:
                     # the backward's per-table sort runs inside the lookup launch
-                    ops.tbe_forward_presort(self.weights, self.row_base, self.T_local, B,
-                                            batch.indices, batch.offsets,
-                                            self._ws_tbe(batch.indices.numel()),
-                                            batch.max_per_table, out=bufs["E"],
+                    ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
+                                            off, self._ws_tbe(idx.numel()),
+                                            batch.max_per_table, out=out,
                                             error_flag=self.tbe_error_flag)
                 elif self.T_local > 0:
-                    ops.tbe_forward(self.weights, self.row_base, self.T_local, B, batch.indices,
-                                    batch.offsets, out=bufs["E"],
-                                    error_flag=self.tbe_error_flag)
+                    ops.tbe_forward(self.weights, self.row_base, self.T_phys, B, idx, off,
+                                    out=out, error_flag=self.tbe_error_flag)
+                if self.T_local > 0 and self.qr_active:
+                    self._qr_combine(bufs, B)
 
         def bottom_fwd():
             h = batch.X
@@ -502,11 +561,14 @@ class DLRMTrainer:
             if chain is not None:
                 # the bottom MLP forward runs as a role of the lookup launch
                 with prof("tbe_fwd"):
-                    ops.tbe_forward_presort(self.weights, self.row_base, self.T_local, B,
-                                            batch.indices, batch.offsets,
-                                            self._ws_tbe(batch.indices.numel()),
-                                            batch.max_per_table, out=bufs["E"],
+                    idx, off = st["csr"] = self._phys_csr(batch, B)
+                    ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
+                                            off, self._ws_tbe(idx.numel()),
+                                            batch.max_per_table,
+                                            out=bufs["P"] if self.qr_active else bufs["E"],
                                             error_flag=self.tbe_error_flag, bottom=chain)
+                    if self.qr_active:
+                        self._qr_combine(bufs, B)
                 return
             s0, s1 = streams()
             if c_fwd:
@@ -589,10 +651,16 @@ class DLRMTrainer:
             with prof("tbe_bwd"):
                 if self.T_local > 0:
                     mode = "rowwise_adagrad" if cfg.optimizer == "rwsadagrad" else "sgd"
-                    ops.tbe_backward(mode, self.weights, self.row_base, self.T_local, B,
-                                     batch.indices, batch.offsets, bufs["dE"], lr=elr,
-                                     eps=cfg.adagrad_eps, momentum=self.momentum,
-                                     workspace=self._ws_tbe(batch.indices.numel()),
+                    idx, off = st["csr"]
+                    grad = bufs["dE"]
+                    if self.qr_active:
+                        ops.qr_pool_combine_backward(cfg.qr_operation, self.T_local, B, D,
+                                                     self._qr_pq, self._qr_pr, bufs["P"],
+                                                     bufs["dE"], bufs["dP"])
+                        grad = bufs["dP"]
+                    ops.tbe_backward(mode, self.weights, self.row_base, self.T_phys, B, idx, off,
+                                     grad, lr=elr, eps=cfg.adagrad_eps, momentum=self.momentum,
+                                     workspace=self._ws_tbe(idx.numel()),
                                      max_lookups_per_table=batch.max_per_table,
                                      error_flag=self.tbe_error_flag, presorted=presort)
 
@@ -647,6 +715,32 @@ class DLRMTrainer:
             ("gpu", dense_update),
             ("comm", done),
         ]
+
+    def _phys_csr(self, batch: Batch, B: int):
+        """(indices, offsets) of the physical tables for this batch: the batch's own CSR, or
+        (QR) the expanded CSR written by one dlrm_qr_expand_csr launch into buffers owned by
+        this (batch size, lookup count) so captured graphs keep their addresses."""
+        if not self.qr_active:
+            return batch.indices, batch.offsets
+        n_log = batch.indices.numel()
+        mx = int(batch.max_per_table)
+        if mx > 0 and mx * self.T_local == n_log:  # every table has mx lookups
+            n = mx * self.T_phys
+        else:  # bound: the tail past the last bag is skipped by the kernels
+            n = n_log + (self.T_phys - self.T_local) * (mx if mx > 0 else n_log)
+        key = (B, n)
+        if key not in self._qr_csr:
+            self._qr_csr[key] = (
+                torch.zeros(max(n, 1), dtype=torch.int32, device=self.dev),
+                torch.zeros(self.T_phys * B + 1, dtype=torch.int32, device=self.dev))
+        pidx, poff = self._qr_csr[key]
+        ops.qr_expand_csr(self.T_phys, B, batch.indices, batch.offsets, self._qr_src,
+                          self._qr_kind, self._qr_coll, mx if mx > 0 else n_log, pidx, poff)
+        return pidx, poff
+
+    def _qr_combine(self, bufs, B: int) -> None:
+        ops.qr_pool_combine_forward(self.cfg.qr_operation, self.T_local, B, self.D, self._qr_pq,
+                                    self._qr_pr, bufs["P"], bufs["E"])
 
     def capture(self, batch: Batch, pool=None):
         """A replayable step for ``batch``: its "gpu" segments captured as hipGraphs (one

@@ -307,6 +307,31 @@ int dlrm_qr_combine_backward(int32_t op, int64_t n_rows, int64_t D, const float*
                              const float* er, const float* grad_out, float* grad_eq,
                              float* grad_er, dlrm_stream_t stream);
 
+/* Table-batched QR for the fused engine (create_emb's QR branch, dlrm_s_pytorch.py:282-290,
+ * on the batched CSR): physical table p takes the bags of logical table src[p] with the
+ * logical indices (kind 0), the quotients trunc((float)idx / coll[p]) (kind 1) or the
+ * remainders idx mod coll[p] (kind 2) -> int32 phys_indices / phys_offsets[T_phys*B+1].
+ * src / kind / coll are DEVICE int32 arrays of T_phys entries. */
+int dlrm_qr_expand_csr(int32_t T_phys, int32_t B, const void* indices, int32_t index_bits,
+                       const void* offsets, int32_t offset_bits, const int32_t* src,
+                       const int32_t* kind, const int32_t* coll,
+                       int64_t max_lookups_per_table, int32_t* phys_indices,
+                       int32_t* phys_offsets, dlrm_stream_t stream);
+/* E[b][t] = op(P[b][pq[t]], P[b][pr[t]]) (QREmbeddingBag.forward's combine,
+ * tricks/qr_embedding_bag.py:166-172; op mult or add) for pr[t] >= 0, else P[b][pq[t]];
+ * P: pooled physical tables [B][.][D] (row stride p_batch_stride), E: [B][T][D].
+ * pq / pr: DEVICE int32 [T].  D and the strides are multiples of 4. */
+int dlrm_qr_pool_combine_forward(int32_t op, int32_t T, int64_t B, int64_t D, const int32_t* pq,
+                                 const int32_t* pr, const float* P, int64_t p_batch_stride,
+                                 float* E, int64_t e_batch_stride, dlrm_stream_t stream);
+/* dP[b][pq[t]] = dE * P[b][pr[t]], dP[b][pr[t]] = dE * P[b][pq[t]] (mult; add: dE to both);
+ * dP[b][pq[t]] = dE for tables without a remainder. */
+int dlrm_qr_pool_combine_backward(int32_t op, int32_t T, int64_t B, int64_t D,
+                                  const int32_t* pq, const int32_t* pr, const float* P,
+                                  int64_t p_batch_stride, const float* dE,
+                                  int64_t e_batch_stride, float* dP, int64_t dp_batch_stride,
+                                  dlrm_stream_t stream);
+
 /* ------------------------------------------------------------ interaction -- */
 /*
  * Feature f of sample b lives at feat_ptrs[f] + b*feat_bstrides[f] (D floats);

@@ -246,3 +246,70 @@ def test_fused_bottom_mlp_step_matches_gemm_path():
     for a, b in zip(*res):
         ok, msg = fp32_close(b.numpy(), a.numpy(), atol=1e-4)  # 3 steps of drift
         assert ok, msg
+
+
+@pytest.mark.parametrize("op", ["mult", "add"])
+@pytest.mark.parametrize("optimizer", ["sgd", "rwsadagrad"])
+@pytest.mark.parametrize("graph", [False, True])
+def test_qr_step_vs_oracle(op, optimizer, graph):
+    """C4 on the fused engine: tables with more than qr_threshold rows become QR tables
+    (quotient ceil(n/c) + remainder c rows, tricks/qr_embedding_bag.py) looked up on the
+    expanded physical CSR, combined by the pooled combine kernel; SGD or RWSAdagrad fused
+    into the backward.  Against the oracle's QREmbeddingBag + SGD / RWSAdagrad, 3 steps,
+    eager or replayed from a captured graph."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    D, B, c, thr = 32, 256, 4, 200
+    rows = [3, 5000, 150, 201, 2000, 64, 1000, 7]
+    bot, top = [13, 64, 32], [64, 1]
+    ln_top = [_num_int(len(rows), D)] + top
+    lr = 0.05
+    np.random.seed(11)
+    ref = O.OracleDLRM(D, rows, bot, ln_top, loss_function="bce")
+    torch.manual_seed(5)
+    for k, n in enumerate(rows):
+        if n > thr:
+            ref.emb_l[k] = O.QREmbeddingBagOracle(n, D, c, op)
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=bot, ln_top=ln_top, loss_function="bce",
+                        learning_rate=lr, optimizer=optimizer, qr_flag=True, qr_collisions=c,
+                        qr_operation=op, qr_threshold=thr)
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    assert tr.T_phys == len(rows) + sum(1 for n in rows if n > thr)
+    opt = O.RWSAdagradOracle(ref.parameters(), lr=lr) if optimizer == "rwsadagrad" else None
+    rng = np.random.RandomState(3)
+    batches = [_rand_batch(rng, rows, B, 1, bot[0], "bce") for _ in range(3)]
+    run = None
+    for s, (X, lS_o, lS_i, T) in enumerate(batches):
+        Xt, ot, it, Tt = (torch.tensor(X), torch.tensor(lS_o), [torch.tensor(i) for i in lS_i],
+                          torch.tensor(T))
+        if opt is None:
+            Zr, Er = ref.train_step(Xt, ot, it, Tt, lr)
+        else:
+            Zr = ref(Xt, ot, it)
+            Er = ref.loss_fn(Zr, Tt)
+            opt.zero_grad()
+            Er.backward()
+            opt.step()
+            Zr, Er = Zr.detach(), Er.detach()
+        b = tr.make_batch(X, lS_o, lS_i, T)
+        if graph and s == 1:
+            static = b
+            run = tr.capture(static)
+        if run is not None:
+            for dst, src in zip((static.X, static.offsets, static.indices, static.target),
+                                (b.X, b.offsets, b.indices, b.target)):
+                dst.copy_(src)
+            run()
+            Z, E = tr._cur["prob"], tr._cur["loss"]
+        else:
+            Z, E = tr.step(b)
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
+        assert ok, (s, msg)
+        ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
+        assert ok, (s, msg)
+    for k, e in enumerate(ref.emb_l):
+        got = tr.table(k)
+        want = (e.weight_q, e.weight_r) if hasattr(e, "weight_q") else (e.weight,)
+        got = got if isinstance(got, tuple) else (got,)
+        for g_, w_ in zip(got, want):
+            ok, msg = fp32_close(g_.cpu().numpy(), w_.detach().numpy())
+            assert ok, ("emb", k, msg)
