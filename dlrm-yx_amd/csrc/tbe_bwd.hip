@@ -31,6 +31,11 @@
 namespace {
 
 constexpr int CH = 16;  // sorted lookups per block (all gradient rows of a block in flight)
+// Large batches of lookups (>= kLongChN) use longer blocks (kLongCH): fewer runs cross a
+// block edge, so fewer partial rows and less combine work; still 16 gradient rows in
+// flight per lane group.  The partial buffer is sized for CH.
+constexpr int kLongCH = 64;
+constexpr int64_t kLongChN = 1 << 18;
 
 // ---------------------------------------------------------------- backward --
 // Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags),
@@ -510,22 +515,22 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
     const KeyT* __restrict__ keys, const int32_t* __restrict__ pos,
     const int32_t* __restrict__ bag_of, const float* __restrict__ psw,
     const float* __restrict__ gout, int64_t gbs, int64_t N, float lr, float eps,
-    KeyT sentinel, float* __restrict__ partial) {
+    KeyT sentinel, float* __restrict__ partial, int ch) {
   using V = typename VecT<VW>::T;
   constexpr int GPW = kWave / LPB;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPB;
   const int gl = lane - g * LPB;
   const int nchunks = (int)(D / VW);
-  const int64_t nblocks = (N + CH - 1) / CH;
+  const int64_t nblocks = (N + ch - 1) / ch;
   const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
 
   for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {
     const int64_t k = k0 + g;
     if (k >= nblocks) continue;
-    const int64_t i0 = k * CH;
-    const int64_t i1 = (i0 + CH < N) ? i0 + CH : N;
+    const int64_t i0 = k * ch;
+    const int64_t i1 = (i0 + ch < N) ? i0 + ch : N;
     const bool has_prev = i0 > 0;
     const bool has_next = i1 < N;
     const KeyT prev_key = has_prev ? keys[i0 - 1] : sentinel;
@@ -586,7 +591,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
           my_off = (int64_t)b * gbs + (int64_t)t * D;
         }
       }
-      constexpr int U = LPB < CH ? LPB : CH;  // gradient rows in flight per group
+      constexpr int U = LPB < CH ? LPB : CH;  // gradient rows in flight per group (ch >= CH)
       for (int j = 0; j < n; j += U) {
         KeyT ku[U];
         int64_t ou[U];
@@ -660,22 +665,22 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
 template <int LPB, int VW, int MAXV, typename KeyT, int MODE>
 __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
     float* __restrict__ W, float* __restrict__ mom, int64_t D, const KeyT* __restrict__ keys,
-    int64_t N, float lr, float eps, KeyT sentinel, const float* __restrict__ partial) {
+    int64_t N, float lr, float eps, KeyT sentinel, const float* __restrict__ partial, int ch) {
   using V = typename VecT<VW>::T;
   constexpr int GPW = kWave / LPB;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPB;
   const int gl = lane - g * LPB;
   const int nchunks = (int)(D / VW);
-  const int64_t nblocks = (N + CH - 1) / CH;
+  const int64_t nblocks = (N + ch - 1) / ch;
   const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
 
   for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {
     const int64_t k = k0 + g;
     if (k >= nblocks) continue;
-    const int64_t i0 = k * CH;
-    const int64_t i1 = (i0 + CH < N) ? i0 + CH : N;
+    const int64_t i0 = k * ch;
+    const int64_t i1 = (i0 + ch < N) ? i0 + ch : N;
     if (i1 >= N) continue;
     const KeyT last = keys[i1 - 1];
     if (last == sentinel || keys[i1] != last) continue;  // run ends inside this block
@@ -698,7 +703,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
       int64_t base = k + 1;
       while (true) {
         const int64_t kk = base + gl;
-        const bool cont = kk < nblocks && keys[kk * CH] == last;
+        const bool cont = kk < nblocks && keys[kk * ch] == last;
         // groups are LPB-aligned lane ranges: find the first lane (in order) that fails
         uint64_t fail = __ballot(!cont);
         if constexpr (LPB < 64) fail = (fail >> ((lane / LPB) * LPB)) & ((1ull << LPB) - 1);
@@ -1202,7 +1207,10 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   const int64_t maxv = dlrm::ceil_div(nchunks, lpb);
   DLRM_REQUIRE(maxv <= 8, DLRM_ERR_UNSUPPORTED, "%s: D=%lld too large", name, (long long)D);
   const int gpw = 64 / lpb;
-  const int64_t nblocks = dlrm::ceil_div(N, CH);
+  const char* chenv = getenv("DLRM_TBE_CH");  // A/B override: 16 or 64
+  int ch = N >= kLongChN ? kLongCH : CH;
+  if (chenv && (atoi(chenv) == CH || atoi(chenv) == kLongCH)) ch = atoi(chenv);
+  const int64_t nblocks = dlrm::ceil_div(N, (int64_t)ch);
   int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(nblocks, gpw), 4);
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
@@ -1211,14 +1219,14 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
     if (per_table)                                                                             \
       hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE, true>), dim3(blocks),  \
                          dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw, \
-                         gout, gbs, N, lr, eps, sentinel, w.partial);                          \
+                         gout, gbs, N, lr, eps, sentinel, w.partial, ch);                      \
     else                                                                                       \
       hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE, false>), dim3(blocks), \
                          dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw, \
-                         gout, gbs, N, lr, eps, sentinel, w.partial);                          \
+                         gout, gbs, N, lr, eps, sentinel, w.partial, ch);                      \
     hipLaunchKernelGGL((tbe_bwd_combine_kernel<LPB, VW, MV, KeyT, MODE>), dim3(blocks),        \
                        dim3(256), 0, st, W, mom, D, w.keys_out, N, lr, eps, sentinel,          \
-                       w.partial);                                                             \
+                       w.partial, ch);                                                         \
   } while (0)
 #define BY_LPB(VW, MODE)                             \
   switch (lpb) {                                     \

@@ -177,6 +177,12 @@ class RecordPipeline:
         self._thread.start()
 
     def _reader(self):
+        try:
+            self._read_loop()
+        except BaseException as e:  # noqa: BLE001 - handed to next(), which raises it
+            self._filled.put(e)
+
+    def _read_loop(self):
         j = 0
         with open(self.data_file, "rb", buffering=0) as f:
             while not self._stop:
@@ -201,6 +207,8 @@ class RecordPipeline:
         i = self._filled.get()
         if i is None:
             return False
+        if isinstance(i, BaseException):
+            raise RuntimeError("RecordPipeline: the reader thread failed") from i
         cs = self.copy_stream
         cs.wait_event(self.consumed[i])  # the device slot's previous decode is done
         with torch.cuda.stream(cs):
