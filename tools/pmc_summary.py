@@ -15,7 +15,8 @@ GROUPS = [
     ("gemm", ("gemm_group_kernel", "gemm_generic_kernel", "gemm_rowsum_kernel",
               "gemm_f32_", "gemm_splitk_reduce_kernel")),
     ("tbe_fwd", ("tbe_fwd_kernel", "tbe_fwd_presort_kernel")),  # presort: + sort + bottom MLP
-    ("tbe_bwd", ("tbe_bwd_", "rocprim")),
+    ("tbe_bwd", ("tbe_bwd_", "tbe_tiled_", "rocprim")),
+    ("qr", ("qr_",)),
     ("interaction", ("interact_",)),
     ("colsum", ("colsum_",)),
     ("head", ("head_", "mean_kernel", "outer_drelu_kernel")),
