@@ -36,6 +36,7 @@ from . import extend_distributed as ext_dist
 from . import functional as HF
 from . import ops, sharders
 from .modules import (HipEmbeddingBagList, HipMLP, HipPrEmbeddingBag, HipQREmbeddingBag,
+                      HipStandaloneEmbeddingBag,
                       Optimizer, SplitTableBatchedEmbeddingBags, TableBatchedEmbeddingBags,
                       make_embedding_list)
 
@@ -68,13 +69,19 @@ class DLRM_Net(nn.Module):
             local.append(i)
         ln_local = [int(ln[i]) for i in local]
         # with --md-flag, lm is md_solver's per-table dim list (dlrm_s_pytorch.py:1510-1516)
-        md_dims = list(lm) if np.ndim(lm) > 0 else None
-        base = int(max(md_dims)) if md_dims is not None else int(lm)
+        md_dims = list(lm) if (np.ndim(lm) > 0 and not self.load_processed) else None
+        base = int(max(md_dims)) if md_dims is not None else None
+        # --load-processed: lm is the per-table dim list of table_configs.json (:1434-1435,
+        # create_emb :276-279); the most common dim shares the flat buffer, the other
+        # tables are standalone modules (apply_emb splits every output into ln_bot[-1]
+        # features, :579-585)
+        pdims = [int(lm[i]) for i in local] if self.load_processed else None
+        if pdims is not None:
+            base = max(sorted(set(pdims)), key=pdims.count) if pdims else int(self.ln_bot[-1])
+        elif base is None:
+            base = int(lm)
         for j, n in enumerate(ln_local):
-            if self.load_processed:
-                raise NotImplementedError("--load-processed per-table dims (mixed D) are not on "
-                                          "the MI355X path yet")
-            m = base
+            m = pdims[j] if pdims is not None else base
             if self.qr_flag and n > self.qr_threshold:
                 extra[j] = HipQREmbeddingBag(n, m, self.qr_collisions,
                                              operation=self.qr_operation, mode="sum",
@@ -98,7 +105,11 @@ class DLRM_Net(nn.Module):
                     torch.empty(n, m).normal_()
                 W = np.random.uniform(low=-np.sqrt(1 / n), high=np.sqrt(1 / n),
                                       size=(n, m)).astype(np.float32)
-                tables.append(W)
+                if m != base:
+                    extra[j] = HipStandaloneEmbeddingBag(n, m, W)
+                    tables.append(None)
+                else:
+                    tables.append(W)
         emb_l = make_embedding_list(ln_local, base, tables, extra, sparse=True)
         if weighted_pooling is None:
             v_W_l = [None] * len(ln_local)
@@ -193,7 +204,10 @@ class DLRM_Net(nn.Module):
                     self.device_indices = list(map(int, allocation.split(",")))
                 else:
                     self.device_indices = sharders.shard(self.ln_emb, ext_dist.my_size, sharder)
-                num_splits = [m_spa // int(self.ln_bot[-1])] * n_emb
+                if load_processed:  # per-table dims (:457-460)
+                    num_splits = [int(m) // int(self.ln_bot[-1]) for m in m_spa]
+                else:
+                    num_splits = [m_spa // int(self.ln_bot[-1])] * n_emb
                 self.n_emb_per_rank = [0] * ext_dist.my_size
                 for i, s in enumerate(num_splits):
                     self.n_emb_per_rank[self.device_indices[i]] += s

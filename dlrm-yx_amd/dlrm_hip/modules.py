@@ -276,6 +276,26 @@ def single_table_lookup(weight: Parameter, indices: torch.Tensor, bag_offsets: t
     return out.view(B, -1)
 
 
+class HipStandaloneEmbeddingBag(nn.Module):
+    """One plain table kept outside the list's shared buffer (a --load-processed table
+    whose dim differs from the shared buffer's): nn.EmbeddingBag(n, m, mode="sum",
+    sparse=True) semantics on the TBE kernel; ``weight`` as the reference's."""
+
+    def __init__(self, num_embeddings: int, embedding_dim: int, weight, sparse: bool = True):
+        super().__init__()
+        self.num_embeddings = int(num_embeddings)
+        self.embedding_dim = int(embedding_dim)
+        self.mode = "sum"
+        self.sparse = sparse
+        self.weight = Parameter(torch.as_tensor(weight))
+
+    def forward(self, input, offsets=None, per_sample_weights=None):
+        return single_table_lookup(self.weight, input, offsets, per_sample_weights, self.sparse)
+
+    def extra_repr(self):
+        return f"{self.num_embeddings}, {self.embedding_dim}, mode='sum'"
+
+
 class QRCombine(torch.autograd.Function):
     @staticmethod
     def forward(ctx, op, eq, er):
