@@ -31,7 +31,10 @@ def _items(g, mir, batched):
 def test_oracle_transform_matches_reference(gold, mir, batched):
     for i, rec, key in _items(gold, mir, batched):
         X, o, idx, y = O.criteo_transform(rec, mir, batched)
-        assert np.array_equal(X.numpy(), gold[f"X_{key}"]), key
+        # log(x+1): torch's CPU log may differ by an ulp between host CPUs (vectorised libm),
+        # so the dense part is held to the fp32 tolerance; the integer parts are exact
+        ok, msg = fp32_close(X.numpy(), gold[f"X_{key}"])
+        assert ok, (key, msg)
         assert np.array_equal(o.numpy(), gold[f"o_{key}"]) and o.dtype == torch.from_numpy(
             gold[f"o_{key}"]).dtype, key
         assert np.array_equal(idx.numpy(), gold[f"i_{key}"]), key
