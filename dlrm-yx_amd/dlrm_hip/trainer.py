@@ -819,6 +819,11 @@ class DLRMTrainer:
         sp = bufs.setdefault("splits", {})
         if key not in sp:
             sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr), partial=True)
+            # tuning override (A/B sweeps only): DLRM_WG_SPLITS="top1:4,bot0:2"
+            for item in os.environ.get("DLRM_WG_SPLITS", "").split(","):
+                name, _, val = item.partition(":")
+                if name == f"{key[0]}{key[1]}" and val.isdigit() and int(val) >= 1:
+                    sp[key] = int(val)
         s = sp[key]
         if s <= 1:
             return self._wgrad(L, g, inp, fused_opt, lr), None
