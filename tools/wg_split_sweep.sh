@@ -10,6 +10,6 @@ run() {
   python -c "import json; d=json.load(open('$OUT/b.json')); print('$1', d['value'], d['kernel_us_per_step']['gemm'])"
 }
 run ""
-for L in top0 top1 top2 top3; do
+for L in ${LAYERS:-top0 top1 top2 top3}; do
   for s in 1 2 4 8; do run "$L:$s"; done
 done
