@@ -342,8 +342,8 @@ def cpu_baseline(c, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="terabyte", choices=list(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="global batch (default: config's)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
