@@ -1382,6 +1382,11 @@ int check_desc(const Desc& d) {
     }
     DLRM_REQUIRE(pipe_ok(d), DLRM_ERR_UNSUPPORTED,
                  "dlrm_gemm_f32: PARTIAL needs 16-B aligned operands, K %% 4 == 0");
+    // the REDUCE job repeats the caller's count: a count the planner would lower (K too
+    // short for it, or above kMaxSplit) would leave slabs unwritten
+    DLRM_ARG(d.splits <= 0 || make_plan(d.splits, d.K).splits == d.splits,
+             "dlrm_gemm_f32: PARTIAL splits=%d is not a normalized count for K=%lld "
+             "(use dlrm_gemm_f32_splits)", (int)d.splits, (long long)d.K);
   }
   DLRM_ARG(d.M >= 0 && d.N >= 0 && d.K >= 0, "dlrm_gemm_f32: negative size");
   if (d.M == 0 || (d.N == 0 && d.ones_col < 0)) return DLRM_OK;
@@ -1437,8 +1442,10 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
   Plan pl[kMaxGroup];
   plan_launch(m, q, t, pl);
   const size_t need = group_ws_bytes(m, q, t, pl);
-  if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: every problem unsplit
-    for (int i = 0; i < m; ++i) pl[i] = make_plan(1, q[i].K);
+  if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: in-launch splits off
+    // (PARTIAL / REDUCE plans pair with each other across launches: kept)
+    for (int i = 0; i < m; ++i)
+      if (q[i].mode == DLRM_GEMM_FULL) pl[i] = make_plan(1, q[i].K);
   }
   if (t.x6) {  // split-bf16 body: 128-wide tiles stage too much per K-tile
     if (t.bm == 32) return launch_group<32, 64, true>(m, q, pl, ws, ws_bytes, st);
@@ -1508,8 +1515,10 @@ extern "C" int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem) {
   if (!problem) return 0;
   Desc d = desc_of(*problem);
   if (d.mode == DLRM_GEMM_REDUCE) d.mode = DLRM_GEMM_FULL;
-  d.splits = 0;
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) return 1;
+  // PARTIAL with a requested count: that count normalized (what the kernel will run)
+  if (d.mode == DLRM_GEMM_PARTIAL && d.splits > 0) return make_plan(d.splits, d.K).splits;
+  d.splits = 0;
   Tile t;
   Plan pl;
   plan_one(d, t, pl);

@@ -267,7 +267,8 @@ template <typename IdxT, typename OffT>
 __global__ __launch_bounds__(256) void qr_expand_kernel(
     int T_phys, int B, const IdxT* __restrict__ idx, const OffT* __restrict__ off,
     const int32_t* __restrict__ src, const int32_t* __restrict__ kind,
-    const int32_t* __restrict__ coll, int32_t* __restrict__ pidx, int32_t* __restrict__ poff) {
+    const int32_t* __restrict__ coll, int32_t* __restrict__ pidx, int32_t* __restrict__ poff,
+    int64_t cap, int32_t* __restrict__ err) {
   const int p = blockIdx.y;
   const int j = src[p];
   const int64_t s = (int64_t)off[(int64_t)j * B];
@@ -289,12 +290,19 @@ __global__ __launch_bounds__(256) void qr_expand_kernel(
         o = v % c;  // torch.remainder: sign of the divisor
         if (o != 0 && ((o < 0) != (c < 0))) o += c;
       }
-      pidx[base + i] = (int32_t)o;
+      if (base + i < cap) {
+        pidx[base + i] = (int32_t)o;
+      } else if (err) {  // past the caller's buffer: dropped (the offsets are clamped)
+        atomicOr(err, DLRM_TBE_ERR_TABLE_CAP);
+      }
     }
-    if (i < B) poff[(int64_t)p * B + i] = (int32_t)(base + (int64_t)off[(int64_t)j * B + i] - s);
+    if (i < B) {
+      const int64_t o = base + (int64_t)off[(int64_t)j * B + i] - s;
+      poff[(int64_t)p * B + i] = (int32_t)(o < cap ? o : cap);
+    }
   }
   if (p == T_phys - 1 && blockIdx.x == 0 && threadIdx.x == 0)
-    poff[(int64_t)T_phys * B] = (int32_t)(base + len);
+    poff[(int64_t)T_phys * B] = (int32_t)(base + len < cap ? base + len : cap);
 }
 
 // E[b][t] = op(P[b][pq[t]], P[b][pr[t]]) for QR tables (pr[t] >= 0), P[b][pq[t]] otherwise.
@@ -353,8 +361,9 @@ extern "C" int dlrm_qr_expand_csr(int32_t T_phys, int32_t B, const void* indices
                                   int32_t index_bits, const void* offsets, int32_t offset_bits,
                                   const int32_t* src, const int32_t* kind, const int32_t* coll,
                                   int64_t max_lookups_per_table, int32_t* phys_indices,
-                                  int32_t* phys_offsets, dlrm_stream_t stream) {
-  DLRM_ARG(T_phys > 0 && B > 0, "dlrm_qr_expand_csr: bad sizes");
+                                  int32_t* phys_offsets, int64_t phys_capacity,
+                                  int32_t* error_flag, dlrm_stream_t stream) {
+  DLRM_ARG(T_phys > 0 && B > 0 && phys_capacity >= 0, "dlrm_qr_expand_csr: bad sizes");
   DLRM_ARG(indices && offsets && src && kind && coll && phys_indices && phys_offsets,
            "dlrm_qr_expand_csr: null pointer");
   DLRM_ARG(index_bits == 32 || index_bits == 64, "dlrm_qr_expand_csr: bad index_bits");
@@ -367,7 +376,7 @@ extern "C" int dlrm_qr_expand_csr(int32_t T_phys, int32_t B, const void* indices
 #define QX(I, O)                                                                              \
   hipLaunchKernelGGL((qr_expand_kernel<I, O>), grid, block, 0, st, T_phys, B,                  \
                      static_cast<const I*>(indices), static_cast<const O*>(offsets), src, kind, \
-                     coll, phys_indices, phys_offsets)
+                     coll, phys_indices, phys_offsets, phys_capacity, error_flag)
   if (index_bits == 32 && offset_bits == 32) QX(int32_t, int32_t);
   else if (index_bits == 32) QX(int32_t, int64_t);
   else if (offset_bits == 32) QX(int64_t, int32_t);

@@ -84,7 +84,7 @@ SIGNATURES = {
     "dlrm_qr_combine_forward": (c_int32, [c_int32, c_int64, c_int64, P, P, P, P]),
     "dlrm_qr_combine_backward": (c_int32, [c_int32, c_int64, c_int64, P, P, P, P, P, P]),
     "dlrm_qr_expand_csr": (c_int32, [c_int32, c_int32, P, c_int32, P, c_int32, P, P, P, c_int64,
-                                     P, P, P]),
+                                     P, P, c_int64, P, P]),
     "dlrm_qr_pool_combine_forward": (c_int32, [c_int32, c_int32, c_int64, c_int64, P, P, P,
                                                c_int64, P, c_int64, P]),
     "dlrm_qr_pool_combine_backward": (c_int32, [c_int32, c_int32, c_int64, c_int64, P, P, P,

@@ -173,6 +173,8 @@ class RecordPipeline:
         self._stop = False
         self._k = 0            # next batch next() returns
         self._issued = 0       # batches whose H2D copy has been enqueued
+        self._eof = False      # the reader reached the end (loop=False): never block again
+        self._err = None       # the reader's failure, re-raised by every later next()
         self._thread = threading.Thread(target=self._reader, daemon=True)
         self._thread.start()
 
@@ -204,10 +206,16 @@ class RecordPipeline:
                 j += 1
 
     def _issue_copy(self):
+        if self._err is not None:
+            raise RuntimeError("RecordPipeline: the reader thread failed") from self._err
+        if self._eof:  # the reader has exited: the queue gets nothing more
+            return False
         i = self._filled.get()
         if i is None:
+            self._eof = True
             return False
         if isinstance(i, BaseException):
+            self._err = i
             raise RuntimeError("RecordPipeline: the reader thread failed") from i
         cs = self.copy_stream
         cs.wait_event(self.consumed[i])  # the device slot's previous decode is done

@@ -146,11 +146,27 @@ class EmbeddingBagsFunction(torch.autograd.Function):
             out = ops.tbe_forward_rows(module.weight_flat, fmt, module.D, module.row_base,
                                        module.T, B, indices, offsets,
                                        per_sample_weights=per_sample_weights, error_flag=flag)
-        if getattr(module, "strict_indices", True):
-            # nn.EmbeddingBag raises IndexError on an out-of-range index; the kernel skips
-            # and flags it, and this reads the flag (one sync, like the driver's per-step
-            # loss read).  Set module.strict_indices = False for graph capture.
+        # nn.EmbeddingBag raises IndexError on an out-of-range index; the kernel skips and
+        # flags it.  module.strict_indices picks when the flag is read:
+        #   "deferred" (default): no host sync - the flag is copied to pinned memory
+        #       asynchronously and the NEXT forward of this module raises (or
+        #       module.tbe_errors.flush() after the last step);
+        #   "sync" / True: read now (one host sync per forward, e.g. for debugging);
+        #   False: never (the caller checks the flag itself).
+        mode = getattr(module, "strict_indices", "deferred")
+        if mode == "sync" or mode is True:
             ops.check_tbe_errors(flag)
+        elif mode:
+            chk = getattr(module, "tbe_errors", None)
+            if chk is None:
+                chk = ops.DeferredErrorCheck()
+                try:
+                    module.tbe_errors = chk
+                except AttributeError:
+                    chk = None
+            if chk is not None:
+                chk.poll()
+                chk.post(flag)
         ctx.module, ctx.B, ctx.counts = module, B, counts
         ctx.save_for_backward(indices, offsets, per_sample_weights)
         ctx.n_params = len(table_params)

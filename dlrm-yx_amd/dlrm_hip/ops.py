@@ -32,6 +32,51 @@ def check_tbe_errors(flag: torch.Tensor, reset: bool = True) -> None:
     if v & TBE_ERR_TABLE_CAP:
         raise ValueError("a table had more lookups than max_lookups_per_table "
                          "(its backward update was skipped)")
+
+
+def _raise_bits(v: int) -> None:
+    if v & TBE_ERR_INDEX:
+        raise TBEIndexError("embedding index out of range for its table (lookup skipped)")
+    if v & TBE_ERR_TABLE_CAP:
+        raise ValueError("a table had more lookups than max_lookups_per_table "
+                         "(its backward update was skipped)")
+
+
+class DeferredErrorCheck:
+    """Reads a TBE error flag without a host sync on the calling step: ``post()`` enqueues
+    an async copy of the flag into pinned host memory (then clears it) and records an event;
+    ``poll()`` - at the next call, by then long complete - raises on what the previous call
+    flagged.  ``flush()`` waits for the last copy and raises (end of training / tests).
+    Skipped while the stream is being captured into a graph."""
+
+    def __init__(self):
+        self._host = None
+        self._event = None
+
+    def poll(self) -> None:
+        if self._event is None:
+            return
+        self._event.synchronize()  # recorded a call ago: normally already complete
+        self._event = None
+        v = int(self._host[0])
+        self._host[0] = 0
+        _raise_bits(v)
+
+    def post(self, flag: torch.Tensor) -> None:
+        if torch.cuda.is_current_stream_capturing():
+            return
+        if self._host is None:
+            self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._event = None
+        self._host.copy_(flag, non_blocking=True)
+        flag.zero_()
+        self._event = torch.cuda.Event()
+        self._event.record()
+
+    def flush(self) -> None:
+        self.poll()
+
+
 LOSS_MSE, LOSS_BCE = 0, 1
 QR_OPS = {"mult": 0, "add": 1, "concat": 2}
 
@@ -296,14 +341,16 @@ def qr_combine_backward(op: str, eq: torch.Tensor, er: torch.Tensor, grad_out: t
 def qr_expand_csr(T_phys: int, B: int, indices: torch.Tensor, offsets: torch.Tensor,
                   src: torch.Tensor, kind: torch.Tensor, coll: torch.Tensor,
                   max_lookups_per_table: int, phys_indices: torch.Tensor,
-                  phys_offsets: torch.Tensor) -> None:
+                  phys_offsets: torch.Tensor, error_flag: Optional[torch.Tensor] = None) -> None:
     """Logical table-batched CSR -> the physical CSR of the QR engine (dlrm_qr_expand_csr):
     physical table p = logical table src[p]'s bags with its indices (kind 0), quotients
-    (kind 1) or remainders (kind 2) by coll[p]; int32 outputs."""
+    (kind 1) or remainders (kind 2) by coll[p]; int32 outputs.  Lookups past
+    phys_indices.numel() are dropped and raise TBE_ERR_TABLE_CAP in ``error_flag``."""
     _check_cuda(indices, offsets, src, kind, coll, phys_indices, phys_offsets)
     _lib.call("dlrm_qr_expand_csr", T_phys, B, _p(indices), _bits(indices), _p(offsets),
               _bits(offsets), _p(src), _p(kind), _p(coll), int(max_lookups_per_table),
-              _p(phys_indices), _p(phys_offsets), _stream(indices.device))
+              _p(phys_indices), _p(phys_offsets), phys_indices.numel(), _p(error_flag),
+              _stream(indices.device))
 
 
 def qr_pool_combine_forward(op: str, T: int, B: int, D: int, pq: torch.Tensor, pr: torch.Tensor,
@@ -447,12 +494,14 @@ def gemm_problem(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False,
     return pr, C
 
 
-def gemm_splits(pr, partial: bool = False) -> int:
+def gemm_splits(pr, partial: bool = False, requested: int = 0) -> int:
     """The planner's K split for a problem launched alone (dlrm_gemm_f32_splits); with
-    partial=True, as a PARTIAL problem (deferred reduction)."""
+    partial=True, as a PARTIAL problem (deferred reduction).  ``requested`` > 0 (PARTIAL):
+    that count normalized to K - the count a PARTIAL launch accepts and its REDUCE repeats."""
     q = _lib.GemmProblem.from_buffer_copy(pr)
     if partial:
         q.mode = GEMM_PARTIAL
+    q.splits = int(requested) if partial else 0
     return int(_lib.load().dlrm_gemm_f32_splits(ctypes.byref(q)))
 
 

@@ -512,6 +512,13 @@ class DLRMTrainer:
         D = self.D
         Bl = batch.X.shape[0]
         B = Bl * self.world
+        # the all-to-all splits assume every rank holds B / W samples of a B-sample batch
+        # (dlrm_s_pytorch.py:139-143); a batch built for another world size or table set
+        # would send wrong-sized chunks
+        n_off = self.T_local * B + 1
+        if self.T_local > 0 and batch.offsets.numel() != n_off:
+            raise ValueError(f"batch offsets hold {batch.offsets.numel()} entries, expected "
+                             f"T_local*B+1 = {n_off} (B = {Bl} x {self.world} ranks)")
         bufs = self._buffers(Bl, B)
         self._cur = bufs
         prof = profile or (lambda name: _NullCtx())
@@ -735,7 +742,8 @@ class DLRMTrainer:
                 torch.zeros(self.T_phys * B + 1, dtype=torch.int32, device=self.dev))
         pidx, poff = self._qr_csr[key]
         ops.qr_expand_csr(self.T_phys, B, batch.indices, batch.offsets, self._qr_src,
-                          self._qr_kind, self._qr_coll, mx if mx > 0 else n_log, pidx, poff)
+                          self._qr_kind, self._qr_coll, mx if mx > 0 else n_log, pidx, poff,
+                          error_flag=self.tbe_error_flag)
         return pidx, poff
 
     def _qr_combine(self, bufs, B: int) -> None:
@@ -823,7 +831,8 @@ class DLRMTrainer:
             for item in os.environ.get("DLRM_WG_SPLITS", "").split(","):
                 name, _, val = item.partition(":")
                 if name == f"{key[0]}{key[1]}" and val.isdigit() and int(val) >= 1:
-                    sp[key] = int(val)
+                    sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr),
+                                              partial=True, requested=int(val))
         s = sp[key]
         if s <= 1:
             return self._wgrad(L, g, inp, fused_opt, lr), None
@@ -900,14 +909,28 @@ class DLRMTrainer:
 
     def _alltoall_fwd(self, bufs, Bl):
         """All2All_Req.forward (extend_distributed.py:405-444): [B, T_r*D] -> W chunks of
-        [B/W, T_s*D] in rank order."""
+        [B/W, T_s*D] in rank order.  A rank that owns no table sends nothing (its E
+        buffer is a 1-table placeholder: only the first sum(send) floats take part)."""
         send, recv = self._split_sizes(Bl)
-        return _a2a(bufs["recv"], bufs["E"].view(-1), recv, send, self.pg)
+        return _a2a(bufs["recv"], bufs["E"].view(-1)[:sum(send)], recv, send, self.pg)
 
     def _alltoall_bwd(self, bufs, Bl):
         """All2All_Wait.backward (extend_distributed.py:489-508): reverse exchange."""
         send, recv = self._split_sizes(Bl)
-        return _a2a(bufs["dE"].view(-1), bufs["drecv"], send, recv, self.pg)
+        return _a2a(bufs["dE"].view(-1)[:sum(send)], bufs["drecv"], send, recv, self.pg)
+
+    def lookup_balance(self, B: int, L: int = 1):
+        """Per-rank load of the table-wise sharding: tables, rows and lookups per step
+        (greedy balances rows, not lookups: SURVEY.md §7 hard part 6)."""
+        rows = [0] * self.world
+        tabs = [0] * self.world
+        for t, r in enumerate(self.device_indices):
+            rows[r] += int(self.cfg.ln_emb[t])
+            tabs[r] += 1
+        look = [n * B * L for n in tabs]
+        mean = sum(look) / max(self.world, 1)
+        return {"tables": tabs, "rows": rows, "lookups": look,
+                "lookup_max_over_mean": round(max(look) / mean, 3) if mean else None}
 
     def _allreduce_dense(self):
         """DDP gradient all-reduce (dlrm_s_pytorch.py:1626-1633) on the flat bucket; the

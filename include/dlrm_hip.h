@@ -311,12 +311,15 @@ int dlrm_qr_combine_backward(int32_t op, int64_t n_rows, int64_t D, const float*
  * on the batched CSR): physical table p takes the bags of logical table src[p] with the
  * logical indices (kind 0), the quotients trunc((float)idx / coll[p]) (kind 1) or the
  * remainders idx mod coll[p] (kind 2) -> int32 phys_indices / phys_offsets[T_phys*B+1].
- * src / kind / coll are DEVICE int32 arrays of T_phys entries. */
+ * src / kind / coll are DEVICE int32 arrays of T_phys entries.  phys_indices holds
+ * phys_capacity entries: lookups past it are dropped, the offsets are clamped to it (the
+ * bags stay well formed) and DLRM_TBE_ERR_TABLE_CAP is set in *error_flag (may be NULL). */
 int dlrm_qr_expand_csr(int32_t T_phys, int32_t B, const void* indices, int32_t index_bits,
                        const void* offsets, int32_t offset_bits, const int32_t* src,
                        const int32_t* kind, const int32_t* coll,
                        int64_t max_lookups_per_table, int32_t* phys_indices,
-                       int32_t* phys_offsets, dlrm_stream_t stream);
+                       int32_t* phys_offsets, int64_t phys_capacity, int32_t* error_flag,
+                       dlrm_stream_t stream);
 /* E[b][t] = op(P[b][pq[t]], P[b][pr[t]]) (QREmbeddingBag.forward's combine,
  * tricks/qr_embedding_bag.py:166-172; op mult or add) for pr[t] >= 0, else P[b][pq[t]];
  * P: pooled physical tables [B][.][D] (row stride p_batch_stride), E: [B][T][D].
@@ -411,7 +414,9 @@ enum dlrm_gemm_mode {
  * hand-off; the sum order is fixed (bitwise the in-launch result).  PARTIAL needs
  * aligned operands (K % 4 == 0); REDUCE needs N % 4 == 0; `partial` holds
  * dlrm_gemm_f32_partial_bytes(M, N, splits) bytes.  `splits` = 0 in PARTIAL takes the
- * planner's choice (dlrm_gemm_f32_splits); REDUCE must repeat the PARTIAL's value.
+ * planner's choice (dlrm_gemm_f32_splits); a PARTIAL count > 0 must already be
+ * normalized (dlrm_gemm_f32_splits of the problem with that count returns it unchanged;
+ * otherwise INVALID_ARG); REDUCE must repeat the PARTIAL's value.
  * Problems with unaligned operands run on a generic kernel (separate launch, unsplit).
  * The workspace follows dlrm_gemm_f32's rules (zeroed 64 KiB ticket head before first
  * use; one workspace per stream).
@@ -437,7 +442,9 @@ typedef struct dlrm_gemm_problem {
 } dlrm_gemm_problem;
 size_t dlrm_gemm_f32_group_workspace_size(int32_t n, const dlrm_gemm_problem* problems);
 /* The planner's K split for one problem as if launched alone, in its mode (FULL: an
- * in-launch split; PARTIAL: the split a deferred REDUCE will finish). */
+ * in-launch split; PARTIAL: the split a deferred REDUCE will finish).  PARTIAL with
+ * splits > 0: that count normalized to K (at most 32 and ceil(K/32); equal chunks of
+ * 32-multiples), the count the launch will use. */
 int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem);
 size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits);
 int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* problems, void* workspace,

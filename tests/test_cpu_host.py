@@ -109,3 +109,29 @@ def test_trainer_layout_bias_folding():
     for k in (13, 479, 512, 1024):
         kp = _pad4(k + 1)
         assert kp % 4 == 0 and kp >= k + 1
+
+
+def _fake_problem(M, N, K, mode, splits):
+    """A dlrm_gemm_problem with aligned placeholder pointers (host-side checks only)."""
+    from dlrm_hip import _lib
+    return _lib.GemmProblem(1, 0, M, N, K, 1.0, 256, M, 256, N, 256, N + 4, 0, None, None, 0,
+                            N, mode, splits, 256)
+
+
+def test_gemm_partial_split_counts_are_normalized_or_rejected():
+    """a PARTIAL count the planner would lower (K too short for it, or over 32)
+    must not reach the kernel, because its REDUCE repeats the caller's count.
+    dlrm_gemm_f32_splits returns the normalized count; the launch rejects the raw one."""
+    import ctypes
+    from dlrm_hip import _lib, ops
+    lib = _lib.load()
+    for K, req, want in ((2048, 12, 11), (2048, 24, 22), (2048, 8, 8), (2048, 64, 32),
+                         (96, 8, 3), (1024, 1, 1)):
+        q = _fake_problem(1024, 1024, K, ops.GEMM_PARTIAL, req)
+        assert lib.dlrm_gemm_f32_splits(ctypes.byref(q)) == want, (K, req)
+        q.splits = want  # a normalized count maps to itself
+        assert lib.dlrm_gemm_f32_splits(ctypes.byref(q)) == want
+    arr = (_lib.GemmProblem * 1)(_fake_problem(1024, 1024, 2048, ops.GEMM_PARTIAL, 12))
+    with pytest.raises(_lib.DLRMHipError) as e:  # rejected on the host, before any launch
+        _lib.call("dlrm_gemm_f32_group", 1, ctypes.cast(arr, ctypes.c_void_p), None, 0, None)
+    assert e.value.code == 1 and "normalized" in str(e.value)

@@ -190,3 +190,35 @@ def test_record_pipeline_matches_batch_from_records(tmp_path, graph):
     torch.cuda.synchronize()
     assert losses == losses_ref
     assert torch.equal(tr.weights, ref.weights)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb", [1, 3])
+def test_record_pipeline_no_loop_ends_with_stop_iteration(tmp_path, nb):
+    """loop=False reads the file once: every batch in order, then StopIteration on this and
+    every later call - never a blocked queue (the prefetch consumed the reader's
+    end marker one batch early).  Batches equal batch_from_records on the same blocks."""
+    from dlrm_hip.data import RecordPipeline
+    from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+    rng = np.random.RandomState(29)
+    B, mir = 64, 1000
+    rec = rng.randint(0, 1 << 20, (B * nb + 5, 40)).astype(np.int32)
+    rec[:, 0] = rng.randint(0, 2, rec.shape[0])
+    path = tmp_path / "once.bin"
+    rec.tofile(path)
+    cfg = TrainerConfig(m_spa=4, ln_emb=[mir] * 26, ln_bot=[13, 16, 4],
+                        ln_top=[4 + 27 * 26 // 2, 8, 1], loss_function="bce")
+    tr = DLRMTrainer(cfg, device="cuda:0", seed=3)
+    pipe = RecordPipeline(str(path), B, tr, max_ind_range=mir, depth=2, loop=False)
+    try:
+        for k in range(nb):
+            got = pipe.next()
+            want = tr.batch_from_records(torch.from_numpy(rec[k * B:(k + 1) * B]).cuda(),
+                                         max_ind_range=mir)
+            assert torch.equal(got.indices, want.indices) and torch.equal(got.X, want.X)
+            assert torch.equal(got.target, want.target)
+        for _ in range(3):
+            with pytest.raises(StopIteration):
+                pipe.next()
+    finally:
+        pipe.close()

@@ -45,19 +45,35 @@ def _batches(n, B):
     return out
 
 
-def _worker(rank, W, port, sharder, q, graph=False):
+def _worker(rank, W, port, sharder, q, graph=False, fixture=False):
     try:
-        sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd")]
+        sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd"), HERE]
         import torch.distributed as dist
         from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=W)
-        cfg = TrainerConfig(**CFG, loss_function="bce", learning_rate=0.05, sharder=sharder)
-        ref = _ref_model()
-        tr = DLRMTrainer.from_oracle(cfg, ref, device="cuda:0", rank=rank, world_size=W,
-                                     process_group=dist.group.WORLD)
+        if fixture:  # the reference's own gloo run (dist.npz)
+            import dist_fixture as DF
+            g = DF.load()
+            cfg = TrainerConfig(**DF.config(g), loss_function="bce",
+                                learning_rate=float(g["lr"][0]), sharder=sharder)
+            tr = DLRMTrainer(cfg, device="cuda:0", rank=rank, world_size=W,
+                             process_group=dist.group.WORLD, init=False)
+            tr.load_dense(DF.init_mlp(g), DF.init_tables(g))
+            data = [(X.numpy(), lS_o.numpy(), [i.numpy() for i in lS_i], T.numpy())
+                    for X, lS_o, lS_i, T in DF.batches(g)]
+        else:
+            alloc = None
+            if sharder.startswith("alloc:"):  # --sharder=input --allocation=...
+                alloc = [int(v) for v in sharder[6:].split(",")]
+            cfg = TrainerConfig(**CFG, loss_function="bce", learning_rate=0.05,
+                                sharder=sharder, allocation=alloc)
+            ref = _ref_model()
+            tr = DLRMTrainer.from_oracle(cfg, ref, device="cuda:0", rank=rank, world_size=W,
+                                         process_group=dist.group.WORLD)
+            data = _batches(3, 12)
         res = {"Z": [], "E": [], "local": tr.local_tables}
-        batches = [tr.make_batch(X, lS_o, lS_i, T) for X, lS_o, lS_i, T in _batches(3, 12)]
+        batches = [tr.make_batch(X, lS_o, lS_i, T) for X, lS_o, lS_i, T in data]
         runs = [lambda b=b: tr.step(b) for b in batches]
         if graph:  # step 0 eager (allocations), steps 1-2 replayed from captured segments
             tr.step(batches[0])
@@ -71,6 +87,7 @@ def _worker(rank, W, port, sharder, q, graph=False):
             res["Z"].append(Z.cpu().numpy())
             res["E"].append(float(E.cpu()))
         torch.cuda.synchronize()
+        tr.check_errors()
         res["tables"] = {t: tr.table(t).cpu().numpy() for t in tr.local_tables}
         res["dense"] = [(w.cpu().numpy(), b.cpu().numpy()) for w, b in tr.dense_state()]
         dist.barrier()
@@ -81,19 +98,12 @@ def _worker(rank, W, port, sharder, q, graph=False):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("sharder,graph", [("naive", False), ("greedy", False),
-                                           ("greedy", True)])
-def test_two_ranks_match_oracle_distributed_step(sharder, graph):
-    """graph=True: steps replayed from trainer.capture (kernel segments as hipGraphs, the
-    exchanges eager between them), the bench's multi-GPU path."""
-    import oracle as O
-    from conftest import fp32_close
-    from dlrm_hip.sharders import shard
-    W = 2
+def _spawn(W, sharder, graph, fixture):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, W, port, sharder, q, graph)) for r in range(W)]
+    ps = [ctx.Process(target=_worker, args=(r, W, port, sharder, q, graph, fixture))
+          for r in range(W)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(W))
@@ -101,8 +111,23 @@ def test_two_ranks_match_oracle_distributed_step(sharder, graph):
         p.join(timeout=60)
     for r in range(W):
         assert isinstance(res[r], dict), res[r]
+    return res
+
+
+@pytest.mark.parametrize("sharder,graph", [("naive", False), ("greedy", False),
+                                           ("greedy", True), ("alloc:1,1,1,1,1", False)])
+def test_two_ranks_match_oracle_distributed_step(sharder, graph):
+    """graph=True: steps replayed from trainer.capture (kernel segments as hipGraphs, the
+    exchanges eager between them), the bench's multi-GPU path.  "alloc:1,1,1,1,1": rank 0
+    owns no table (sends nothing, receives every feature)."""
+    import oracle as O
+    from conftest import fp32_close
+    from dlrm_hip.sharders import shard
+    W = 2
+    res = _spawn(W, sharder, graph, False)
     ref = _ref_model()
-    di = shard(CFG["ln_emb"], W, sharder)
+    di = [int(v) for v in sharder[6:].split(",")] if sharder.startswith("alloc:") else \
+        shard(CFG["ln_emb"], W, sharder)
     for s, (X, lS_o, lS_i, T) in enumerate(_batches(3, 12)):
         Zs, Es = O.distributed_step(ref, W, di, X, lS_o, lS_i, T, 0.05)
         for r in range(W):
@@ -117,6 +142,140 @@ def test_two_ranks_match_oracle_distributed_step(sharder, graph):
             assert ok, (r, t, msg)
         lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq
                if isinstance(m, torch.nn.Linear)]
+        for i, (w, b) in enumerate(res[r]["dense"]):
+            ok, msg = fp32_close(w, lin[i].weight.detach().numpy())
+            assert ok, (r, "W", i, msg)
+            ok, msg = fp32_close(b, lin[i].bias.detach().numpy())
+            assert ok, (r, "b", i, msg)
+
+
+@pytest.mark.parametrize("W,sharder,graph", [(2, "naive_chunk", False), (2, "naive", False),
+                                             (2, "greedy", True), (4, "naive_chunk", False),
+                                             (4, "greedy", False), (4, "greedy", True)])
+def test_ranks_match_reference_gloo_run(W, sharder, graph):
+    """W ranks of the fused trainer (one GPU, host-staged exchange) against the REFERENCE's
+    own gloo run of distributed_forward + DDP + SGD (dist.npz, make_golden_dist.py): per-rank
+    Z and loss of 3 steps, every rank's final local tables and dense parameters."""
+    import dist_fixture as DF
+    from conftest import fp32_close
+    g = DF.load()
+    res = _spawn(W, sharder, graph, True)
+    for r in range(W):
+        assert res[r]["local"] == g[DF.rank_key(W, sharder, r, "local")].tolist()
+        for s in range(int(g["steps"][0])):
+            ok, msg = fp32_close(res[r]["Z"][s], g[DF.rank_key(W, sharder, r, f"s{s}_Z")].ravel())
+            assert ok, (s, r, msg)
+            ok, msg = fp32_close(np.array([res[r]["E"][s]]),
+                                 g[DF.rank_key(W, sharder, r, f"s{s}_loss")])
+            assert ok, (s, r, msg)
+        for t, w in res[r]["tables"].items():
+            ok, msg = fp32_close(w, g[DF.rank_key(W, sharder, r, f"final_emb{t}")])
+            assert ok, (r, t, msg)
+        names = [("bot", 2 * i) for i in range(len(g["ln_bot"]) - 1)] + \
+                [("top", 2 * i) for i in range(len(g["ln_top"]) - 1)]
+        for (w, b), (pre, i) in zip(res[r]["dense"], names):
+            ok, msg = fp32_close(w, g[DF.rank_key(W, sharder, r, f"final_{pre}.{i}.weight")])
+            assert ok, (r, pre, i, msg)
+            ok, msg = fp32_close(b, g[DF.rank_key(W, sharder, r, f"final_{pre}.{i}.bias")])
+            assert ok, (r, pre, i, msg)
+
+
+def _c3_spec(W):
+    import oracle as O
+    rows = [min(r, 2000) for r in O.TERABYTE_ROWS]
+    # placement of the TRUE Terabyte rows (greedy, the driver default): at W = 8 rank 2
+    # owns 6 tables and rank 0 one (SURVEY.md §8e)
+    alloc = O.shard(O.TERABYTE_ROWS, W, "greedy")
+    D = 128
+    return dict(m_spa=D, ln_emb=rows, ln_bot=[13, 512, 256, D],
+                ln_top=[D + 27 * 26 // 2, 1024, 1024, 512, 256, 1]), alloc
+
+
+def _c3_model():
+    import oracle as O
+    spec, _ = _c3_spec(2)
+    np.random.seed(5)
+    return O.OracleDLRM(spec["m_spa"], spec["ln_emb"], spec["ln_bot"], spec["ln_top"],
+                        loss_function="bce")
+
+
+def _c3_batches(B):
+    rng = np.random.RandomState(12)
+    spec, _ = _c3_spec(2)
+    out = []
+    for _ in range(2):
+        X = torch.tensor(np.log1p(rng.rand(B, 13)).astype(np.float32))
+        lS_o = torch.arange(B).repeat(len(spec["ln_emb"]), 1)
+        lS_i = [torch.tensor(rng.randint(0, n, B)) for n in spec["ln_emb"]]
+        T = torch.tensor(rng.randint(0, 2, (B, 1)).astype(np.float32))
+        out.append((X, lS_o, lS_i, T))
+    return out
+
+
+def _c3_worker(rank, W, port, q, B):
+    try:
+        sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd"), HERE]
+        import torch.distributed as dist
+        from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=W)
+        spec, alloc = _c3_spec(W)
+        cfg = TrainerConfig(**spec, loss_function="bce", learning_rate=0.1, allocation=alloc)
+        tr = DLRMTrainer.from_oracle(cfg, _c3_model(), device="cuda:0", rank=rank,
+                                     world_size=W, process_group=dist.group.WORLD)
+        res = {"Z": [], "E": [], "local": tr.local_tables}
+        for X, lS_o, lS_i, T in _c3_batches(B):
+            Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
+            res["Z"].append(Z.cpu().numpy())
+            res["E"].append(float(E.cpu()))
+        tr.check_errors()
+        res["tables"] = {t: tr.table(t).cpu().numpy() for t in tr.local_tables}
+        res["dense"] = [(w.cpu().numpy(), b.cpu().numpy()) for w, b in tr.dense_state()]
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("W", [4, 8])
+def test_c3_table_list_greedy_ranks_match_oracle(W):
+    """The C3 table list (rows capped at 2000, D = 128, C3 MLP widths) placed as greedy
+    places the TRUE Terabyte rows: W = 4 [2,13,7,4] tables per rank; W = 8 [1,2,6,5,2,3,5,2]
+    (rank 2 owns 6, rank 0 one).  Uneven all-to-all splits, every rank's Z / loss / tables /
+    dense weights vs oracle.distributed_step (itself pinned to the reference's gloo runs)."""
+    import oracle as O
+    from conftest import fp32_close
+    B = 64
+    spec, alloc = _c3_spec(W)
+    per_rank = [alloc.count(r) for r in range(W)]
+    assert per_rank == {4: [2, 13, 7, 4], 8: [1, 2, 6, 5, 2, 3, 5, 2]}[W]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_c3_worker, args=(r, W, port, q, B)) for r in range(W)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(W))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(W):
+        assert isinstance(res[r], dict), res[r]
+    ref = _c3_model()
+    for s, (X, lS_o, lS_i, T) in enumerate(_c3_batches(B)):
+        Zs, Es = O.distributed_step(ref, W, alloc, X, lS_o, lS_i, T, 0.1)
+        for r in range(W):
+            ok, msg = fp32_close(res[r]["Z"][s], Zs[r].numpy().ravel())
+            assert ok, (s, r, msg)
+            ok, msg = fp32_close(np.array([res[r]["E"][s]]), Es[r].numpy().reshape(1))
+            assert ok, (s, r, msg)
+    lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
+    for r in range(W):
+        assert res[r]["local"] == [t for t in range(26) if alloc[t] == r]
+        for t, w in res[r]["tables"].items():
+            ok, msg = fp32_close(w, ref.emb_l[t].weight.detach().numpy())
+            assert ok, (r, t, msg)
         for i, (w, b) in enumerate(res[r]["dense"]):
             ok, msg = fp32_close(w, lin[i].weight.detach().numpy())
             assert ok, (r, "W", i, msg)

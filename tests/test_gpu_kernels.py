@@ -485,6 +485,45 @@ def test_qr_split_and_combine(ops, golden):
         assert torch.allclose(y, ref)
 
 
+def test_qr_expand_csr_vs_oracle_and_capacity(ops):
+    """dlrm_qr_expand_csr: logical CSR -> physical (plain | quotient | remainder) CSR, bit-
+    exact vs the oracle's split (float division, truncation; torch remainder), and with an
+    undersized phys_indices buffer: no write past it, offsets clamped to it,
+    TBE_ERR_TABLE_CAP raised."""
+    rng = np.random.RandomState(3)
+    B, rows = 5, [30, 700, 9]
+    lo = [torch.tensor(np.concatenate([[0], np.sort(rng.randint(0, 9, B - 1))]))
+          for _ in rows]
+    li = [torch.tensor(rng.randint(0, n, int(o[-1]) + 3)) for n, o in zip(rows, lo)]
+    off, idx = O.batched_csr(lo, li)
+    # physical tables: t0 plain, t1 -> quotient (c=4) + remainder, t2 plain
+    src, kind, coll = [0, 1, 1, 2], [0, 1, 2, 0], [1, 4, 4, 1]
+    per = [int(li[t].numel()) for t in range(3)]
+    n = sum(per[s_] for s_ in src)
+    want_idx, want_off, base = [], [], 0
+    for p_, s_ in enumerate(src):
+        v = li[s_].long()
+        q, r = O.QREmbeddingBagOracle.split(v, coll[p_]) if kind[p_] else (v, v)
+        want_idx.append([v, q, r][kind[p_]])
+        want_off.append(lo[s_] + base)
+        base += per[s_]
+    want_off = torch.cat(want_off + [torch.tensor([base])]).to(torch.int32)
+    want_idx = torch.cat(want_idx).to(torch.int32)
+    i32 = dict(dtype=torch.int32, device=dev)
+    args = (torch.tensor(src, **i32), torch.tensor(kind, **i32), torch.tensor(coll, **i32))
+    for cap in (n, n - 7):
+        pidx = torch.full((cap + 16,), -5, **i32)  # 16 guard entries past the capacity
+        poff = torch.empty(4 * B + 1, **i32)
+        flag = torch.zeros(1, **i32)
+        ops.qr_expand_csr(4, B, idx.to(dev), off.to(dev), *args, max(per), pidx[:cap], poff,
+                          error_flag=flag)
+        torch.cuda.synchronize()
+        assert torch.equal(pidx[:cap].cpu(), want_idx[:cap])
+        assert (pidx[cap:] == -5).all()
+        assert torch.equal(poff.cpu(), want_off.clamp(max=cap))
+        assert int(flag.item()) == (0 if cap == n else ops.TBE_ERR_TABLE_CAP)
+
+
 def test_csr_builder_device(ops):
     lo = [torch.tensor([0, 3, 5]), torch.tensor([0, 0, 2]), torch.tensor([0, 1, 4])]
     li = [torch.arange(7), torch.arange(4), torch.arange(6)]
@@ -882,3 +921,61 @@ def test_tbe_backward_tiled_sort_cap_violation(ops):
     torch.cuda.synchronize()
     assert int(flag.item()) & 2  # TBE_ERR_TABLE_CAP
     assert torch.equal(W, W0)  # both tables overflow their 2 tiles: nothing updated
+
+
+def _c1_case(dist: str, seed: int):
+    """C1 table shape: 8 x 1e5 rows, D = 64, B = 2048, L = 100 (1.64 M lookups, >= 2^18:
+    the long-block path).  uniform: the reference generator's distribution (sorted within
+    a bag); zipf: Zipf(1.05) ranks folded onto the rows (SURVEY.md §8d's skew run: row 0
+    takes ~5 % of a table's lookups, so its run crosses ~160 blocks of 64)."""
+    T, R, D, B, L = 8, 100000, 64, 2048, 100
+    rng = np.random.RandomState(seed)
+    if dist == "uniform":
+        li = np.sort(rng.randint(0, R, (T, B, L)), axis=2)
+    else:
+        li = (rng.zipf(1.05, (T, B, L)) - 1) % R
+    idx = torch.tensor(li.reshape(-1), dtype=torch.int32)
+    off = torch.arange(T * B + 1, dtype=torch.int32) * L
+    g = torch.Generator().manual_seed(seed)
+    W0 = torch.empty(T * R, D).uniform_(-0.05, 0.05, generator=g)
+    G = torch.empty(B, T, D).uniform_(-1.0, 1.0, generator=g)
+    row_base = torch.arange(T + 1, dtype=torch.int64) * R
+    return T, R, D, B, L, idx, off, W0, G, row_base
+
+
+@pytest.mark.parametrize("dist", ["uniform", "zipf"])
+def test_tbe_c1_full_shape_forward_and_backward_vs_oracle(ops, monkeypatch, dist):
+    """The C1-shape lookup and its backward + exact SGD at FULL size against the oracle:
+    forward vs nn.EmbeddingBag (fp32, lookup order), backward vs the fp64 coalesced update
+    W0 - lr * sum(g), with the block length forced to 16 and to 64 (DLRM_TBE_CH) and left
+    to the planner (64 at this size; the planner's choice is bitwise the forced 64)."""
+    T, R, D, B, L, idx, off, W0, G, row_base = _c1_case(dist, 17 if dist == "uniform" else 18)
+    lr = 0.25
+    out = ops.tbe_forward(W0.to(dev), row_base.to(dev), T, B, idx.to(dev), off.to(dev)).cpu()
+    for t in range(T):
+        e = torch.nn.functional.embedding_bag(idx[t * B * L:(t + 1) * B * L].long(),
+                                              W0[t * R:(t + 1) * R],
+                                              torch.arange(B) * L, mode="sum")
+        ok, msg = fp32_close(out[:, t].numpy(), e.numpy())
+        assert ok, (t, msg)
+    gsum = torch.zeros(T * R, D, dtype=torch.float64)
+    bag = torch.arange(B * L) // L
+    for t in range(T):
+        gsum.index_add_(0, t * R + idx[t * B * L:(t + 1) * B * L].long(), G[bag, t].double())
+    ref = (W0.double() - lr * gsum).numpy()
+    res = {}
+    for ch in ("16", "64", ""):
+        if ch:
+            monkeypatch.setenv("DLRM_TBE_CH", ch)
+        else:
+            monkeypatch.delenv("DLRM_TBE_CH", raising=False)
+        W = W0.to(dev)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops.tbe_backward("sgd", W, row_base.to(dev), T, B, idx.to(dev), off.to(dev), G.to(dev),
+                         lr=lr, max_lookups_per_table=B * L, error_flag=flag)
+        torch.cuda.synchronize()
+        assert int(flag.item()) == 0
+        res[ch] = W.cpu()
+        ok, msg = fp32_close(res[ch].numpy(), ref)
+        assert ok, (ch, msg)
+    assert torch.equal(res["64"], res[""])

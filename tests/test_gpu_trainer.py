@@ -313,3 +313,108 @@ def test_qr_step_vs_oracle(op, optimizer, graph):
         for g_, w_ in zip(got, want):
             ok, msg = fp32_close(g_.cpu().numpy(), w_.detach().numpy())
             assert ok, ("emb", k, msg)
+
+
+def test_c1_full_shape_step_vs_oracle():
+    """C1 (bench/dlrm_s_benchmark.sh:36-43) at its FULL shape: 8 x 1e5 rows, D = 64,
+    B = 2048, L = 100 (1.64 M lookups per step: the long-block TBE backward and the tiled
+    per-table sort, the paths bench --config small times), 2 SGD steps vs the oracle."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    D, rows, B, L = 64, [100000] * 8, 2048, 100
+    bot, top = [512, 512, 64], [1024, 1024, 1024, 1]
+    ln_top = [_num_int(len(rows), D)] + top
+    np.random.seed(21)
+    ref = O.OracleDLRM(D, rows, bot, ln_top, loss_function="mse")
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=bot, ln_top=ln_top, loss_function="mse",
+                        learning_rate=0.1)
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    rng = np.random.RandomState(4)
+    for s in range(2):
+        X, lS_o, lS_i, T = _rand_batch(rng, rows, B, L, bot[0], "mse")
+        Zr, Er = ref.train_step(torch.tensor(X), torch.tensor(lS_o),
+                                [torch.tensor(i) for i in lS_i], torch.tensor(T), 0.1)
+        Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
+        assert ok, (s, msg)
+        ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
+        assert ok, (s, msg)
+    tr.check_errors()
+    _compare_state(tr, ref)
+
+
+def _checksums(W: torch.Tensor, row_base):
+    """Per-table (sum, row-weighted sum) of the device tables in fp64, in 1 M-row pieces."""
+    out = []
+    for t in range(len(row_base) - 1):
+        s0 = s1 = 0.0
+        a, b = int(row_base[t]), int(row_base[t + 1])
+        for c in range(a, b, 1 << 20):
+            e = min(b, c + (1 << 20))
+            blk = W[c:e].double()
+            w = (torch.arange(c, e, device=W.device, dtype=torch.float64) % 1021 + 1)
+            s0 += float(blk.sum())
+            s1 += float((blk.sum(1) * w).sum())
+        out.append((s0, s1))
+    return out
+
+
+def test_c3_true_terabyte_rows_vs_touched_row_oracle():
+    """C3 at the TRUE Terabyte row counts (54,063,992 rows, 27.7 GB on the device; 24-bit
+    keys in the per-table LDS sort of the lookup launch, 64-bit row bases), B = 2048, the
+    bench's synthetic batches and fused step, 2 steps.  The CPU oracle materialises only the
+    rows the batches touch: each table's indices are remapped to its sorted unique-row list
+    and those rows copied from the device.  Compared: Z and loss per step, every touched
+    row after the updates, and per-table checksums of the whole tables (untouched rows
+    unchanged: the checksum moves by exactly the touched rows' change)."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    rows, D, B = list(O.TERABYTE_ROWS), 128, 2048
+    bot, top = [13, 512, 256, 128], [1024, 1024, 512, 256, 1]
+    ln_top = [_num_int(len(rows), D)] + top
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=bot, ln_top=ln_top, loss_function="bce",
+                        learning_rate=0.1)
+    tr = DLRMTrainer(cfg, device=dev, seed=3)
+    assert tr.total_rows == 54063992
+    batches = [tr.synthetic_batch(B, 1, seed=40 + s) for s in range(2)]
+    T = len(rows)
+    idx = [b.indices.view(T, B).long().cpu() for b in batches]
+    uniq = [torch.unique(torch.cat([i[t] for i in idx])) for t in range(T)]
+    assert max(int(u.max()) for u in uniq) >= (1 << 23)  # 24-bit keys really occur
+    rb = tr.row_base.cpu()
+    gidx = [(u + int(rb[t])).to(dev) for t, u in enumerate(uniq)]
+    tabs0 = [tr.weights.index_select(0, g).cpu().numpy() for g in gidx]
+    sums0 = _checksums(tr.weights, rb)
+    ref = O.OracleDLRM(D, [len(u) for u in uniq], bot, ln_top, loss_function="bce",
+                       tables=tabs0)
+    lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
+    with torch.no_grad():
+        for m, (W, b) in zip(lin, tr.dense_state()):
+            m.weight.copy_(W.cpu())
+            m.bias.copy_(b.cpu())
+    for s, b in enumerate(batches):
+        X = b.X[:, :13].cpu()
+        lS_o = torch.arange(B).repeat(T, 1)
+        lS_i = [torch.searchsorted(uniq[t], idx[s][t]) for t in range(T)]  # compact rows
+        Tg = b.target.cpu().view(-1, 1)
+        Zr, Er = ref.train_step(X, lS_o, lS_i, Tg, 0.1)
+        Z, E = tr.step(b)
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
+        assert ok, (s, msg)
+        ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
+        assert ok, (s, msg)
+    torch.cuda.synchronize()
+    tr.check_errors()
+    sums1 = _checksums(tr.weights, rb)
+    for t in range(T):
+        got = tr.weights.index_select(0, gidx[t]).cpu().double()
+        want = ref.emb_l[t].weight.detach()
+        ok, msg = fp32_close(got.numpy(), want.double().numpy())
+        assert ok, ("table", t, msg)
+        w = (gidx[t].cpu().double() % 1021 + 1)
+        d0 = float((got - torch.tensor(tabs0[t]).double()).sum())
+        d1 = float(((got - torch.tensor(tabs0[t]).double()).sum(1) * w).sum())
+        tol = 1e-6 * (1 + abs(sums0[t][0])) + 1e-4
+        assert abs((sums1[t][0] - sums0[t][0]) - d0) <= tol, ("checksum", t)
+        assert abs((sums1[t][1] - sums0[t][1]) - d1) <= 1100 * tol, ("weighted checksum", t)
+    for m, (W, b_) in zip(lin, tr.dense_state()):
+        ok, msg = fp32_close(W.cpu().numpy(), m.weight.detach().numpy())
+        assert ok, msg
