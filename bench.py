@@ -243,6 +243,87 @@ def gather_rooflines(tr, batch, B, c, dev):
     return out
 
 
+def box_calibration(dev):
+    """Fixed-work probes that separate box-to-box variance from code regressions: the
+    library's own f32 MFMA GEMM at 4096^3 (TFLOP/s), a 1 GiB device-to-device copy (GB/s,
+    read + write), and the clocks the SMI reports (rocm-smi; may be absent)."""
+    from dlrm_hip import ops
+    out = {}
+    try:
+        g = torch.Generator(device=dev).manual_seed(3)
+        n = 4096
+        A = torch.randn(n, n, device=dev, generator=g)
+        Bm = torch.randn(n, n, device=dev, generator=g)
+        C = torch.empty(n, n, device=dev)
+        ws = torch.zeros(ops.gemm_group_workspace_size([ops.gemm_problem(A, Bm, C=C)[0]]) + 256,
+                         dtype=torch.uint8, device=dev)
+        us = _graph_time_us(lambda: ops.gemm(A, Bm, C=C, workspace=ws), n=5, reps=4)
+        out["gemm_f32_4096_tflops"] = round(2 * n ** 3 / us / 1e6, 2)
+        src = torch.empty(1 << 28, device=dev)  # 1 GiB
+        dst = torch.empty_like(src)
+        us = _graph_time_us(lambda: dst.copy_(src), n=5, reps=4)
+        out["copy_1gib_gbs"] = round(2 * src.numel() * 4 / us / 1e3, 1)
+        del A, Bm, C, src, dst
+    except Exception as e:  # noqa: BLE001
+        out["error"] = repr(e)
+    try:
+        import subprocess
+        r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True,
+                           text=True, timeout=30)
+        d = json.loads(r.stdout) if r.returncode == 0 else {}
+        card = d.get(sorted(d)[0], {}) if d else {}
+        out["smi_clocks"] = {k: v for k, v in card.items()
+                             if k.lower().startswith(("sclk", "mclk", "fclk"))}
+    except Exception as e:  # noqa: BLE001
+        out["smi_clocks"] = repr(e)
+    return out
+
+
+def hbm_gather_roofline(dev, nb=10):
+    """The lookup's HBM rate with the caches out of the picture: a C1-like lookup (8 tables,
+    D = 64, L = 100, B = 2048: 1.64 M random rows per call) over 8 x 1e6 rows (2 GB, 8x the
+    256 MB Infinity Cache), a FRESH batch per call (10 distinct index sets replayed in
+    turn), forward and backward + exact SGD.  The C1-shape figures above reuse one batch
+    over a 205 MB table set that the Infinity Cache holds."""
+    from dlrm_hip import ops
+    T, R, D, L, B = 8, 1_000_000, 64, 100, 2048
+    g = torch.Generator(device=dev).manual_seed(11)
+    W = torch.empty(T * R, D, device=dev).uniform_(-0.003, 0.003, generator=g)
+    rb = torch.arange(T + 1, dtype=torch.int64, device=dev) * R
+    idxs = [torch.randint(0, R, (T * B * L,), dtype=torch.int32, device=dev, generator=g)
+            for _ in range(nb)]
+    off = torch.arange(T * B + 1, dtype=torch.int32, device=dev) * L
+    pooled = torch.empty(B, T, D, device=dev)
+    grad = torch.empty(B, T, D, device=dev).uniform_(-1e-3, 1e-3, generator=g)
+    ws = torch.empty(ops.tbe_backward_workspace_size(T * B * L, T * R, D), dtype=torch.uint8,
+                     device=dev)
+    k = [0]
+
+    def fwd():
+        ops.tbe_forward(W, rb, T, B, idxs[k[0] % nb], off, out=pooled)
+        k[0] += 1
+
+    def bwd():
+        ops.tbe_backward("sgd", W, rb, T, B, idxs[k[0] % nb], off, grad, lr=1e-9, workspace=ws,
+                         max_lookups_per_table=B * L)
+        k[0] += 1
+    n = T * B * L
+    fus = _graph_time_us(fwd, n=nb, reps=3)
+    bus = _graph_time_us(bwd, n=nb, reps=3)
+    fby = n * (4 * D + 4) + 4 * (T * B + 1) + 4 * T * B * D
+    uniq = int(torch.unique(idxs[0].view(T, -1).long()
+                            + torch.arange(T, device=dev).view(-1, 1) * R).numel())
+    bby = 4 * T * B * D + n * 4 + uniq * 8 * D
+    del W, idxs, ws
+    return {"tables": T, "rows": R, "emb_dim": D, "lookups_per_bag": L, "batch": B,
+            "table_bytes": T * R * D * 4, "fresh_batches": nb,
+            "fwd_us": round(fus, 2), "fwd_bytes": fby, "fwd_achieved": round(fby / fus / 1e3, 1),
+            "fwd_frac": round(fby / fus / 1e3 / HBM_PEAK_GBS, 4),
+            "bwd_sgd_us": round(bus, 2), "unique_rows": uniq, "bwd_bytes_dedup": bby,
+            "bwd_achieved_dedup": round(bby / bus / 1e3, 1),
+            "bwd_frac_dedup": round(bby / bus / 1e3 / HBM_PEAK_GBS, 4)}
+
+
 def input_pipeline_rate(tr, c, B, dev, steps=60, warmup=5, nb=16):
     """The step fed from Criteo binary records on the host: a
     synthetic record file of the workload's shape (label, 13 dense counts, 26 indices within
@@ -291,12 +372,66 @@ def input_pipeline_rate(tr, c, B, dev, steps=60, warmup=5, nb=16):
         os.unlink(path)
 
 
-def cpu_baseline(c, seconds: float):
-    """The CPU oracle (a restatement of the reference step, pinned to its golden vectors)
-    timed on this host's cores: bounded sample of the same workload."""
+def socket0_physical_cores(limit: int):
+    """One hardware thread per physical core of CPU package 0, within this process's allowed
+    CPUs (bench/dlrm_s_benchmark.sh:20-25 binds `numactl --physcpubind=<socket 0 physical
+    cores> -m 0`), at most ``limit`` of them (the GPU box's CPU share per GPU is 16)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    seen, cores = set(), []
+    for cpu in allowed:
+        base = f"/sys/devices/system/cpu/cpu{cpu}/topology"
+        try:
+            pkg = int(open(f"{base}/physical_package_id").read())
+            core = int(open(f"{base}/core_id").read())
+        except OSError:
+            pkg, core = 0, cpu
+        if pkg != 0 or core in seen:
+            continue
+        seen.add(core)
+        cores.append(cpu)
+    return cores[:limit] if cores else allowed[:limit]
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(c, seconds: float, config_name: str, max_cores: int = 16):
+    """The CPU oracle (a restatement of the reference step, pinned to its golden vectors and
+    calibrated against the reference's own DLRM_Net step: profiles/r03_cpu_calibration.json)
+    timed on this host: a CHILD process (no GPU runtime in it: HIP/CUDA devices hidden) pinned
+    to socket 0's physical cores, one torch thread per core; memory is first-touch on the
+    pinned cores' node (numactl is not in the image).  Bounded sample of the same workload."""
+    import subprocess
+    cores = socket0_physical_cores(max_cores)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
+               ROCR_VISIBLE_DEVICES="", OMP_NUM_THREADS=str(len(cores)))
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", "--config", config_name,
+           "--cpu-seconds", str(seconds), "--cpu-cores", ",".join(map(str, cores))]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True,
+                           timeout=seconds * 4 + 240)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            return {"error": f"cpu child rc={r.returncode}: {r.stderr[-400:]}"}
+        return json.loads(line[-1])
+    except Exception as e:  # noqa: BLE001 - reported; the headline line must still print
+        return {"error": repr(e)}
+
+
+def cpu_child(c, seconds: float, cores):
+    """Runs in the pinned child: times the oracle's training step (SGD at the workload's lr
+    scaled by 0.01 so the capped tables stay finite; the step's work does not depend on lr)."""
+    os.sched_setaffinity(0, cores)
+    torch.set_num_threads(len(cores))
     sys.path.insert(0, ROOT)
     import oracle as O
-    threads = torch.get_num_threads()
     cap = 1_000_000
     rows = [min(r, cap) for r in c["rows"]]
     D = c["D"]
@@ -332,11 +467,16 @@ def cpu_baseline(c, seconds: float):
         el = time.perf_counter() - t0
         if (el >= seconds and n >= 3) or n >= 2000:
             break
-    return {"value": B * n / el, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (torch-CPU restatement of the reference step) on the "
-                      f"{c['workload']} shape with tables capped at {cap} rows, B={B}, "
-                      f"{n} timed steps ({el:.1f} s), {threads} threads",
-            "ms_per_step": 1000.0 * el / n}
+    capped = sum(1 for r in c["rows"] if r > cap)
+    print(json.dumps({
+        "value": B * n / el, "unit": "samples/s", "cores": len(cores), "kind": "port",
+        "cpu_model": cpu_model(), "cpu_list": cores,
+        "binding": "socket 0, one thread per physical core (os.sched_setaffinity; first-touch "
+                   "memory on that node), torch threads = cores",
+        "sample": f"oracle (torch-CPU restatement of the reference step) on the "
+                  f"{c['workload']} shape, B={B}, {n} timed steps ({el:.1f} s)"
+                  + (f", {capped} tables capped at {cap} rows" if capped else ""),
+        "ms_per_step": 1000.0 * el / n}), flush=True)
 
 
 def main():
@@ -346,11 +486,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="terabyte", choices=list(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="global batch (default: config's)")
+    ap.add_argument("--lr", type=float, default=0.0, help="learning rate (default: config's)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-cores", default="", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_child:  # the pinned CPU-baseline process (no GPU runtime)
+        cpu_child(dict(CONFIGS[args.config]), args.cpu_seconds,
+                  [int(v) for v in args.cpu_cores.split(",") if v])
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -370,6 +517,8 @@ def main():
     from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
 
     c = dict(CONFIGS[args.config])
+    if args.lr > 0:
+        c["lr"] = args.lr
     B = args.batch or c["B"]
     T = len(c["rows"])
     ln_top = [num_int(T, c["D"])] + c["top"]
@@ -397,6 +546,12 @@ def main():
             pool = torch.cuda.graph_pool_handle()
             graphs = [tr.capture(batches[i], pool=pool) for i in range(nb)]
             torch.cuda.synchronize()
+            # setup, not warm-up: replay every captured graph twice so the first (upload)
+            # replay of each of the nb graphs happens here, whatever --warmup is
+            for _ in range(2):
+                for gr in graphs:
+                    gr()
+            torch.cuda.synchronize()
         except Exception as e:  # capture unsupported -> eager
             print(f"[bench] hipGraph capture failed ({e!r}); eager launches", file=sys.stderr)
             graphs = None
@@ -417,6 +572,7 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    loss_first = float(tr._bufs[(B // world, B)]["loss"].item())  # after setup + warm-up
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     evs[0].record()
@@ -437,7 +593,7 @@ def main():
     loss = float(tr._bufs[(B // world, B)]["loss"].item())
 
     # ---- per-kernel HIP-event timing pass (same step, eager launches) for the roofline
-    roofline, emb_roof, groups = None, None, None
+    roofline, emb_roof, groups, interaction_roof = None, None, None, None
     Bl = B // world
     # lookups run on the physical tables (a QR table is a quotient + a remainder table)
     flops, fwd_bytes, bwd_bytes = algorithmic_work(c, Bl, B, tr.T_phys, world,
@@ -472,6 +628,21 @@ def main():
                         "timing": f"per-group hipGraph of {cap_steps} steps' launches, HIP "
                                   f"events over {reps} replays",
                         "algorithmic_flop_per_step": flops}
+        i_us = tot_us.get("interaction_fwd", 0.0) + tot_us.get("interaction_bwd", 0.0)
+        if i_us > 0 and c.get("interaction", "dot") == "dot":
+            F = len(c["rows"]) + 1
+            alg = 3 * F * (F - 1) * c["D"] * Bl          # fwd F(F-1)D + bwd 2F(F-1)D per sample
+            Fp = (F + 31) // 32 * 32                       # the kernels' 32-padded Gram tiles
+            issued = 3 * 2 * Fp * Fp * c["D"] * Bl
+            interaction_roof = {
+                "bound": "mfma (fp32 v_mfma_f32_32x32x2f32)", "us_per_step": round(i_us, 2),
+                "algorithmic_flop_per_step": alg, "mfma_flop_per_step": issued,
+                "achieved_tflops": round(alg / i_us / 1e6, 3),
+                "frac_of_fp32_peak": round(alg / i_us / 1e6 / FP32_MFMA_PEAK_TFS, 4),
+                "issued_mfma_frac": round(issued / i_us / 1e6 / FP32_MFMA_PEAK_TFS, 4),
+                "hbm_bytes_per_step": (F * c["D"] + F * (F - 1) // 2 + c["D"]) * 4 * Bl * 2,
+                "hbm_achieved_gbs": round((F * c["D"] + F * (F - 1) // 2 + c["D"]) * 8 * Bl
+                                          / i_us / 1e3, 1)}
         f_ms = tot.get("tbe_fwd", 0.0)
         b_ms = tot.get("tbe_bwd", 0.0)
         if f_ms > 0 and b_ms > 0:
@@ -485,14 +656,21 @@ def main():
                                     "backward's index sort and the bottom MLP forward"}
         if rank == 0 and world == 1 and emb_roof is not None:
             emb_roof.update(gather_rooflines(tr, batches[0], B, c, dev))
+            try:
+                emb_roof["hbm_fresh_batches"] = hbm_gather_roofline(dev)
+            except Exception as e:  # noqa: BLE001 - reported; the line must still print
+                emb_roof["hbm_fresh_batches"] = {"error": repr(e)}
 
+    calib = None
+    if not args.no_kernel_timing:
+        calib = box_calibration(dev)
     pipe_rate = None
     if world == 1 and not args.no_kernel_timing:
         pipe_rate = input_pipeline_rate(tr, c, B, dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(c, args.cpu_seconds)
+        cpu = cpu_baseline(c, args.cpu_seconds, args.config)
 
     if rank == 0:
         line = {
@@ -508,14 +686,17 @@ def main():
                        "optimizer": c["optimizer"], "qr": c.get("qr"),
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
                        "hip_graph": use_graph},
-            "loss_last": loss,
+            "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,
+            "loss_before_timed": loss_first, "loss_last": loss, "lr": c["lr"],
             "roofline": roofline,
             "embedding_roofline": emb_roof,
+            "interaction_roofline": interaction_roof,
             "kernel_us_per_step": groups,
+            "box_calibration": calib,
             "input_pipeline": pipe_rate,
             "cpu_baseline": cpu,
         }
-        if cpu:
+        if cpu and "value" in cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
     if world > 1:

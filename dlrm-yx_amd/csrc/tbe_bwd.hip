@@ -536,9 +536,9 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
     const KeyT prev_key = has_prev ? keys[i0 - 1] : sentinel;
     const KeyT next_key = has_next ? keys[i1] : sentinel;
 
-    V acc[MAXV];
+    V acc[MAXV], comp[MAXV];  // run sum, Kahan-compensated (hot rows: long runs)
 #pragma unroll
-    for (int c = 0; c < MAXV; ++c) vzero(acc[c]);
+    for (int c = 0; c < MAXV; ++c) vzero(acc[c]), vzero(comp[c]);
     KeyT cur = sentinel;
     int64_t seg_a = i0;
     bool have = false;
@@ -553,6 +553,8 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
 
     auto flush = [&](int64_t b_end) {
       if (cur == sentinel) return;
+#pragma unroll
+      for (int c = 0; c < MAXV; ++c) vsub(acc[c], comp[c]);  // fold the compensation in
       const bool starts = (seg_a > i0) || !has_prev || (prev_key != cur);
       const bool ends = (b_end < i1) || !has_next || (next_key != cur);
       if (starts && ends) {
@@ -645,7 +647,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
               cur = ku[u];
               seg_a = base + j + u;
 #pragma unroll
-              for (int c = 0; c < MAXV; ++c) vzero(acc[c]);
+              for (int c = 0; c < MAXV; ++c) vzero(acc[c]), vzero(comp[c]);
               if constexpr (PF) {
 #pragma unroll
                 for (int c = 0; c < MAXV; ++c) wcur[c] = wv[u][c];
@@ -653,7 +655,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
               }
             }
 #pragma unroll
-            for (int c = 0; c < MAXV; ++c) vadd(acc[c], gv[u][c]);
+            for (int c = 0; c < MAXV; ++c) vkahan(acc[c], comp[c], gv[u][c]);
           }
         }
       }
@@ -723,7 +725,11 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
       else
         vzero(acc[c]);
     }
-    // partials of blocks k+1 .. kend in block order, NF loads in flight
+    // partials of blocks k+1 .. kend in block order, NF loads in flight, Kahan-compensated
+    // (a hot row's run crosses hundreds of blocks)
+    V comp[MAXV];
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) vzero(comp[c]);
     constexpr int NF = MAXV <= 2 ? 16 : 8;
     for (int64_t kk0 = k + 1; kk0 <= kend; kk0 += NF) {
       V pv[NF][MAXV];
@@ -743,9 +749,11 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
       for (int u = 0; u < NF; ++u)
         if (kk0 + u <= kend) {
 #pragma unroll
-          for (int c = 0; c < MAXV; ++c) vadd(acc[c], pv[u][c]);
+          for (int c = 0; c < MAXV; ++c) vkahan(acc[c], comp[c], pv[u][c]);
         }
     }
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) vsub(acc[c], comp[c]);  // fold the compensation back in
     finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)last, acc, gl, nchunks, lr, eps);
   }
 }

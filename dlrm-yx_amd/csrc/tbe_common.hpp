@@ -26,6 +26,24 @@ __device__ __forceinline__ void vadd(float4& a, const float4& b) {
   a.w += b.w;
 }
 __device__ __forceinline__ void vadd(float& a, const float& b) { a += b; }
+// Compensated (Kahan) accumulation a += b, c carrying the lost low-order part: long runs
+// of one row (hot rows: thousands of lookups) keep fp32 sums close to the exact sum.
+__device__ __forceinline__ void vkahan(float& a, float& c, float b) {
+  const float y = b - c;
+  const float t = a + y;
+  c = (t - a) - y;
+  a = t;
+}
+__device__ __forceinline__ void vsub(float& a, const float& b) { a -= b; }
+__device__ __forceinline__ void vsub(float4& a, const float4& b) {
+  a.x -= b.x, a.y -= b.y, a.z -= b.z, a.w -= b.w;
+}
+__device__ __forceinline__ void vkahan(float4& a, float4& c, const float4& b) {
+  vkahan(a.x, c.x, b.x);
+  vkahan(a.y, c.y, b.y);
+  vkahan(a.z, c.z, b.z);
+  vkahan(a.w, c.w, b.w);
+}
 __device__ __forceinline__ void vfma(float4& a, float w, const float4& b) {
   a.x = fmaf(w, b.x, a.x);
   a.y = fmaf(w, b.y, a.y);

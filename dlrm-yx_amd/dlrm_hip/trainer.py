@@ -322,7 +322,8 @@ class DLRMTrainer:
             idxs.append(ii)
             start += ii.numel()
         offsets = torch.cat(offs + [torch.tensor([start])]).to(torch.int32).to(self.dev)
-        indices = torch.cat(idxs).to(torch.int32).to(self.dev)
+        indices = (torch.cat(idxs) if idxs else torch.zeros(0, dtype=torch.int64)).to(
+            torch.int32).to(self.dev)  # a rank may own no table
         tg = torch.as_tensor(target).reshape(-1)[sl].to(torch.float32).to(self.dev)
         mx = max([int(i.numel()) for i in idxs], default=0)
         return Batch(Xp, offsets, indices, tg, mx)

@@ -576,13 +576,19 @@ def test_tbe_backward_table_cap_violation_is_skipped_and_flagged(ops, mode):
 
 
 def test_module_lookup_raises_index_error(ops):
-    """The drop-in EmbeddingBag path raises IndexError like nn.EmbeddingBag."""
+    """The drop-in EmbeddingBag path raises IndexError like nn.EmbeddingBag: at once with
+    strict_indices="sync", at the module's next call by default (no host sync per call;
+    test_gpu_module.py::test_module_index_errors_are_deferred_not_synced)."""
     from dlrm_hip.modules import TableBatchedEmbeddingBags
     m = TableBatchedEmbeddingBags(2, [10, 20], 8).to(dev)
     off = torch.tensor([0, 1, 2, 3, 4], dtype=torch.int32, device=dev)
     idx = torch.tensor([1, 2, 3, 4], dtype=torch.int32, device=dev)
     assert m(idx, off).shape == (2, 2, 8)
     bad = torch.tensor([1, 10, 3, 4], dtype=torch.int32, device=dev)  # 10 >= rows of table 0
+    m(bad, off)
+    with pytest.raises(IndexError):
+        m(idx, off)
+    m.strict_indices = "sync"
     with pytest.raises(IndexError):
         m(bad, off)
 

@@ -66,7 +66,7 @@ def accuracy(dev):
     print(line, flush=True)
 
 
-def timing(dev, B, cfgs):
+def timing(dev, B, cfgs, maths=("x6",)):
     ws = torch.zeros(256 << 20, dtype=torch.uint8, device=dev)
     tot = {}
     for li, (K, N) in enumerate(LAYERS["terabyte"]):
@@ -97,29 +97,30 @@ def timing(dev, B, cfgs):
                 s = ops.gemm_splits(pr, partial=name == "wgrad") if name == "wgrad" else 0
                 pr = mk(s)
                 res[m] = timeit(lambda: ops.gemm_group([pr], ws))
-            set_math("x6")
-            for c in cfgs:
-                os.environ["DLRM_GEMM_CFG"] = c
-                for s in ([1, 2, 4, 8] if name == "wgrad" else [1]):
-                    os.environ["DLRM_GEMM_SPLIT"] = str(s)
-                    pr = mk(s)
-                    try:
-                        res[f"x6:{c}s{s}"] = timeit(lambda: ops.gemm_group([pr], ws))
-                    except Exception as e:  # noqa: BLE001
-                        print("skip", c, s, e)
-                os.environ.pop("DLRM_GEMM_SPLIT", None)
+            for math in maths:
+                set_math(math)
+                for c in cfgs:
+                    os.environ["DLRM_GEMM_CFG"] = c
+                    for s in ([1, 2, 4, 8] if name == "wgrad" else [1, 2]):
+                        os.environ["DLRM_GEMM_SPLIT"] = str(s)
+                        pr = mk(s)
+                        try:
+                            res[f"{math}:{c}s{s}"] = timeit(lambda: ops.gemm_group([pr], ws))
+                        except Exception as e:  # noqa: BLE001
+                            print("skip", c, s, e)
+                    os.environ.pop("DLRM_GEMM_SPLIT", None)
             os.environ.pop("DLRM_GEMM_CFG", None)
-            best = min((v, k) for k, v in res.items() if k.startswith("x6"))
+            best = min((v, k) for k, v in res.items() if k.startswith("x6") or ":" in k)
             for k, v in res.items():
                 tot[k] = tot.get(k, 0.0) + v
             tot["x6best"] = tot.get("x6best", 0.0) + best[0]
             print(f"L{li} {name:5s} {fl / 1e9:5.2f} GF  f32 {res['f32'] * 1e6:6.1f} us "
                   f"({fl / res['f32'] / 1e12:5.1f} TF)  x6 {res['x6'] * 1e6:6.1f} us "
                   f"({fl / res['x6'] / 1e12:5.1f} TF)  best x6 {best[1]} {best[0] * 1e6:6.1f} us  | "
-                  + " ".join(f"{k[3:]}:{v * 1e6:.1f}" for k, v in res.items()
-                             if k.startswith("x6:")), flush=True)
+                  + " ".join(f"{k}:{v * 1e6:.1f}" for k, v in res.items()
+                             if ":" in k), flush=True)
     print("TOTAL " + " ".join(f"{k}:{v * 1e6:.1f}" for k, v in tot.items()
-                              if not k.startswith("x6:")))
+                              if ":" not in k))
 
 
 def main():
@@ -127,11 +128,12 @@ def main():
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--cfgs", default="64x64,64x32,32x64")
     ap.add_argument("--skip-acc", action="store_true")
+    ap.add_argument("--maths", default="x6")
     args = ap.parse_args()
     dev = "cuda"
     if not args.skip_acc:
         accuracy(dev)
-    timing(dev, args.batch, args.cfgs.split(","))
+    timing(dev, args.batch, args.cfgs.split(","), args.maths.split(","))
     os.environ.pop("DLRM_GEMM_MATH", None)
 
 
