@@ -243,6 +243,27 @@ def gather_rooflines(tr, batch, B, c, dev):
     return out
 
 
+def preheat_device(dev, ms: float) -> float:
+    """Setup, not measurement: a 4096^3 GEMM loop on scratch buffers (no model state read or
+    written) for ~ms milliseconds.  From idle the chip needs ~50 steps (~25 ms) of load to
+    reach its steady clocks (tools/ramp_probe.py, profiles/r03_ramp_probe.txt: the first 50
+    steps average 487 us against 451 us after), which a 5-step warm-up does not give."""
+    from dlrm_hip import ops
+    n = 4096
+    A = torch.randn(n, n, device=dev)
+    C = torch.empty(n, n, device=dev)
+    ws = torch.zeros(ops.gemm_group_workspace_size([ops.gemm_problem(A, A, C=C)[0]]) + 256,
+                     dtype=torch.uint8, device=dev)
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(4):
+            ops.gemm(A, A, C=C, workspace=ws)
+        torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) * 1e3
+    del A, C, ws
+    return round(el, 1)
+
+
 def box_calibration(dev):
     """Fixed-work probes that separate box-to-box variance from code regressions: the
     library's own f32 MFMA GEMM at 4096^3 (TFLOP/s), a 1 GiB device-to-device copy (GB/s,
@@ -487,6 +508,9 @@ def main():
     ap.add_argument("--config", default="terabyte", choices=list(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="global batch (default: config's)")
     ap.add_argument("--lr", type=float, default=0.0, help="learning rate (default: config's)")
+    ap.add_argument("--preheat-ms", type=float, default=300.0,
+                    help="setup: ms of a model-independent 4096^3 GEMM loop before the warm-up "
+                         "steps, so the clocks have left their idle state (tools/ramp_probe.py)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -556,6 +580,8 @@ def main():
             print(f"[bench] hipGraph capture failed ({e!r}); eager launches", file=sys.stderr)
             graphs = None
             use_graph = False
+
+    preheat = preheat_device(dev, args.preheat_ms) if args.preheat_ms > 0 else 0.0
 
     def run_step(k):
         if graphs is not None:
@@ -693,6 +719,7 @@ def main():
             "interaction_roofline": interaction_roof,
             "kernel_us_per_step": groups,
             "box_calibration": calib,
+            "setup_preheat_ms": preheat,
             "input_pipeline": pipe_rate,
             "cpu_baseline": cpu,
         }

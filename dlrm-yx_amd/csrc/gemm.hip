@@ -1166,8 +1166,6 @@ constexpr PlanEntry kPlans[] = {
 // wave layouts of pipe_body - 64x32 on 2x1, 32x64 on 1x2, 128x32 on 4x1 - measured slower
 // on every DLRM shape: tools/gemm_cfg_ab.py, profiles/r02_gemm_cfg_ab.txt.)
 bool tile_ok(int bm, int bn, int wm, int wn) {
-  if (wm == 2 && wn == 4) return bm == 128 && bn == 128;  // 512-thread workgroups
-  if (wm == 4 && wn == 2) return bm == 128 && bn == 128;
   return wm == 2 && wn == 2 &&
          ((bm == 64 && bn == 64) || (bm == 128 && bn == 64) || (bm == 64 && bn == 128) ||
           (bm == 32 && bn == 64) || (bm == 64 && bn == 32));
@@ -1249,7 +1247,7 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   }
   const int env = gemm_math_env();
   t.x6 = env >= 0 ? env : (gemms > 0 && votes == gemms);
-  if (t.x6 && (t.bm == 128 || t.bn == 128) && t.wm * t.wn == 4) t = Tile{64, 64, 2, 2, 1};
+  if (t.x6 && (t.bm == 128 || t.bn == 128)) t = Tile{64, 64, 2, 2, 1};
 }
 
 // Split-K workspace: the fixed 64 KiB ticket head, then each problem's records.
@@ -1449,15 +1447,12 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
     for (int i = 0; i < m; ++i)
       if (q[i].mode == DLRM_GEMM_FULL) pl[i] = make_plan(1, q[i].K);
   }
-  if (t.x6) {  // split-bf16 body: 128-wide tiles only on 8-wave workgroups
-    if (t.wm == 2 && t.wn == 4) return launch_group<128, 128, true, 2, 4>(m, q, pl, ws, ws_bytes, st);
-    if (t.wm == 4 && t.wn == 2) return launch_group<128, 128, true, 4, 2>(m, q, pl, ws, ws_bytes, st);
+  if (t.x6) {  // split-bf16 body: 128-wide tiles stage too much per K-tile (and 128x128 on
+              // 8-wave workgroups leaves half the CUs idle at M = 2048: r03_gemm_tiles_ab.txt)
     if (t.bm == 32) return launch_group<32, 64, true>(m, q, pl, ws, ws_bytes, st);
     if (t.bn == 32) return launch_group<64, 32, true>(m, q, pl, ws, ws_bytes, st);
     return launch_group<64, 64, true>(m, q, pl, ws, ws_bytes, st);
   }
-  if (t.wm == 2 && t.wn == 4) return launch_group<128, 128, false, 2, 4>(m, q, pl, ws, ws_bytes, st);
-  if (t.wm == 4 && t.wn == 2) return launch_group<128, 128, false, 4, 2>(m, q, pl, ws, ws_bytes, st);
   if (t.bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, st);
   if (t.bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, st);
   if (t.bm == 32) return launch_group<32, 64>(m, q, pl, ws, ws_bytes, st);
