@@ -623,6 +623,224 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   finish_tile<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0, smem);
 }
 
+// ------------------------------------------------------------- LDS-DMA f32 body --
+// The second fp32 body (r03), picked per shape by the plan: operand panels go global -> LDS by LDS-DMA
+// (buffer_load_dwordx4 ... lds, 1 KiB per wave instruction) through a kStages-deep ring,
+// so kStages - 1 K-tiles are in flight with no staging registers and no ds_write; the
+// fragments of K-tile t+1 are read under the second half of tile t's MFMAs (one barrier
+// per K-tile).  A/B against the register-staged pipe_body (DLRM_GEMM_BODY=reg):
+// profiles/r03_gemm_dma_probe.txt (C3 shapes 5-20 % faster).
+// LDS images (1 KiB blocks, bank maps checked offline: every ds_read group touches 64
+// distinct banks):
+//   KC  : 8 rows x 32 k per block; row r's 16-B chunk c in slot 8 (r % 8) + (c ^ s(r)),
+//         s(r) = (r ^ (r >> 3)) & 7  (fragment reads: ds_read_b128);
+//   !KC : 256/MN k-rows x MN per block; chunk c of row k in slot (k % rpb)(MN/4) + (c ^ g(k)),
+//         g(k) = 4 ((k >> 3) & 1) mod MN/4  (fragment reads: ds_read_b32).
+constexpr int kStages = 4;
+typedef __attribute__((address_space(3))) const float lds_cfloat;
+
+template <int MN, bool KC>
+struct DImg {
+  static constexpr int FLOATS = MN * kBK;           // one stage
+  static constexpr int BLOCKS = FLOATS * 4 / 1024;  // KiB blocks (one DMA instruction each)
+  static constexpr int CPR = MN / 4;                // !KC: 16-B chunks per k-row
+  static constexpr int RPB = KC ? 8 : 256 / MN;     // rows per block
+  __device__ __forceinline__ static int swz(int r) { return (r ^ (r >> 3)) & 7; }
+  __device__ __forceinline__ static int g(int k) { return (4 * ((k >> 3) & 1)) % CPR; }
+  // (mn, k) of the 16-B chunk lane l of block b loads
+  __device__ __forceinline__ static void lane_src(int b, int l, int& mn, int& k) {
+    if constexpr (KC) {
+      mn = b * 8 + (l >> 3);
+      k = 4 * ((l & 7) ^ swz(mn));
+    } else {
+      k = b * RPB + l / CPR;
+      mn = 4 * ((l % CPR) ^ g(k));
+    }
+  }
+  __device__ __forceinline__ static int at(int mn, int k) {  // float offset in the stage
+    if constexpr (KC)
+      return (mn >> 3) * 256 + ((mn & 7) * 8 + ((k >> 2) ^ swz(mn))) * 4 + (k & 3);
+    else
+      return (k / RPB) * 256 + ((k % RPB) * CPR + ((mn >> 2) ^ g(k))) * 4 + (mn & 3);
+  }
+};
+
+// One LDS-DMA wave instruction (64 lanes x 16 B -> LDS [lds, +1 KiB)) in inline asm: the
+// compiler's waitcnt pass does not see it as an LDS store, so it does not drain every
+// in-flight DMA (vmcnt(0)) before the next ds_read of ANOTHER ring stage; wait_vm<N>
+// orders instead.  (M0 is reserved by the compiler, which keeps no value in it here.)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const float* lds, int voff) {
+  const unsigned a = (unsigned)(uintptr_t)(lds_cfloat*)lds;
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(a),
+               "v"(voff), "s"(r)
+               : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN>
+constexpr int dma_smem_floats() {
+  return kStages * (BM + BN) * kBK;
+}
+
+template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS>
+__device__ __forceinline__ void pipe_body_dma(const GemmParams& p, int lb, float* smem) {
+  constexpr int S = kStages;
+  constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+  constexpr int NW = WGM * WGN;
+  constexpr int KL = kBK / 4;
+  using IA = DImg<BM, A_KC>;
+  using IB = DImg<BN, B_KC>;
+  constexpr int STAGE = IA::FLOATS + IB::FLOATS;
+  static_assert(IA::BLOCKS % NW == 0 && IB::BLOCKS % NW == 0, "DMA blocks per wave");
+  constexpr int NIA = IA::BLOCKS / NW, NIB = IB::BLOCKS / NW;  // DMA instrs per wave / tile
+  constexpr int NI = NIA + NIB;
+
+  const int tile = lb / p.splits;
+  const int split = lb - tile * p.splits;
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM;
+  const int64_t n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * p.kchunk;
+  const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int wm0 = (wave / WGN) * WM, wn0 = (wave % WGN) * WN;
+  const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
+
+  const int64_t a_ext = A_KC ? (p.M - 1) * p.lda + p.K : (p.K - 1) * p.lda + p.M;
+  const int64_t b_ext = B_KC ? (p.N - 1) * p.ldb + p.K : (p.K - 1) * p.ldb + p.N;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)(a_ext * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)(b_ext * 4), 0x00020000);
+  // per DMA instruction of this wave: byte offset at the split's first K-tile (-1: the
+  // row / column is outside the operand), the chunk's k within a tile
+  int aoff[NIA], akp[NIA], boff[NIB], bkp[NIB];
+#pragma unroll
+  for (int i = 0; i < NIA; ++i) {
+    int mn, k;
+    IA::lane_src(wave * NIA + i, lane, mn, k);
+    const int64_t gmn = m0 + mn, gk = kbeg + k;
+    aoff[i] = gmn < p.M ? (int)(4 * (A_KC ? gmn * p.lda + gk : gk * p.lda + gmn)) : -1;
+    akp[i] = k;
+  }
+#pragma unroll
+  for (int i = 0; i < NIB; ++i) {
+    int mn, k;
+    IB::lane_src(wave * NIB + i, lane, mn, k);
+    const int64_t gmn = n0 + mn, gk = kbeg + k;
+    boff[i] = gmn < p.N ? (int)(4 * (B_KC ? gmn * p.ldb + gk : gk * p.ldb + gmn)) : -1;
+    bkp[i] = k;
+  }
+  const int a_step = A_KC ? 4 * kBK : (int)(4 * kBK * p.lda);
+  const int b_step = B_KC ? 4 * kBK : (int)(4 * kBK * p.ldb);
+  const int krem = (int)(kend - kbeg);  // k range of this split
+  // DMA of K-tile t into stage t % S; tiles past the split (t >= nk) and chunks past K load
+  // zeros (out-of-descriptor offset), so every wave issues the same instruction count
+  auto issue = [&](int t) {
+    float* st = smem + (t % S) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NIA; ++i) {
+      const bool ok = aoff[i] >= 0 && t * kBK + akp[i] < krem;
+      dma16(ra, st + (wave * NIA + i) * 256, ok ? aoff[i] + t * a_step : 0x7ffffff0);
+    }
+#pragma unroll
+    for (int i = 0; i < NIB; ++i) {
+      const bool ok = boff[i] >= 0 && t * kBK + bkp[i] < krem;
+      dma16(rb, st + IA::FLOATS + (wave * NIB + i) * 256, ok ? boff[i] + t * b_step : 0x7ffffff0);
+    }
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rs[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) rs[i] = 0.f;
+  auto read = [&](int t, float (&a)[FM][KL], float (&b)[FN][KL]) {
+    const float* st = smem + (t % S) * STAGE;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int mn = wm0 + i * 16 + l16;
+#pragma unroll
+      for (int s = 0; s < KL; s += (A_KC ? 4 : 1)) {
+        if constexpr (A_KC) {
+          const float4 v = *reinterpret_cast<const float4*>(st + IA::at(mn, kq * KL + s));
+          a[i][s] = v.x, a[i][s + 1] = v.y, a[i][s + 2] = v.z, a[i][s + 3] = v.w;
+        } else {
+          a[i][s] = st[IA::at(mn, kq * KL + s)];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int mn = wn0 + j * 16 + l16;
+#pragma unroll
+      for (int s = 0; s < KL; s += (B_KC ? 4 : 1)) {
+        if constexpr (B_KC) {
+          const float4 v =
+              *reinterpret_cast<const float4*>(st + IA::FLOATS + IB::at(mn, kq * KL + s));
+          b[j][s] = v.x, b[j][s + 1] = v.y, b[j][s + 2] = v.z, b[j][s + 3] = v.w;
+        } else {
+          b[j][s] = st[IA::FLOATS + IB::at(mn, kq * KL + s)];
+        }
+      }
+    }
+  };
+  auto mfma = [&](const float (&a)[FM][KL], const float (&b)[FN][KL], int s0, int s1) {
+#pragma unroll
+    for (int s = s0; s < s1; ++s) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+      if constexpr (RS) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], a[i][s]);
+      }
+    }
+  };
+  float ca[FM][KL], cb[FN][KL], na[FM][KL], nb[FN][KL];
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t) issue(t);
+  wait_vm<(S - 2) * NI>();       // tile 0 landed (this wave)
+  __builtin_amdgcn_s_barrier();  // (every wave; a bare barrier: __syncthreads' fence would
+  asm volatile("" ::: "memory");  //  drain every DMA in flight)
+  read(0, ca, cb);
+  auto step = [&](int t, float (&a)[FM][KL], float (&b)[FN][KL], float (&a2)[FM][KL],
+                  float (&b2)[FN][KL]) {
+    mfma(a, b, 0, KL / 2);
+    wait_vm<(S - 3) * NI>();       // tile t+1 landed (this wave)
+    __builtin_amdgcn_s_barrier();  // every wave's has; every wave has read tile t-1's stage
+    asm volatile("" ::: "memory");
+    issue(t + S - 1);  // into tile t-1's stage
+    read(t + 1, a2, b2);
+    mfma(a, b, KL / 2, KL);
+  };
+  for (int t = 0; t < nk; t += 2) {
+    step(t, ca, cb, na, nb);
+    if (t + 1 >= nk) break;
+    step(t + 1, na, nb, ca, cb);
+  }
+  wait_vm<0>();  // the trailing DMAs (tiles >= nk) land before smem is reused or released
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    rs[i] += __shfl_xor(rs[i], 16, 64);
+    rs[i] += __shfl_xor(rs[i], 32, 64);
+  }
+  finish_tile<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0, smem);
+}
+
 // ---------------------------------------------------------------- split-bf16 body --
 // fp32 GEMM on the bf16 matrix core (v_mfma_f32_16x16x32_bf16, 16x the f32 MFMA rate).
 // Every fp32 operand x is split exactly into three bf16 terms, x = h + m + l (round to
@@ -970,6 +1188,36 @@ __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
     if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
 }
 
+// The same grouped launch on the LDS-DMA body (pipe_body_dma).
+template <int BM, int BN, int WGM, int WGN, int KINDS>
+__global__ __launch_bounds__(WGM * WGN * 64, (BM * BN > 4096 ? 1 : 2)) void gemm_group_dma_kernel(
+    const GemmGroup g) {
+  constexpr int SM = dma_smem_floats<BM, BN>() > group_smem_floats<BM, BN>()
+                         ? dma_smem_floats<BM, BN>()
+                         : group_smem_floats<BM, BN>();
+  __shared__ __attribute__((aligned(1024))) float smem[SM];
+  const int b = blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxGroup; ++i)
+    if (i < g.n && b >= g.p[i].block0) q = i;
+  const GemmParams& p = g.p[q];
+  const int nq = (q + 1 < g.n ? g.p[q + 1].block0 : g.total) - p.block0;
+  const int lb = xcd_remap(b - p.block0, nq);
+  if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
+  const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
+  if constexpr ((KINDS & 1) != 0)
+    if (kind == 0) return pipe_body_dma<BM, BN, WGM, WGN, true, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 2) != 0)
+    if (kind == 1) return pipe_body_dma<BM, BN, WGM, WGN, true, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 4) != 0)
+    if (kind == 2) return pipe_body_dma<BM, BN, WGM, WGN, false, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 8) != 0)
+    if (kind == 3) return pipe_body_dma<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 16) != 0)
+    if (kind == 4) return pipe_body_dma<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
+}
+
 // The same grouped launch on the split-bf16 body (pipe_body6).
 template <int BM, int BN, int WGM, int WGN, int KINDS>
 __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group6_kernel(const GemmGroup g) {
@@ -1152,7 +1400,8 @@ struct PlanEntry {
   int64_t M, N, K;
   int layout, bm, bn, split;
   int wm = 2, wn = 2;
-  int x6 = 0;  // 1: the split-bf16 body measured faster (tools/gemm_x6_ab.py)
+  int x6 = 0;   // 1: the split-bf16 body measured faster (tools/gemm_x6_ab.py)
+  int dma = 0;  // 1: the LDS-DMA f32 body (tools/gemm_body_ab.py)
 };
 
 // Measured plans for the DLRM step shapes of single-problem launches (exact match), from
@@ -1173,7 +1422,8 @@ bool tile_ok(int bm, int bn, int wm, int wn) {
 
 struct Tile {
   int bm = 64, bn = 32, wm = 2, wn = 2;
-  int x6 = 0;  // math vote of a problem / the launch's math
+  int x6 = 0;   // math vote of a problem / the launch's math
+  int dma = 0;  // f32 body vote of a problem / the launch's body (1: LDS-DMA)
   bool operator==(const Tile& o) const {
     return bm == o.bm && bn == o.bn && wm == o.wm && wn == o.wn;
   }
@@ -1183,6 +1433,15 @@ struct Tile {
 // bitwise the same in any group: the split decides the summation order, the tile shape
 // does not).  Tuning overrides (read per call, for sweeps): DLRM_GEMM_CFG=<BM>x<BN> or
 // <BM>x<BN>x<WGM>x<WGN>, DLRM_GEMM_SPLIT=<n>.
+// A/B override for the large shapes (>= 2^20 outputs): DLRM_GEMM_BIG=dma64 puts them on
+// 64x64 tiles and the LDS-DMA body; dma64h also halves a split K (read per call).
+void big_override(const Desc& d, Tile& t, Plan& pl) {
+  const char* v = getenv("DLRM_GEMM_BIG");
+  if (!v || strncmp(v, "dma64", 5) != 0 || d.M * d.N < (1 << 20)) return;
+  t = Tile{64, 64, 2, 2, 0, 1};
+  if (v[5] == 'h' && pl.splits > 1) pl = make_plan(pl.splits / 2, d.K);
+}
+
 void plan_one(const Desc& d, Tile& t, Plan& pl) {
   t = Tile{64, 64, 2, 2};
   if (d.mode == DLRM_GEMM_REDUCE) {  // elementwise job: no tiles, no K
@@ -1210,8 +1469,9 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
   if (!getenv("DLRM_GEMM_NOTABLE"))
     for (const PlanEntry& e : kPlans)
       if (e.M == d.M && e.N == d.N && e.K == d.K && e.layout == layout_of(d)) {
-        t = Tile{e.bm, e.bn, e.wm, e.wn, e.x6};
+        t = Tile{e.bm, e.bn, e.wm, e.wn, e.x6, e.dma};
         pl = make_plan(e.split, d.K);
+        big_override(d, t, pl);
         return;
       }
   // Heuristic (shapes not in the table): 64x32 tiles (the sweep's best almost everywhere);
@@ -1224,6 +1484,7 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
   int64_t s = 1;
   while (tiles * s < target && dlrm::ceil_div(d.K, s + 1) >= 256 && s < kMaxSplit) ++s;
   pl = make_plan(s, d.K);
+  big_override(d, t, pl);
 }
 
 // Tile config of a launch: the GEMM problems' common choice, else 64x32 (REDUCE jobs have
@@ -1231,13 +1492,14 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
 void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   bool first = true;
   t = Tile{64, 64, 2, 2};
-  int votes = 0, gemms = 0;
+  int votes = 0, gemms = 0, dvotes = 0;
   for (int i = 0; i < n; ++i) {
     Tile a;
     plan_one(d[i], a, pl[i]);
     if (d[i].mode == DLRM_GEMM_REDUCE) continue;
     ++gemms;
     votes += a.x6;
+    dvotes += a.dma;
     if (first) {
       t = a;
       first = false;
@@ -1247,6 +1509,7 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   }
   const int env = gemm_math_env();
   t.x6 = env >= 0 ? env : (gemms > 0 && votes == gemms);
+  t.dma = gemms > 0 && dvotes == gemms;  // every GEMM of the launch asks for the DMA body
   if (t.x6 && (t.bm == 128 || t.bn == 128)) t = Tile{64, 64, 2, 2, 1};
 }
 
@@ -1265,7 +1528,20 @@ size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
   return any ? c.used + 256 : 0;
 }
 
-template <int BM, int BN, bool X6 = false, int WGM = 2, int WGN = 2>
+// Body of a launch: kBodyReg (register-staged f32 pipe_body), kBodyX6 (split-bf16),
+// kBodyDma (LDS-DMA f32 pipe_body_dma, where the plan asks for it).
+constexpr int kBodyReg = 0, kBodyX6 = 1, kBodyDma = 2;
+
+// f32 body of a launch: the plan's vote, or DLRM_GEMM_BODY=reg / dma everywhere (A/B; read
+// per call).
+int f32_body(int plan_dma) {
+  const char* v = getenv("DLRM_GEMM_BODY");
+  if (v && strcmp(v, "reg") == 0) return kBodyReg;
+  if (v && strcmp(v, "dma") == 0) return kBodyDma;
+  return plan_dma ? kBodyDma : kBodyReg;
+}
+
+template <int BM, int BN, int BODY = kBodyDma, int WGM = 2, int WGN = 2>
 int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes, hipStream_t st) {
   constexpr int NT = WGM * WGN * 64;
   GemmGroup g{};
@@ -1313,7 +1589,7 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
   // row sums, two wgrads), else all kinds
-  if constexpr (X6) {
+  if constexpr (BODY == kBodyX6) {
     switch (kinds) {
 #define K_(M_)                                                                           \
   case M_:                                                                              \
@@ -1323,6 +1599,17 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
 #undef K_
       default:
         hipLaunchKernelGGL((gemm_group6_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
+    }
+  } else if constexpr (BODY == kBodyDma) {
+    switch (kinds) {
+#define K_(M_)                                                                              \
+  case M_:                                                                                 \
+    hipLaunchKernelGGL((gemm_group_dma_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g); \
+    break;
+      K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
+#undef K_
+      default:
+        hipLaunchKernelGGL((gemm_group_dma_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
     }
   } else {
     switch (kinds) {
@@ -1449,9 +1736,16 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
   }
   if (t.x6) {  // split-bf16 body: 128-wide tiles stage too much per K-tile (and 128x128 on
               // 8-wave workgroups leaves half the CUs idle at M = 2048: r03_gemm_tiles_ab.txt)
-    if (t.bm == 32) return launch_group<32, 64, true>(m, q, pl, ws, ws_bytes, st);
-    if (t.bn == 32) return launch_group<64, 32, true>(m, q, pl, ws, ws_bytes, st);
-    return launch_group<64, 64, true>(m, q, pl, ws, ws_bytes, st);
+    if (t.bm == 32) return launch_group<32, 64, kBodyX6>(m, q, pl, ws, ws_bytes, st);
+    if (t.bn == 32) return launch_group<64, 32, kBodyX6>(m, q, pl, ws, ws_bytes, st);
+    return launch_group<64, 64, kBodyX6>(m, q, pl, ws, ws_bytes, st);
+  }
+  if (f32_body(t.dma) == kBodyReg) {
+    if (t.bm == 128) return launch_group<128, 64, kBodyReg>(m, q, pl, ws, ws_bytes, st);
+    if (t.bn == 128) return launch_group<64, 128, kBodyReg>(m, q, pl, ws, ws_bytes, st);
+    if (t.bm == 32) return launch_group<32, 64, kBodyReg>(m, q, pl, ws, ws_bytes, st);
+    if (t.bn == 32) return launch_group<64, 32, kBodyReg>(m, q, pl, ws, ws_bytes, st);
+    return launch_group<64, 64, kBodyReg>(m, q, pl, ws, ws_bytes, st);
   }
   if (t.bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, st);
   if (t.bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, st);

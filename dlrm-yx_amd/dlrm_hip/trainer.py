@@ -215,6 +215,9 @@ class DLRMTrainer:
         # MLP backward: a layer's split wgrad (partials only) in the same launch as its dgrad
         self.group_wgrad = os.environ.get("DLRM_GROUP_WGRAD", "1") != "0"
         self.full_last_wgrad = os.environ.get("DLRM_FULL_LAST_WGRAD", "0") == "1"
+        # bottom-MLP backward schedule: "partial" (split wgrads reduced in the next launch)
+        # or "full" (in-launch split-K, n_bot launches; bottom_bwd_full)
+        self.bot_sched = os.environ.get("DLRM_BOT_SCHED", "partial")
         # one GPU: the bottom MLP forward as a role of the lookup launch (mlp_rows.hpp)
         self.fuse_bottom = os.environ.get("DLRM_FUSE_BOTTOM", "1") != "0"
         self.bottom_fused = False  # set by the last step
@@ -454,7 +457,7 @@ class DLRMTrainer:
         # g_l while the main stream's next two data-gradient GEMMs produce g_{l-1}, g_{l-2}
         bufs["g"] = [torch.zeros((Bl, wmax), **f32) for _ in range(3)]
         wbot = max(L.Kp for L in self.bot)
-        bufs["gb"] = [torch.zeros((Bl, wbot), **f32) for _ in range(2)]
+        bufs["gb"] = [torch.zeros((Bl, wbot), **f32) for _ in range(3)]
         bufs["dx"] = torch.zeros((Bl, D), **f32)
         bufs["gx"] = torch.zeros((Bl, D), **f32)
         bufs["E"] = torch.zeros((B, max(self.T_local, 1), D), **f32)
@@ -634,7 +637,29 @@ class DLRMTrainer:
                                       grad_ly=gfeats, relu_x=True)
             st["rq"] = rq
 
+        def bottom_bwd_full():
+            """Bottom-MLP backward with in-launch split-K wgrads (FULL, SGD fused): the
+            wgrad of layer l rides in the launch of dgrad(l-1), which does not read W_l,
+            and the last launch holds the two lowest wgrads - n_bot launches, no trailing
+            REDUCE.  dgrad(l) writes g_{l-1} into buffer l % 3: the wgrad it shares a launch
+            with reads g_{l+1} from buffer (l+2) % 3."""
+            rq = st.pop("rq")
+            g = bufs["gx"]
+            pending = []
+            for li in range(self.n_bot - 1, -1, -1):
+                L = self.bot[li]
+                inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
+                w = self._wgrad(L, g, inp, fused_opt, lr)
+                if li > 0:
+                    out = bufs["gb"][li % 3]
+                    self._gemm([self._dgrad(L, g, inp, out)] + pending + rq)
+                    rq, pending, g = [], [w], out
+                else:
+                    self._gemm(pending + [w] + rq)
+
         def bottom_bwd(s1=None):
+            if self.bot_sched == "full" and not c_bot and fused_opt:
+                return bottom_bwd_full()
             rq = st.pop("rq")
             g = bufs["gx"]  # dLoss/d(pre-ReLU bottom output), from the interaction backward
             bg = [bufs["gb"][0], bufs["gb"][1]]

@@ -91,7 +91,9 @@ enum dlrm_tbe_error {
 enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
 
 /* ---------------------------------------------------------------- library -- */
-/* 2: the TBE backward entry points take an error_flag (round 2). */
+/* 2: the TBE backward entry points take an error_flag (round 2).
+ * 3: dlrm_qr_expand_csr takes phys_capacity + error_flag; a PARTIAL split count must be
+ *    normalized (dlrm_gemm_f32_splits) (round 3). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 

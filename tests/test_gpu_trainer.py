@@ -418,3 +418,29 @@ def test_c3_true_terabyte_rows_vs_touched_row_oracle():
     for m, (W, b_) in zip(lin, tr.dense_state()):
         ok, msg = fp32_close(W.cpu().numpy(), m.weight.detach().numpy())
         assert ok, msg
+
+
+@pytest.mark.parametrize("name", ["c3_small", "c2_small"])
+def test_bottom_backward_full_schedule_vs_oracle(name):
+    """bot_sched="full": the bottom-MLP wgrads split K inside their own launch (SGD fused)
+    and ride in the next dgrad's launch (n_bot launches, no trailing REDUCE); C3 (3 bottom
+    layers) and C2 (4: the third g buffer) widths, 2 steps vs the oracle."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    ln_top = [_num_int(len(rows), D)] + c["top"]
+    np.random.seed(7)
+    ref = O.OracleDLRM(D, rows, c["bot"], ln_top, loss_function=c["loss"])
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"], ln_top=ln_top,
+                        loss_function=c["loss"], learning_rate=c["lr"])
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    tr.bot_sched = "full"
+    rng = np.random.RandomState(3)
+    for s in range(2):
+        X, lS_o, lS_i, T = _rand_batch(rng, rows, c["B"], c["L"], c["bot"][0], c["loss"])
+        Zr, Er = ref.train_step(torch.tensor(X), torch.tensor(lS_o),
+                                [torch.tensor(i) for i in lS_i], torch.tensor(T), c["lr"])
+        Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
+        assert ok, (s, msg)
+    _compare_state(tr, ref)
