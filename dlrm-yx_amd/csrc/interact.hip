@@ -33,6 +33,15 @@ struct GradArgs {
   float* ptr[kMaxF];
   int64_t bs[kMaxF];
 };
+// The one-hot lookup fused into the interaction (dlrm_interact_dot_forward_gather): feature
+// f >= 1 of sample b is row row_base[f-1] + idx[(f-1) * B + b] of W (L = 1, table-major
+// CSR indices: the lookup of apply_emb with one index per bag); feature 0 stays fa.ptr[0].
+struct GatherArgs {
+  const float* W;
+  const int64_t* row_base;  // [F] device: table starts, row_base[F-1] = total rows
+  const int32_t* idx;       // [(F-1) * B]
+  int32_t* err;             // DLRM_TBE_ERR_INDEX on an index outside its table (may be null)
+};
 
 // p-th pair of the row-major lower triangle (i > j, or i >= j with self interaction).
 __device__ __forceinline__ void pair_of(int p, bool self, int& i, int& j) {
@@ -341,6 +350,19 @@ __device__ __forceinline__ const float* row_ptr(const FeatArgs& fa, int F, int64
   return p + b * bs;
 }
 
+// Gather mode: lane f (1 <= f < F) looks up its feature's row for sample b (one index
+// load per lane per sample; the table bounds were loaded once).  -1: index out of range
+// (the row reads as zeros, like the TBE, which drops it from the bag, and is flagged).
+__device__ __forceinline__ int64_t gather_row(const GatherArgs& gt, int F, int B, int64_t b,
+                                              int lane, int64_t rb_lo, int64_t nrows,
+                                              bool active) {
+  if (lane < 1 || lane >= F) return 0;
+  const int64_t r = gt.idx[(int64_t)(lane - 1) * B + b];
+  if (r >= 0 && r < nrows) return rb_lo + r;
+  if (active && gt.err) atomicOr(gt.err, DLRM_TBE_ERR_INDEX);
+  return -1;
+}
+
 template <int D>
 __device__ __forceinline__ float* grad_row_ptr(const GradArgs& ga, int F, int64_t b, int i0,
                                                int sub) {
@@ -360,11 +382,11 @@ __device__ __forceinline__ float* grad_row_ptr(const GradArgs& ga, int F, int64_
 // Forward: T (F x D) -> LDS with coalesced float4 loads; lane (f, h) then feeds T[f][k] for
 // its k-half as both MFMA operands (Z = T T^T, two accumulator chains); the strict lower
 // triangle and x are staged in LDS in output order and written as whole float4 rows.
-template <int D>
+template <int D, bool GATHER>
 __global__ __launch_bounds__(256) void interact_dot_fwd_v4(int B, int F, FeatArgs fa, int self,
                                                            float* __restrict__ out,
                                                            int64_t ld_out, int width,
-                                                           int vec_out) {
+                                                           int vec_out, GatherArgs gt) {
   constexpr int DP = D + 4, C4 = D / 4, RPI = 64 / C4, KH = D / 2;
   constexpr int OUTP = D + 32 * 33 / 2 + 4;  // x + <= 528 pairs, rounded
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -375,6 +397,11 @@ __global__ __launch_bounds__(256) void interact_dot_fwd_v4(int B, int F, FeatArg
   const int sub = lane / C4, c = lane - sub * C4;
   const bool rowok = l32 < F;
   constexpr int NI = 32 / RPI;  // row-load instructions covering F <= 32 rows
+  int64_t rb_lo = 0, nrows = 0;  // gather: lane f's table bounds (once per kernel)
+  if (GATHER && lane >= 1 && lane < F) {
+    rb_lo = gt.row_base[lane - 1];
+    nrows = gt.row_base[lane] - rb_lo;
+  }
   for (int64_t b0 = (int64_t)blockIdx.x * 4; b0 < B; b0 += (int64_t)gridDim.x * 4) {
     const int64_t b = b0 + wave;
     const bool active = b < B;
@@ -383,11 +410,20 @@ __global__ __launch_bounds__(256) void interact_dot_fwd_v4(int B, int F, FeatArg
       // latency per sample, not one per row group); rows >= F / inactive waves read a
       // valid row (feature 0 of sample 0) and store nothing
       const int64_t bl = active ? b : 0;
+      const int64_t grow = GATHER ? gather_row(gt, F, B, bl, lane, rb_lo, nrows, active) : 0;
       float4 v[NI];
 #pragma unroll
       for (int q = 0; q < NI; ++q) {
-        const float* src = row_ptr<D>(fa, F, bl, q * RPI, sub);
-        v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
+        if constexpr (GATHER) {
+          const int f = q * RPI + sub;
+          const int64_t g = __shfl(grow, f < 64 ? f : 0, 64);
+          const float* src = (f >= 1 && g >= 0) ? gt.W + g * D : fa.ptr[0] + bl * fa.bs[0];
+          v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
+          if (f >= 1 && g < 0) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          const float* src = row_ptr<D>(fa, F, bl, q * RPI, sub);
+          v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
+        }
       }
       // unconditional stores (rows >= F are masked by rowok below; inactive waves' rows are
       // never read), so no load sinks into a branch and waits alone
@@ -439,11 +475,11 @@ __global__ __launch_bounds__(256) void interact_dot_fwd_v4(int B, int F, FeatArg
 // T columns it consumed, then every feature's gradient row leaves as whole float4 rows.
 // Feature 0 (the bottom-MLP output x) gets dR[0:D] added and, with relu_x, the ReLU' mask
 // of x applied (the backward of the bottom MLP's last ReLU, fused).
-template <int D>
+template <int D, bool GATHER>
 __global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArgs fa, int self,
                                                            const float* __restrict__ gout,
                                                            int64_t ld_g, GradArgs ga,
-                                                           int relu_x, int vec_g) {
+                                                           int relu_x, int vec_g, GatherArgs gt) {
   constexpr int DP = D + 4, C4 = D / 4, RPI = 64 / C4;
   constexpr int GP = D + 32 * 33 / 2 + 4;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -456,25 +492,40 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArg
   const int width = D + npairs;
   constexpr int NI = 32 / RPI;          // row-load instructions covering 32 rows
   constexpr int NG = (GP / 4 + 63) / 64;  // float4 of the dR row per lane (vec_g)
+  int64_t rb_lo = 0, nrows = 0;  // gather: lane f's table bounds (once per kernel)
+  if (GATHER && lane >= 1 && lane < F) {
+    rb_lo = gt.row_base[lane - 1];
+    nrows = gt.row_base[lane] - rb_lo;
+  }
   for (int64_t b0 = (int64_t)blockIdx.x * 4; b0 < B; b0 += (int64_t)gridDim.x * 4) {
     const int64_t b = b0 + wave;
     const bool active = b < B;
     {
       // all loads of the sample in flight at once (rows >= F are zero: they meet S's zeros)
       const int64_t bl = active ? b : 0;
+      // (gather: the forward flagged bad indices; the backward reads them as zeros again)
+      const int64_t grow = GATHER ? gather_row(gt, F, B, bl, lane, rb_lo, nrows, false) : 0;
       float4 v[NI];
 #pragma unroll
       for (int q = 0; q < NI; ++q) {
-        const float* src = row_ptr<D>(fa, F, bl, q * RPI, sub);
-        v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
+        if constexpr (GATHER) {
+          const int f = q * RPI + sub;
+          const int64_t g = __shfl(grow, f < 64 ? f : 0, 64);
+          const float* src = (f >= 1 && g >= 0) ? gt.W + g * D : fa.ptr[0] + bl * fa.bs[0];
+          v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
+          if (f >= 1 && g < 0) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          const float* src = row_ptr<D>(fa, F, bl, q * RPI, sub);
+          v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
+        }
       }
-      const float* grow = gout + bl * ld_g;
+      const float* gsrc = gout + bl * ld_g;
       const int w4 = vec_g ? width / 4 : 0;
       float4 gv[NG];
 #pragma unroll
       for (int u = 0; u < NG; ++u) {
         const int q = lane + 64 * u;
-        gv[u] = q < w4 ? *reinterpret_cast<const float4*>(grow + 4 * q)
+        gv[u] = q < w4 ? *reinterpret_cast<const float4*>(gsrc + 4 * q)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       // unconditional stores into this wave's own LDS region (no load sinks into a branch)
@@ -490,7 +541,7 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArg
         if (4 * (lane + 64 * u) < GP) *reinterpret_cast<float4*>(Gl + 4 * q) = gv[u];
       }
       if (active)
-        for (int q = 4 * w4 + lane; q < width; q += 64) Gl[q] = grow[q];
+        for (int q = 4 * w4 + lane; q < width; q += 64) Gl[q] = gsrc[q];
     }
     __syncthreads();
     if (active) {
@@ -692,8 +743,8 @@ extern "C" int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D,
     const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
     const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
 #define L4(DD)                                                                                \
-  hipLaunchKernelGGL(interact_dot_fwd_v4<DD>, dim3(grid), dim3(256), lds, st, B, F, fa,        \
-                     self_interaction ? 1 : 0, out, ld_out, width, vec_out)
+  hipLaunchKernelGGL((interact_dot_fwd_v4<DD, false>), dim3(grid), dim3(256), lds, st, B, F, fa, \
+                     self_interaction ? 1 : 0, out, ld_out, width, vec_out, GatherArgs{})
     if (D == 16) L4(16); else if (D == 32) L4(32); else if (D == 64) L4(64); else L4(128);
 #undef L4
     DLRM_LAUNCH_CHECK(name);
@@ -755,8 +806,9 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
     const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
     const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
 #define L3B(DD)                                                                               \
-  hipLaunchKernelGGL(interact_dot_bwd_v3<DD>, dim3(grid), dim3(256), lds, st, B, F, fa,        \
-                     self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g)
+  hipLaunchKernelGGL((interact_dot_bwd_v3<DD, false>), dim3(grid), dim3(256), lds, st, B, F, fa, \
+                     self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g,      \
+                     GatherArgs{})
     if (D == 16) L3B(16); else if (D == 32) L3B(32); else if (D == 64) L3B(64); else L3B(128);
 #undef L3B
     DLRM_LAUNCH_CHECK(name);
@@ -824,6 +876,84 @@ extern "C" int dlrm_interact_cat_backward(int32_t B, int32_t F, int32_t D,
   const int64_t n = (int64_t)B * F * D;
   hipLaunchKernelGGL(interact_cat_bwd, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0,
                      dlrm::as_stream(stream), B, F, D, grad_out, ld_gout, ga);
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+// One-hot lookup fused into the interaction (one GPU, L = 1): features 1..F-1 are gathered
+// straight from the table buffer (no [B, T, D] pooled-embedding round trip through HBM).
+// Same math and output as dlrm_interact_dot_forward on the looked-up rows.
+extern "C" int dlrm_interact_dot_forward_gather(int32_t B, int32_t F, int32_t D, const float* x,
+                                                int64_t x_bstride, const float* weights,
+                                                const int64_t* row_base, const int32_t* indices,
+                                                int32_t self_interaction, float* out,
+                                                int64_t ld_out, int32_t* error_flag,
+                                                dlrm_stream_t stream) {
+  const char* name = "dlrm_interact_dot_forward_gather";
+  DLRM_ARG(B >= 0 && F >= 2 && F <= 32, "%s: need F in [2,32]", name);
+  DLRM_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, DLRM_ERR_UNSUPPORTED,
+               "%s: D must be 16, 32, 64 or 128", name);
+  if (B == 0) return DLRM_OK;
+  DLRM_ARG(x && weights && row_base && indices && out, "%s: null pointer", name);
+  DLRM_ARG(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weights)) & 15) == 0 &&
+               x_bstride % 4 == 0,
+           "%s: x / weights must be 16-B aligned, x_bstride %% 4 == 0", name);
+  const int npairs = self_interaction ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  DLRM_ARG(ld_out >= D + npairs, "%s: ld_out < D + pairs", name);
+  FeatArgs fa{};
+  for (int f = 0; f < F; ++f) fa.ptr[f] = x, fa.bs[f] = x_bstride;
+  const GatherArgs gt{weights, row_base, indices, error_flag};
+  const int width = D + npairs;
+  const int vec_out = ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 4 == 0) ? 1 : 0;
+  const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
+  const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
+  hipStream_t st = dlrm::as_stream(stream);
+#define L4G(DD)                                                                              \
+  hipLaunchKernelGGL((interact_dot_fwd_v4<DD, true>), dim3(grid), dim3(256), lds, st, B, F, fa, \
+                     self_interaction ? 1 : 0, out, ld_out, width, vec_out, gt)
+  if (D == 16) L4G(16); else if (D == 32) L4G(32); else if (D == 64) L4G(64); else L4G(128);
+#undef L4G
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
+}
+
+// Its backward: T re-gathered from the same (not yet updated) rows; gradients as
+// dlrm_interact_dot_backward (grad_ptrs[f] / grad_bstrides[f], e.g. the [B, T, D] buffer
+// the TBE backward reads), ReLU' of x optional.
+extern "C" int dlrm_interact_dot_backward_gather(
+    int32_t B, int32_t F, int32_t D, const float* x, int64_t x_bstride, const float* weights,
+    const int64_t* row_base, const int32_t* indices, int32_t self_interaction,
+    const float* grad_out, int64_t ld_gout, float* const* grad_ptrs,
+    const int64_t* grad_bstrides, int32_t relu_x, dlrm_stream_t stream) {
+  const char* name = "dlrm_interact_dot_backward_gather";
+  DLRM_ARG(B >= 0 && F >= 2 && F <= 32, "%s: need F in [2,32]", name);
+  DLRM_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, DLRM_ERR_UNSUPPORTED,
+               "%s: D must be 16, 32, 64 or 128", name);
+  if (B == 0) return DLRM_OK;
+  DLRM_ARG(x && weights && row_base && indices && grad_out, "%s: null pointer", name);
+  DLRM_ARG(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weights)) & 15) == 0 &&
+               x_bstride % 4 == 0,
+           "%s: x / weights must be 16-B aligned, x_bstride %% 4 == 0", name);
+  const int npairs = self_interaction ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  DLRM_ARG(ld_gout >= D + npairs, "%s: ld_gout < D + pairs", name);
+  GradArgs ga{};
+  int rc = fill_grad(ga, F, grad_ptrs, grad_bstrides, name);
+  if (rc) return rc;
+  for (int f = 0; f < F; ++f)
+    DLRM_ARG(((reinterpret_cast<uintptr_t>(ga.ptr[f]) & 15) == 0) && (ga.bs[f] & 3) == 0,
+             "%s: gradient rows must be 16-B aligned", name);
+  FeatArgs fa{};
+  for (int f = 0; f < F; ++f) fa.ptr[f] = x, fa.bs[f] = x_bstride;
+  const GatherArgs gt{weights, row_base, indices, nullptr};
+  const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
+  const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
+  const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
+  hipStream_t st = dlrm::as_stream(stream);
+#define L3G(DD)                                                                               \
+  hipLaunchKernelGGL((interact_dot_bwd_v3<DD, true>), dim3(grid), dim3(256), lds, st, B, F, fa,  \
+                     self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g, gt)
+  if (D == 16) L3G(16); else if (D == 32) L3G(32); else if (D == 64) L3G(64); else L3G(128);
+#undef L3G
   DLRM_LAUNCH_CHECK(name);
   return DLRM_OK;
 }

@@ -1404,6 +1404,7 @@ int launch_fwd_presort(const float* W, int64_t D, const int64_t* row_base, int T
   int64_t gblocks = dlrm::ceil_div(dlrm::ceil_div(nbags, gpw), kPreThreads / 64);
   if (gblocks > 8192) gblocks = 8192;
   if (gblocks < 1) gblocks = 1;
+  if (!out) gblocks = 0;  // the lookup is fused into its consumer (interaction gather)
   const dim3 grid((unsigned)(T + 1 + mlp_blocks + gblocks)), block(kPreThreads);
   const IdxT* ip = static_cast<const IdxT*>(idx);
   const OffT* op = static_cast<const OffT*>(off);
@@ -1458,13 +1459,15 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
   }
   if (!presort_applies((uint64_t)total_rows < 0xFFFFFFFFull ? 4 : 8, max_lookups_per_table,
                        num_lookups) || num_lookups == 0 || T * (int64_t)B >= INT32_MAX) {
+    DLRM_REQUIRE(out, DLRM_ERR_UNSUPPORTED,
+                 "%s: out = NULL needs the per-table sort (32-bit keys, bounded tables)", name);
     const int rc = dlrm_tbe_forward(weights, D, row_base, T, B, indices, index_bits, offsets,
                                     offset_bits, per_sample_weights, out, out_batch_stride,
                                     error_flag, stream);
     if (rc != DLRM_OK || !bottom) return rc;
     return dlrm_mlp_chain_forward(bottom, stream);
   }
-  DLRM_ARG(weights && row_base && out && offsets && indices, "%s: null pointer", name);
+  DLRM_ARG(weights && row_base && offsets && indices, "%s: null pointer", name);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: index_bits must be 32|64", name);
   DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: offset_bits must be 32|64", name);

@@ -93,6 +93,10 @@ SIGNATURES = {
                                             P]),
     "dlrm_interact_dot_backward": (c_int32, [c_int32, c_int32, c_int32, P, P, c_int32, P,
                                              c_int64, P, P, c_int32, P]),
+    "dlrm_interact_dot_forward_gather": (c_int32, [c_int32, c_int32, c_int32, P, c_int64, P, P,
+                                                   P, c_int32, P, c_int64, P, P]),
+    "dlrm_interact_dot_backward_gather": (c_int32, [c_int32, c_int32, c_int32, P, c_int64, P, P,
+                                                    P, c_int32, P, c_int64, P, P, c_int32, P]),
     "dlrm_interact_cat_forward": (c_int32, [c_int32, c_int32, c_int32, P, P, P, c_int64, P]),
     "dlrm_interact_cat_backward": (c_int32, [c_int32, c_int32, c_int32, P, c_int64, P, P, P]),
     "dlrm_gemm_f32_workspace_size": (c_size_t, [c_int32, c_int32, c_int64, c_int64, c_int64]),

@@ -177,6 +177,10 @@ def mlp_chain_forward(chain, device=None) -> None:
               _stream(dev))
 
 
+# lookups per table the in-launch per-table sort handles (tbe_bwd.hip kSegCap)
+TBE_PRESORT_SEG_CAP = 4096
+
+
 def tbe_forward_presort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
                         indices: torch.Tensor, offsets: torch.Tensor, workspace: torch.Tensor,
                         max_lookups_per_table: int, out: Optional[torch.Tensor] = None,
@@ -446,6 +450,49 @@ def interact_backward(op: str, x: torch.Tensor, ly, grad_out: torch.Tensor,
                   _stream(x.device))
         if relu_x:
             relu_backward(grad_x, x, out=grad_x)
+    return grad_x, grad_ly
+
+
+def interact_forward_gather(x: torch.Tensor, weights: torch.Tensor, row_base: torch.Tensor,
+                            indices: torch.Tensor, self_interaction: bool = False,
+                            out: Optional[torch.Tensor] = None,
+                            error_flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Dot interaction of x and the one-hot lookups (L = 1) of T = len(row_base) - 1 tables
+    gathered straight from ``weights`` (dlrm_interact_dot_forward_gather): the same R as
+    interact_forward(x, tbe_forward(...)) without the pooled [B, T, D] buffer."""
+    _check_cuda(x, weights, row_base, indices)
+    B, D = x.shape
+    F = row_base.numel()
+    npairs = F * (F + 1) // 2 if self_interaction else F * (F - 1) // 2
+    if indices.dtype != torch.int32 or indices.numel() != (F - 1) * B:
+        raise ValueError("gather interaction: int32 indices [(F-1) * B] (one per bag)")
+    if out is None:
+        out = torch.empty(B, D + npairs, dtype=torch.float32, device=x.device)
+    _lib.call("dlrm_interact_dot_forward_gather", B, F, D, _p(x), x.stride(0), _p(weights),
+              _p(row_base), _p(indices), int(self_interaction), _p(out), out.stride(0),
+              _p(error_flag), _stream(x.device))
+    return out
+
+
+def interact_backward_gather(x: torch.Tensor, weights: torch.Tensor, row_base: torch.Tensor,
+                             indices: torch.Tensor, grad_out: torch.Tensor,
+                             self_interaction: bool = False,
+                             grad_x: Optional[torch.Tensor] = None,
+                             grad_ly: Optional[torch.Tensor] = None, relu_x: bool = False):
+    """Backward of interact_forward_gather (rows re-gathered; call before the embedding
+    update): grad_x [B, D] and grad_ly [B, T, D]."""
+    B, D = x.shape
+    T = row_base.numel() - 1
+    if grad_x is None:
+        grad_x = torch.empty_like(x, memory_format=torch.contiguous_format)
+    if grad_ly is None:
+        grad_ly = torch.empty(B, T, D, dtype=torch.float32, device=x.device)
+    gfeats, gstrides = feature_views(grad_x, grad_ly)
+    gptrs, gbs = _feature_arrays(gfeats, gstrides)
+    g = grad_out if grad_out.stride(1) == 1 else grad_out.contiguous()
+    _lib.call("dlrm_interact_dot_backward_gather", B, T + 1, D, _p(x), x.stride(0), _p(weights),
+              _p(row_base), _p(indices), int(self_interaction), _p(g), g.stride(0), gptrs, gbs,
+              int(relu_x), _stream(x.device))
     return grad_x, grad_ly
 
 

@@ -71,6 +71,7 @@ class Batch:
     indices: torch.Tensor  # int32 table-local rows
     target: torch.Tensor   # [B_local] fp32
     max_per_table: int = 0  # upper bound on one table's lookups (0 = unknown)
+    one_hot: bool = False   # every bag holds exactly one index (offsets = arange)
 
 
 @dataclass
@@ -220,6 +221,10 @@ class DLRMTrainer:
         self.bot_sched = os.environ.get("DLRM_BOT_SCHED", "partial")
         # one GPU: the bottom MLP forward as a role of the lookup launch (mlp_rows.hpp)
         self.fuse_bottom = os.environ.get("DLRM_FUSE_BOTTOM", "1") != "0"
+        # one GPU, one-hot batches: the dot interaction gathers the embedding rows itself
+        # (dlrm_interact_dot_forward_gather); the lookup launch keeps only its sort role
+        self.fuse_gather = os.environ.get("DLRM_FUSE_GATHER", "1") != "0"
+        self.gather_fused = False  # set by the last step
         self.bottom_fused = False  # set by the last step
         # device TBE error bits (ops.TBE_ERR_*): out-of-range indices are skipped by the
         # kernels and flagged here; check_errors() reads it (the step never syncs)
@@ -329,7 +334,11 @@ class DLRMTrainer:
             torch.int32).to(self.dev)  # a rank may own no table
         tg = torch.as_tensor(target).reshape(-1)[sl].to(torch.float32).to(self.dev)
         mx = max([int(i.numel()) for i in idxs], default=0)
-        return Batch(Xp, offsets, indices, tg, mx)
+        one_hot = all(torch.equal(torch.as_tensor(lS_o[t]).to(torch.int64),
+                                  torch.arange(Bl * self.world)) and
+                      int(torch.as_tensor(lS_i[t]).numel()) == Bl * self.world
+                      for t in self.local_tables)
+        return Batch(Xp, offsets, indices, tg, mx, one_hot and bool(self.local_tables))
 
     def batch_from_records(self, records: torch.Tensor, max_ind_range: int = -1) -> Batch:
         """A Batch straight from raw Criteo binary records on the device (int32
@@ -354,7 +363,7 @@ class DLRMTrainer:
             indices = indices.view(self.T, B)[self.local_tables].reshape(-1).contiguous()
             offsets = offsets[:self.T_local * B + 1].contiguous()
         return Batch(dense[sl].contiguous() if Bl != B else dense, offsets, indices,
-                     label.reshape(-1)[sl].contiguous(), B)
+                     label.reshape(-1)[sl].contiguous(), B, True)
 
     def record_batch(self, B: int) -> Batch:
         """Fixed device buffers for global batches of B Criteo records (L = 1), filled by
@@ -374,7 +383,7 @@ class DLRMTrainer:
                 indices=torch.empty(self.T * B, dtype=torch.int32, device=self.dev),
                 offsets=torch.empty(self.T * B + 1, dtype=torch.int32, device=self.dev),
                 tables=torch.tensor(self.local_tables, dtype=torch.int64, device=self.dev))
-        return Batch(X, offsets, indices, target, B)
+        return Batch(X, offsets, indices, target, B, True)
 
     def decode_into(self, records: torch.Tensor, batch: Batch, max_ind_range: int = -1) -> Batch:
         """Decode device records int32 [B * (1 + m_den + T)] into ``batch`` (from
@@ -428,7 +437,7 @@ class DLRMTrainer:
         tg = torch.rand(Bl, generator=g, device=self.dev)
         if self.cfg.loss_function == "bce":
             tg = tg.round()
-        return Batch(Xp, offsets, indices, tg, B * L)
+        return Batch(Xp, offsets, indices, tg, B * L, L == 1)
 
     # ------------------------------------------------------------- buffers --
     def _buffers(self, Bl: int, B: int):
@@ -535,6 +544,8 @@ class DLRMTrainer:
         c_bot = conc and "bot" in self.overlaps and not dist
         st = {}  # state shared by the segments (collective handles, pending reductions)
         presort = self.tbe_presort
+        gather = presort and not dist and self._gather_applies(batch)
+        self.gather_fused = gather
 
         def streams():
             s0 = torch.cuda.current_stream(self.dev)
@@ -549,10 +560,11 @@ class DLRMTrainer:
                     idx, off = st["csr"] = self._phys_csr(batch, B)
                     out = bufs["P"] if self.qr_active else bufs["E"]
                 if self.T_local > 0 and presort:
-                    # the backward's per-table sort runs inside the lookup launch
+                    # the backward's per-table sort runs inside the lookup launch (alone,
+                    # when the interaction gathers the rows itself)
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
-                                            batch.max_per_table, out=out,
+                                            batch.max_per_table, out=None if gather else out,
                                             error_flag=self.tbe_error_flag)
                 elif self.T_local > 0:
                     ops.tbe_forward(self.weights, self.row_base, self.T_phys, B, idx, off,
@@ -573,10 +585,10 @@ class DLRMTrainer:
                 # the bottom MLP forward runs as a role of the lookup launch
                 with prof("tbe_fwd"):
                     idx, off = st["csr"] = self._phys_csr(batch, B)
+                    out = None if gather else bufs["P"] if self.qr_active else bufs["E"]
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
-                                            batch.max_per_table,
-                                            out=bufs["P"] if self.qr_active else bufs["E"],
+                                            batch.max_per_table, out=out,
                                             error_flag=self.tbe_error_flag, bottom=chain)
                     if self.qr_active:
                         self._qr_combine(bufs, B)
@@ -593,8 +605,13 @@ class DLRMTrainer:
         def middle():  # interaction, top MLP, head, top backward, interaction backward
             x, feats = self._features(bufs, Bl)
             with prof("interaction_fwd"):
-                ops.interact_forward(cfg.arch_interaction_op, x, feats,
-                                     cfg.arch_interaction_itself, out=bufs["R"])
+                if gather:  # one-hot lookup fused: rows read straight from the tables
+                    ops.interact_forward_gather(x, self.weights, self.row_base, batch.indices,
+                                                cfg.arch_interaction_itself, out=bufs["R"],
+                                                error_flag=self.tbe_error_flag)
+                else:
+                    ops.interact_forward(cfg.arch_interaction_op, x, feats,
+                                         cfg.arch_interaction_itself, out=bufs["R"])
             h = bufs["R"]
             for L, out in zip(self.top[:-1], bufs["top_act"]):
                 self._gemm([self._fwd(L, h, out)])
@@ -632,9 +649,14 @@ class DLRMTrainer:
                 g, gi = G[gn], gn
             _, gfeats = self._features(bufs, Bl, grad=True)
             with prof("interaction_bwd"):  # + the backward of the bottom MLP's last ReLU
-                ops.interact_backward(cfg.arch_interaction_op, x, feats, g[:, :self.num_int],
-                                      cfg.arch_interaction_itself, grad_x=bufs["gx"],
-                                      grad_ly=gfeats, relu_x=True)
+                if gather:  # rows re-gathered (the embedding update comes later)
+                    ops.interact_backward_gather(x, self.weights, self.row_base, batch.indices,
+                                                 g[:, :self.num_int], cfg.arch_interaction_itself,
+                                                 grad_x=bufs["gx"], grad_ly=gfeats, relu_x=True)
+                else:
+                    ops.interact_backward(cfg.arch_interaction_op, x, feats, g[:, :self.num_int],
+                                          cfg.arch_interaction_itself, grad_x=bufs["gx"],
+                                          grad_ly=gfeats, relu_x=True)
             st["rq"] = rq
 
         def bottom_bwd_full():
@@ -748,6 +770,17 @@ class DLRMTrainer:
             ("gpu", dense_update),
             ("comm", done),
         ]
+
+    def _gather_applies(self, batch: Batch) -> bool:
+        """One-hot lookups gathered inside the dot interaction: one GPU, plain tables, every
+        bag one index, and the lookup launch able to run its sort role alone (the per-table
+        sort of dlrm_tbe_forward_presort: <= 4096 lookups per table, 32-bit row keys)."""
+        return (self.fuse_gather and batch.one_hot and self.world == 1 and not self.qr_active
+                and self.cfg.arch_interaction_op == "dot" and self.D in (16, 32, 64, 128)
+                and 1 <= self.T_local == self.T and self.T + 1 <= 32
+                and 0 < batch.max_per_table <= ops.TBE_PRESORT_SEG_CAP
+                and self.weights.shape[0] < 0xFFFFFFFF
+                and batch.indices.numel() == self.T * batch.X.shape[0])
 
     def _phys_csr(self, batch: Batch, B: int):
         """(indices, offsets) of the physical tables for this batch: the batch's own CSR, or

@@ -155,6 +155,8 @@ int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream);
  * bottom != NULL: the bottom MLP forward (an independent input of the same step) runs as
  * a third role of the same launch (dlrm_mlp_chain semantics; it must be supported); when
  * the presort does not apply it runs as its own launch.
+ * out == NULL (round 3): no lookup role - its consumer gathers the rows itself
+ * (dlrm_interact_dot_forward_gather); needs the per-table sort to apply (else UNSUPPORTED).
  */
 int dlrm_tbe_forward_presort(const float* weights, int64_t D, const int64_t* row_base, int32_t T,
                              int32_t B, const void* indices, int32_t index_bits,
@@ -358,6 +360,32 @@ int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
                                int64_t ld_gout, float* const* grad_ptrs,
                                const int64_t* grad_bstrides, int32_t relu_x,
                                dlrm_stream_t stream);
+
+/*
+ * The one-hot lookup fused into the dot interaction (one GPU, L = 1: apply_emb with one
+ * index per bag, dlrm_s_pytorch.py:526-587, then interact_features :627-659): feature 0 is
+ * x (x_bstride floats per sample), feature f >= 1 of sample b is row
+ * row_base[f-1] + indices[(f-1) * B + b] of `weights` (table-major CSR indices; row_base
+ * DEVICE int64 [F], its last entry the total row count).  An index outside its table
+ * reads as a zero row (the TBE drops it from its bag) and sets DLRM_TBE_ERR_INDEX in
+ * *error_flag (may be NULL).  Output as dlrm_interact_dot_forward; the [B, T, D] pooled
+ * embeddings are never written.  D in {16, 32, 64, 128}, 2 <= F <= 32, x / weights 16-B
+ * aligned (else UNSUPPORTED / INVALID_ARG).
+ */
+int dlrm_interact_dot_forward_gather(int32_t B, int32_t F, int32_t D, const float* x,
+                                     int64_t x_bstride, const float* weights,
+                                     const int64_t* row_base, const int32_t* indices,
+                                     int32_t self_interaction, float* out, int64_t ld_out,
+                                     int32_t* error_flag, dlrm_stream_t stream);
+/* Its backward: the rows re-gathered from `weights` (call before the embedding update);
+ * gradients and relu_x as dlrm_interact_dot_backward. */
+int dlrm_interact_dot_backward_gather(int32_t B, int32_t F, int32_t D, const float* x,
+                                      int64_t x_bstride, const float* weights,
+                                      const int64_t* row_base, const int32_t* indices,
+                                      int32_t self_interaction, const float* grad_out,
+                                      int64_t ld_gout, float* const* grad_ptrs,
+                                      const int64_t* grad_bstrides, int32_t relu_x,
+                                      dlrm_stream_t stream);
 /* Cat: out[b][f*D:(f+1)*D] = feature f. */
 int dlrm_interact_cat_forward(int32_t B, int32_t F, int32_t D, const float* const* feat_ptrs,
                               const int64_t* feat_bstrides, float* out, int64_t ld_out,

@@ -985,3 +985,42 @@ def test_tbe_c1_full_shape_forward_and_backward_vs_oracle(ops, monkeypatch, dist
         ok, msg = fp32_close(res[ch].numpy(), ref)
         assert ok, (ch, msg)
     assert torch.equal(res["64"], res[""])
+
+
+@pytest.mark.parametrize("D", [16, 32, 64, 128])
+@pytest.mark.parametrize("F,self_int", [(2, False), (9, True), (27, False), (32, False)])
+def test_interact_gather_matches_lookup_then_interact(ops, D, F, self_int):
+    """The one-hot lookup fused into the dot interaction (dlrm_interact_dot_*_gather) vs
+    tbe_forward (L = 1) followed by interact_forward / interact_backward on the pooled
+    buffer: the same rows feed the same MFMA sequence, so results are bit-identical.  An
+    out-of-range index reads as a zero row and raises the TBE index bit, as the lookup does."""
+    torch.manual_seed(D * 100 + F)
+    T, B = F - 1, 203  # B not a multiple of the 4 samples per block
+    rows = [int(r) for r in torch.randint(1, 500, (T,))]
+    row_base = torch.tensor([0] + list(np.cumsum(rows)), dtype=torch.int64, device=dev)
+    W = torch.randn(int(row_base[-1]), D, device=dev)
+    idx = torch.cat([torch.randint(0, n, (B,)) for n in rows]).to(torch.int32).to(dev)
+    off = torch.arange(T * B + 1, dtype=torch.int32, device=dev)
+    x = torch.randn(B, D + 4, device=dev)[:, :D]  # strided x, as the trainer passes it
+    E = ops.tbe_forward(W, row_base, T, B, idx, off)
+    R0 = ops.interact_forward("dot", x, E, self_int)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    R1 = ops.interact_forward_gather(x, W, row_base, idx, self_int, error_flag=err)
+    torch.cuda.synchronize()
+    assert torch.equal(R0, R1)
+    assert int(err.item()) == 0
+    gR = torch.randn_like(R0)
+    gx0, gly0 = ops.interact_backward("dot", x, E, gR, self_int, relu_x=True)
+    gx1, gly1 = ops.interact_backward_gather(x, W, row_base, idx, gR, self_int, relu_x=True)
+    torch.cuda.synchronize()
+    assert torch.equal(gx0, gx1)
+    assert torch.equal(gly0, gly1)
+    # an out-of-range index of the last table: a zero row, flagged
+    bad = idx.clone()
+    bad[(T - 1) * B + 5] = rows[-1]
+    E2 = E.clone()
+    E2[5, T - 1] = 0.0
+    R2 = ops.interact_forward_gather(x, W, row_base, bad, self_int, error_flag=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) & ops.TBE_ERR_INDEX
+    assert torch.equal(R2, ops.interact_forward("dot", x, E2, self_int))

@@ -444,3 +444,44 @@ def test_bottom_backward_full_schedule_vs_oracle(name):
         ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
         assert ok, (s, msg)
     _compare_state(tr, ref)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_gather_fused_step_matches_pooled_path(graph):
+    """One-hot batches with the lookup gathered inside the dot interaction (the lookup
+    launch keeping only its sort role) vs the pooled path (lookup -> [B, T, D] -> interaction):
+    the interaction sees identical rows, so 3 SGD steps leave identical state.  Eager and
+    replayed from a captured graph; a batch with L = 2 keeps the pooled path."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES["c3_small"]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function="bce",
+                        learning_rate=0.1)
+    res = []
+    for fuse in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.fuse_gather = fuse
+        batches = [tr.synthetic_batch(512, 1, seed=s) for s in range(3)]
+        if graph:
+            tr.step(batches[0])  # eager warm-up step (allocations), then capture
+            run = tr.capture(batches[0])
+            for b in batches:
+                for src, dst in zip((b.X, b.offsets, b.indices, b.target),
+                                    (batches[0].X, batches[0].offsets, batches[0].indices,
+                                     batches[0].target)):
+                    if src is not dst:
+                        dst.copy_(src)
+                run()
+        else:
+            for b in batches:
+                tr.step(b)
+        assert tr.gather_fused == fuse
+        torch.cuda.synchronize()
+        tr.check_errors()
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
+                    tr._bufs[(512, 512)]["prob"].cpu().clone()))
+        tr.step(tr.synthetic_batch(256, 2, seed=9))
+        assert not tr.gather_fused
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
