@@ -872,14 +872,22 @@ __device__ __forceinline__ float lo_f(unsigned u) { return __builtin_bit_cast(fl
 __device__ __forceinline__ float hi_f(unsigned u) {
   return __builtin_bit_cast(float, u & 0xffff0000u);
 }
+// The conversion is opaque inline asm so the compiler keeps lo_f(h) as one shift (left to
+// itself it re-converts x0 alone); gemm.hip is built with -fno-slp-vectorize so the two
+// subtractions stay v_sub_f32 (a v_pk_add_f32 beside MFMAs costs ~26 cycles per gap).
+__device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 // x0, x1 -> packed (h, m, l) bf16 pairs, x = h + m + l exactly.
 __device__ __forceinline__ void split2(float x0, float x1, unsigned& h, unsigned& m,
                                        unsigned& l) {
-  h = pk_bf16(x0, x1);
+  h = cvt_pk_bf16(x0, x1);
   const float r0 = x0 - lo_f(h), r1 = x1 - hi_f(h);
-  m = pk_bf16(r0, r1);
+  m = cvt_pk_bf16(r0, r1);
   const float s0 = r0 - lo_f(m), s1 = r1 - hi_f(m);
-  l = pk_bf16(s0, s1);
+  l = cvt_pk_bf16(s0, s1);
 }
 
 // bf16 three-plane image of one operand's (MN x 32) panel (one LDS buffer).
@@ -1106,6 +1114,328 @@ __device__ __forceinline__ void pipe_body6(const GemmParams& p, int lb, float* s
   finish_tile<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0, smem);
 }
 
+// ------------------------------------------------- split-bf16 body, 128x128 tiles --
+// The x6 math of pipe_body6 on v_mfma_f32_32x32x16_bf16, 128x128 workgroup tiles on 2x2
+// waves (64x64 per wave, one wave per SIMD).  Why this shape: the split costs ~22 VALU
+// cycles per 64 staged elements and an MFMA leaves the SIMD's vector issue free for 24 of
+// its 32 cycles (32x32x16; 8 of 16 on 16x16x32), so the split fits beside the MFMAs only
+// when a tile does enough MFMA work per staged element: (BM + BN) / (BM * BN) small.  At
+// 64x64 / 16x16x32 (pipe_body6) the split needs ~1.8x the free issue cycles (VALU-bound);
+// at 128x128 / 32x32x16 it needs ~0.6x.  Fewer, larger tiles are made up by split-K (the
+// plan's split count, in-launch or PARTIAL).
+// Measured (profiles/r03_x6l_ab.txt, r03_x6l_pmc.txt): accurate (max error below the f32
+// body's) but no faster than the exact-f32 body on the C3 shapes - the split's VALU issue
+// (~250 instructions per K-tile and wave) exceeds the 24 free issue cycles per MFMA, and
+// 128x128 tiles fill only half the CUs at M = 2048 unless K is split.  Kept as an A/B body
+// (DLRM_GEMM_MATH=x6l, plan entries with x6 = 2); the default plan does not use it.
+// Per K-tile (32 k) a 64x64 wave runs 2 k16-steps x 6 products x 2x2 tiles = 48 MFMAs (1536
+// cycles); the step-1 fragments are read under step 0, the next tile's step-0 fragments
+// after the barrier under the last product of step 1; staging of tile t+1 (split to three
+// planes on the way into LDS) and the fetch of tile t+2 ride between the MFMA groups.
+// LDS images: Img6 with the !KC pitch MN + 32 (row stride = 16 dwords mod 64): the two
+// 16-lane groups of a half-wave read columns +0 / +16 of the same four k rows with
+// ds_read_b64_tr_b16 on disjoint banks; KC rows of 40 bf16 (20 dwords) keep a 16-lane
+// ds_read_b128 group on 64 distinct banks.
+template <int MN, bool KC>
+struct Img6L {
+  static constexpr int BK = kBK;
+  static constexpr int PITCH = KC ? BK + 8 : MN + 32;  // bf16 per row
+  static constexpr int OCT = 8 * PITCH;                // !KC: bf16 per k-octet
+  static constexpr int PLANE = KC ? MN * PITCH : (BK / 8) * OCT;
+  static constexpr int SIZE = 3 * PLANE;  // bf16 per buffer
+
+  __device__ __forceinline__ static void store(__bf16* buf, int mn, int k, float4 f) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split2(f.x, f.y, h0, m0, l0);
+    split2(f.z, f.w, h1, m1, l1);
+    const int e = KC ? mn * PITCH + k : (k >> 3) * OCT + (k & 7) * PITCH + mn;
+    *reinterpret_cast<uint2*>(buf + e) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(buf + PLANE + e) = make_uint2(m0, m1);
+    *reinterpret_cast<uint2*>(buf + 2 * PLANE + e) = make_uint2(l0, l1);
+  }
+
+  // 32x32x16 operand fragment of the 32-wide sub-tile at mn0, k16-step `step` of the
+  // K-tile: lane l holds mn0 + (l & 31), k = 16 step + 8 (l >> 5) .. +7 of plane q.
+  __device__ __forceinline__ static bf16x8 frag(const __bf16* buf, int q, int mn0, int lane,
+                                                int step) {
+    const __bf16* pl = buf + q * PLANE;
+    if constexpr (KC) {
+      return __builtin_bit_cast(
+          bf16x8, *reinterpret_cast<const uint4*>(pl + (mn0 + (lane & 31)) * PITCH + 16 * step +
+                                                  8 * (lane >> 5)));
+    } else {
+      // 16-lane group g: columns mn0 + 16 (g & 1) .. +15, k-octet 2 step + (g >> 1); lane
+      // 4r+c of the group addresses row r, columns 4c..4c+3 (ds_read_b64_tr_b16)
+      const int l16 = lane & 15, r = l16 >> 2, c = l16 & 3;
+      const __bf16* b0 = pl + (2 * step + (lane >> 5)) * OCT + r * PITCH + mn0 +
+                         16 * ((lane >> 4) & 1) + 4 * c;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0 + 4 * PITCH));
+      using s16x8 = __attribute__((ext_vector_type(8))) short;
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+template <int BM, int BN>
+constexpr int x6l_smem_bytes() {
+  constexpr int a = Img6L<BM, true>::SIZE > Img6L<BM, false>::SIZE ? Img6L<BM, true>::SIZE
+                                                                    : Img6L<BM, false>::SIZE;
+  constexpr int b = Img6L<BN, true>::SIZE > Img6L<BN, false>::SIZE ? Img6L<BN, true>::SIZE
+                                                                    : Img6L<BN, false>::SIZE;
+  return 2 * (a + b) * 2;  // double-buffered, 2 B per bf16
+}
+
+// finish_tile for 32x32 accumulators (register r of lane l: row 8 (r >> 2) + 4 (l >> 5) +
+// (r & 3), column l & 31); rs[i] is the row sum of row wm0 + 32 i + (l & 31).
+template <int BM, int BN, int WGM, int WGN, bool RS, int FM, int FN>
+__device__ __forceinline__ void finish_tile32(const GemmParams& p, const f32x16 (&acc)[FM][FN],
+                                              float (&rs)[FM], int tile, int split, int tn,
+                                              int64_t m0, int64_t n0, float* smem) {
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int hi = lane >> 5;
+  const int l32 = lane & 31;
+  const int wm0 = (wave / WGN) * WM;
+  const int wn0 = (wave % WGN) * WN;
+  const bool rs_owner = RS && tn == 0 && (wave % WGN) == 0 && hi == 0;
+  constexpr int NV = FM * FN * 16;
+  float v[NV];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[(i * FN + j) * 16 + r] = acc[i][j][r];
+  auto row_of = [&](int i, int r) -> int64_t {
+    return m0 + wm0 + i * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+  };
+  if (p.mode == DLRM_GEMM_PARTIAL) {
+    float* slab = p.part + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t col = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = row_of(i, r);
+          if (row < p.M && col < p.N) slab[row * p.N + col] = v[(i * FN + j) * 16 + r];
+        }
+      }
+    if (rs_owner) {
+      float* rslab = p.part + (int64_t)p.splits * p.M * p.N + (int64_t)split * p.M;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int64_t row = m0 + wm0 + i * 32 + l32;
+        if (row < p.M) rslab[row] = rs[i];
+      }
+    }
+    return;
+  }
+  if (!splitk_reduce<BM, BN, NV, FM>(p, tile, split, v, rs, wm0 + l32, 32, rs_owner, smem))
+    return;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t col = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = row_of(i, r);
+        if (row < p.M && col < p.N)
+          apply_epilogue(p, row, col, p.alpha * v[(i * FN + j) * 16 + r]);
+      }
+    }
+  if (rs_owner) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int64_t row = m0 + wm0 + i * 32 + l32;
+      if (row < p.M) apply_epilogue(p, row, p.ones_col, p.alpha * rs[i]);
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS>
+__device__ __forceinline__ void pipe_body6L(const GemmParams& p, int lb, float* smem) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int FM = WM / 32, FN = WN / 32;
+  static_assert(FM >= 1 && FN >= 1, "wave sub-tile");
+  using SA = Stage<BM, kBK, A_KC, true, NT>;
+  using SB = Stage<BN, kBK, B_KC, true, NT>;
+  using IA = Img6L<BM, A_KC>;
+  using IB = Img6L<BN, B_KC>;
+  constexpr int BUF = IA::SIZE + IB::SIZE;  // bf16 per LDS buffer
+  constexpr int NS = SA::NV + SB::NV;       // staged float4 per thread per K-tile
+  constexpr int NP = 6;                     // bf16 products per k16-step
+  static_assert(NS <= 2 * NP - 1, "staging must finish before the barrier");
+  static_assert(!RS || !A_KC, "row sums are taken on the mn-contiguous A (wgrad)");
+
+  const int tile = lb / p.splits;
+  const int split = lb - tile * p.splits;
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM;
+  const int64_t n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * p.kchunk;
+  const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wm0 = (wave / WGN) * WM;
+  const int wn0 = (wave % WGN) * WN;
+  __bf16* lds = reinterpret_cast<__bf16*>(smem);
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float4 rsq[SA::NV];  // RS: this thread's staged A float4s summed over its k rows
+#pragma unroll
+  for (int v = 0; v < SA::NV; ++v) rsq[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
+  SA sa;
+  SB sb;
+  const int64_t a_ext = A_KC ? (p.M - 1) * p.lda + p.K : (p.K - 1) * p.lda + p.M;
+  const int64_t b_ext = B_KC ? (p.N - 1) * p.ldb + p.K : (p.K - 1) * p.ldb + p.N;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)(a_ext * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)(b_ext * 4), 0x00020000);
+  typename SA::Fetch fa;
+  typename SB::Fetch fb;
+  sa.fetch_init(fa, p.lda, m0, p.M, kbeg, tid);
+  sb.fetch_init(fb, p.ldb, n0, p.N, kbeg, tid);
+  const int a_step = A_KC ? kBK * 4 : (int)(kBK * p.lda * 4);
+  const int b_step = B_KC ? kBK * 4 : (int)(kBK * p.ldb * 4);
+  const int kb32 = (int)kbeg, K32 = (int)p.K;
+  auto fetch_one = [&](int c, int t) {
+    if (c < SA::NV)
+      sa.fetch4(c, fa, ra, a_step, t, kb32 + t * kBK, K32);
+    else
+      sb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * kBK, K32);
+  };
+  auto put_one = [&](int c, __bf16* buf, bool live) {  // live: the tile is < nk
+    int mn, k;
+    if (c < SA::NV) {
+      sa.coords(tid + c * NT, mn, k);
+      IA::store(buf, mn, k, sa.regs[c]);
+      if (RS && live) {
+        rsq[c].x = add_f32(rsq[c].x, sa.regs[c].x);
+        rsq[c].y = add_f32(rsq[c].y, sa.regs[c].y);
+        rsq[c].z = add_f32(rsq[c].z, sa.regs[c].z);
+        rsq[c].w = add_f32(rsq[c].w, sa.regs[c].w);
+      }
+    } else {
+      sb.coords(tid + (c - SA::NV) * NT, mn, k);
+      IB::store(buf + IA::SIZE, mn, k, sb.regs[c - SA::NV]);
+    }
+  };
+  struct Frag {
+    bf16x8 q[3];
+  };
+  auto read_frags = [&](const __bf16* buf, int step, Frag (&a)[FM], Frag (&b)[FN]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i].q[q] = IA::frag(buf, q, wm0 + i * 32, lane, step);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j].q[q] = IB::frag(buf + IA::SIZE, q, wn0 + j * 32, lane, step);
+    }
+  };
+  auto products = [&](int s, const Frag (&ca)[FM], const Frag (&cb)[FN]) {
+    constexpr int PA[NP] = {0, 2, 1, 0, 1, 0};
+    constexpr int PB[NP] = {2, 0, 1, 1, 0, 0};
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ca[i].q[PA[s]], cb[j].q[PB[s]],
+                                                            acc[i][j], 0, 0, 0);
+  };
+
+  Frag a0[FM], b0[FN], a1[FM], b1[FN];
+#pragma unroll
+  for (int c = 0; c < NS; ++c) fetch_one(c, 0);
+#pragma unroll
+  for (int c = 0; c < NS; ++c) put_one(c, lds, true);
+#pragma unroll
+  for (int c = 0; c < NS; ++c) fetch_one(c, 1);
+  __syncthreads();
+  read_frags(lds, 0, a0, b0);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const __bf16* cbuf = lds + (kt & 1) * BUF;
+    __bf16* nbuf = lds + ((kt + 1) & 1) * BUF;
+    const bool live = kt + 1 < nk;
+    read_frags(cbuf, 1, a1, b1);  // step 1 of this tile, consumed after step 0
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      products(s, a0, b0);
+      if (s < NS) {
+        put_one(s, nbuf, live);  // tile t+1 (staged last iteration) -> LDS planes
+        fetch_one(s, kt + 2);    // refill with tile t+2
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int s = 0; s < NP - 1; ++s) {
+      products(s, a1, b1);
+      if (NP + s < NS) {
+        put_one(NP + s, nbuf, live);
+        fetch_one(NP + s, kt + 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // tile t+1 complete in LDS; every wave is done reading tile t
+    read_frags(nbuf, 0, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    products(NP - 1, a1, b1);
+  }
+
+  float rs[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) rs[i] = 0.f;
+  if constexpr (RS) {
+    constexpr int Q = BM / 4, R = NT / Q;
+    static_assert(NT % Q == 0, "row-sum map");
+    float4 t = rsq[0];
+#pragma unroll
+    for (int v = 1; v < SA::NV; ++v) {
+      t.x = add_f32(t.x, rsq[v].x);
+      t.y = add_f32(t.y, rsq[v].y);
+      t.z = add_f32(t.z, rsq[v].z);
+      t.w = add_f32(t.w, rsq[v].w);
+    }
+    __syncthreads();  // every wave is done with the LDS images
+    float* part = smem;  // [R][BM]
+    *reinterpret_cast<float4*>(part + (tid / Q) * BM + 4 * (tid % Q)) = t;
+    __syncthreads();
+    float* sums = smem + R * BM;  // [BM]
+    if (tid < BM) {
+      float s = part[tid];
+      for (int r = 1; r < R; ++r) s += part[r * BM + tid];
+      sums[tid] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i) rs[i] = sums[wm0 + i * 32 + (lane & 31)];
+    __syncthreads();  // the split-K hand-off reuses smem[0]
+  }
+  finish_tile32<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0, smem);
+}
+
 // REDUCE job: C = epi(alpha * sum_s part[s]) in split order (the same additions as the
 // in-launch reduction), one float4 of the [M][N] slab per thread, then one row sum per
 // thread for ones_col.  Up to 8 splits' loads in flight.
@@ -1244,6 +1574,32 @@ __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group6_kernel(const Ge
     if (kind == 4) return pipe_body6<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
 }
 
+// The same grouped launch on the 128x128 split-bf16 body (pipe_body6L): one wave per SIMD.
+template <int BM, int BN, int WGM, int WGN, int KINDS>
+__global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_group6L_kernel(const GemmGroup g) {
+  __shared__ __attribute__((aligned(16))) float smem[x6l_smem_bytes<BM, BN>() / 4];
+  const int b = blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxGroup; ++i)
+    if (i < g.n && b >= g.p[i].block0) q = i;
+  const GemmParams& p = g.p[q];
+  const int nq = (q + 1 < g.n ? g.p[q + 1].block0 : g.total) - p.block0;
+  const int lb = xcd_remap(b - p.block0, nq);
+  if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
+  const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
+  if constexpr ((KINDS & 1) != 0)
+    if (kind == 0) return pipe_body6L<BM, BN, WGM, WGN, true, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 2) != 0)
+    if (kind == 1) return pipe_body6L<BM, BN, WGM, WGN, true, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 4) != 0)
+    if (kind == 2) return pipe_body6L<BM, BN, WGM, WGN, false, false, false>(p, lb, smem);
+  if constexpr ((KINDS & 8) != 0)
+    if (kind == 3) return pipe_body6L<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
+  if constexpr ((KINDS & 16) != 0)
+    if (kind == 4) return pipe_body6L<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
+}
+
 // Fallback for operands the pipelined body cannot take (unaligned rows, ragged float4
 // extents, > 2 GiB extents): 32x32x2 MFMA, register-staged, unsplit, element-guarded.
 template <bool A_KC, bool B_KC>
@@ -1341,9 +1697,10 @@ int env_int(const char* name, int dflt) {
 // Math of the pipelined GEMMs: exact-f32 MFMA, or the split-bf16 body where the plan table
 // measured it faster and every GEMM of the launch agrees (default "auto"); DLRM_GEMM_MATH=
 // f32 / x6 forces one everywhere.  Read per call, like the tuning overrides.
-int gemm_math_env() {  // 0 f32, 1 x6, -1 auto
+int gemm_math_env() {  // 0 f32, 1 x6 (64-wide tiles), 2 x6 on 128x128 tiles, -1 auto
   const char* v = getenv("DLRM_GEMM_MATH");
   if (v && strcmp(v, "x6") == 0) return 1;
+  if (v && strcmp(v, "x6l") == 0) return 2;
   if (v && strcmp(v, "f32") == 0) return 0;
   return -1;
 }
@@ -1400,7 +1757,8 @@ struct PlanEntry {
   int64_t M, N, K;
   int layout, bm, bn, split;
   int wm = 2, wn = 2;
-  int x6 = 0;   // 1: the split-bf16 body measured faster (tools/gemm_x6_ab.py)
+  int x6 = 0;   // 1: the split-bf16 body measured faster (tools/gemm_x6_ab.py); 2: on
+                //    128x128 tiles (pipe_body6L)
   int dma = 0;  // 1: the LDS-DMA f32 body (tools/gemm_body_ab.py)
 };
 
@@ -1442,6 +1800,23 @@ void big_override(const Desc& d, Tile& t, Plan& pl) {
   if (v[5] == 'h' && pl.splits > 1) pl = make_plan(pl.splits / 2, d.K);
 }
 
+// DLRM_GEMM_MATH=x6l: every problem of >= 2^18 outputs on the 128x128 split-bf16 body,
+// K split until the tiles fill the CUs once (>= 256 blocks, K chunks >= 128).  The split is
+// decided here, per problem, so a problem sums in the same order in any launch.
+void x6l_override(const Desc& d, Tile& t, Plan& pl) {
+  if (gemm_math_env() != 2 || d.M * d.N < (1 << 18)) return;
+  t = Tile{128, 128, 2, 2, 2};
+  const int force_split = env_int("DLRM_GEMM_SPLIT", 0);  // (A/B sweeps)
+  if (force_split > 0) {
+    pl = make_plan(force_split, d.K);
+    return;
+  }
+  const int64_t tiles = dlrm::ceil_div(d.M, 128) * dlrm::ceil_div(d.N, 128);
+  int64_t s = 1;
+  while (tiles * s < 256 && dlrm::ceil_div(d.K, s + 1) >= 128 && s < kMaxSplit) ++s;
+  pl = make_plan(s, d.K);
+}
+
 void plan_one(const Desc& d, Tile& t, Plan& pl) {
   t = Tile{64, 64, 2, 2};
   if (d.mode == DLRM_GEMM_REDUCE) {  // elementwise job: no tiles, no K
@@ -1471,6 +1846,7 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
       if (e.M == d.M && e.N == d.N && e.K == d.K && e.layout == layout_of(d)) {
         t = Tile{e.bm, e.bn, e.wm, e.wn, e.x6, e.dma};
         pl = make_plan(e.split, d.K);
+        if (e.x6 != 2) x6l_override(d, t, pl);
         big_override(d, t, pl);
         return;
       }
@@ -1484,6 +1860,7 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
   int64_t s = 1;
   while (tiles * s < target && dlrm::ceil_div(d.K, s + 1) >= 256 && s < kMaxSplit) ++s;
   pl = make_plan(s, d.K);
+  x6l_override(d, t, pl);
   big_override(d, t, pl);
 }
 
@@ -1492,13 +1869,14 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
 void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   bool first = true;
   t = Tile{64, 64, 2, 2};
-  int votes = 0, gemms = 0, dvotes = 0;
+  int votes = 0, gemms = 0, dvotes = 0, lvotes = 0;
   for (int i = 0; i < n; ++i) {
     Tile a;
     plan_one(d[i], a, pl[i]);
     if (d[i].mode == DLRM_GEMM_REDUCE) continue;
     ++gemms;
-    votes += a.x6;
+    votes += a.x6 == 1;
+    lvotes += a.x6 == 2;
     dvotes += a.dma;
     if (first) {
       t = a;
@@ -1508,9 +1886,12 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
     }
   }
   const int env = gemm_math_env();
-  t.x6 = env >= 0 ? env : (gemms > 0 && votes == gemms);
+  // 128x128 split-bf16 only when every GEMM of the launch asks for it (their tiles agree)
+  t.x6 = gemms > 0 && lvotes == gemms ? 2 : env == 1 ? 1 : env == 0 ? 0
+         : (gemms > 0 && votes == gemms);
   t.dma = gemms > 0 && dvotes == gemms;  // every GEMM of the launch asks for the DMA body
-  if (t.x6 && (t.bm == 128 || t.bn == 128)) t = Tile{64, 64, 2, 2, 1};
+  if (t.x6 == 1 && (t.bm == 128 || t.bn == 128)) t = Tile{64, 64, 2, 2, 1};
+  if (t.x6 != 2 && t.bm == 128 && t.bn == 128) t = Tile{64, 32, 2, 2, t.x6, t.dma};
 }
 
 // Split-K workspace: the fixed 64 KiB ticket head, then each problem's records.
@@ -1530,7 +1911,7 @@ size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
 
 // Body of a launch: kBodyReg (register-staged f32 pipe_body), kBodyX6 (split-bf16),
 // kBodyDma (LDS-DMA f32 pipe_body_dma, where the plan asks for it).
-constexpr int kBodyReg = 0, kBodyX6 = 1, kBodyDma = 2;
+constexpr int kBodyReg = 0, kBodyX6 = 1, kBodyDma = 2, kBodyX6L = 3;
 
 // f32 body of a launch: the plan's vote, or DLRM_GEMM_BODY=reg / dma everywhere (A/B; read
 // per call).
@@ -1589,7 +1970,18 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
   // row sums, two wgrads), else all kinds
-  if constexpr (BODY == kBodyX6) {
+  if constexpr (BODY == kBodyX6L) {
+    switch (kinds) {
+#define K_(M_)                                                                            \
+  case M_:                                                                               \
+    hipLaunchKernelGGL((gemm_group6L_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g); \
+    break;
+      K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
+#undef K_
+      default:
+        hipLaunchKernelGGL((gemm_group6L_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
+    }
+  } else if constexpr (BODY == kBodyX6) {
     switch (kinds) {
 #define K_(M_)                                                                           \
   case M_:                                                                              \
@@ -1734,6 +2126,9 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
     for (int i = 0; i < m; ++i)
       if (q[i].mode == DLRM_GEMM_FULL) pl[i] = make_plan(1, q[i].K);
   }
+  // 128x128 split-bf16 on 2x4 waves (64x32 per wave, two waves per SIMD; the 2x2 layout,
+  // one wave per SIMD, measured 1.15x slower: profiles/r03_x6l_ab.txt)
+  if (t.x6 == 2) return launch_group<128, 128, kBodyX6L, 2, 4>(m, q, pl, ws, ws_bytes, st);
   if (t.x6) {  // split-bf16 body: 128-wide tiles stage too much per K-tile (and 128x128 on
               // 8-wave workgroups leaves half the CUs idle at M = 2048: r03_gemm_tiles_ab.txt)
     if (t.bm == 32) return launch_group<32, 64, kBodyX6>(m, q, pl, ws, ws_bytes, st);

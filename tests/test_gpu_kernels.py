@@ -1024,3 +1024,64 @@ def test_interact_gather_matches_lookup_then_interact(ops, D, F, self_int):
     torch.cuda.synchronize()
     assert int(err.item()) & ops.TBE_ERR_INDEX
     assert torch.equal(R2, ops.interact_forward("dot", x, E2, self_int))
+
+
+@pytest.mark.parametrize("split", ["1", "3"])
+def test_gemm_x6l_body(ops, split, monkeypatch):
+    """The 128x128 split-bf16 body (DLRM_GEMM_MATH=x6l, pipe_body6L, 32x32x16 MFMA, 2x4
+    waves): ragged shapes in all four operand layouts within the fp32 dot-product bound;
+    epilogues (bias+ReLU, ReLU', SGD with the ones_col bias row sums); a PARTIAL problem
+    + REDUCE bitwise equal to the in-launch split."""
+    monkeypatch.setenv("DLRM_GEMM_MATH", "x6l")
+    monkeypatch.setenv("DLRM_GEMM_SPLIT", split)
+    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
+    for (M, N, K) in [(1000, 300, 130), (2048, 256, 480), (515, 520, 36)]:
+        for ta, tb in [(0, 1), (0, 0), (1, 0), (1, 1)]:
+            torch.manual_seed(M + N + K + ta * 3 + tb)
+            A = torch.randn(K, M) if ta else torch.randn(M, K)
+            Bm = torch.randn(N, K) if tb else torch.randn(K, N)
+            opA = A.double().t() if ta else A.double()
+            opB = Bm.double().t() if tb else Bm.double()
+            C = ops.gemm(A.to(dev), Bm.to(dev), bool(ta), bool(tb), workspace=ws).cpu()
+            ok, msg = gemm_close(C.numpy(), (opA @ opB).numpy(),
+                                 (opA.abs() @ opB.abs()).numpy(), K)
+            assert ok, (M, N, K, ta, tb, msg)
+    torch.manual_seed(3)
+    M, N, K = 1024, 300, 130
+    X, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
+    Y = ops.gemm(X.to(dev), W.to(dev), False, True, epilogue=ops.EPI_BIAS_RELU, bias=b.to(dev),
+                 workspace=ws).cpu()
+    ref = X.double() @ W.double().t() + b.double()
+    ok, msg = gemm_close(Y.numpy(), torch.relu(ref).numpy(),
+                         (X.double().abs() @ W.double().abs().t() + b.double().abs()).numpy(), K)
+    assert ok, msg
+    G, aux = torch.randn(M, N), torch.randn(M, K)
+    dX = ops.gemm(G.to(dev), W.to(dev), epilogue=ops.EPI_DRELU, aux=aux.to(dev),
+                  workspace=ws).cpu()
+    ref = (G.double() @ W.double()) * (aux > 0)
+    ok, msg = gemm_close(dX.numpy(), ref.numpy(), (G.double().abs() @ W.double().abs()).numpy(), N)
+    assert ok, msg
+    # wgrad + fused SGD + bias row sums: FULL in-launch vs PARTIAL + REDUCE (bitwise)
+    Bt, Nout, Kw = 2048, 512, 256
+    g = torch.randn(Bt, Nout, device=dev)
+    Xw = torch.randn(Bt, Kw + 4, device=dev)
+    W0 = torch.randn(Nout, Kw + 4, device=dev)
+    kw = dict(trans_a=True, alpha=0.5, epilogue=ops.EPI_SGD, ones_col=Kw)
+    W1 = W0.clone()
+    pr, _ = ops.gemm_problem(g, Xw[:, :Kw], C=W1, **kw)
+    ops.gemm_group([pr], ws)
+    s = ops.gemm_splits(pr, partial=True)
+    W2 = W0.clone()
+    part = torch.empty(ops.gemm_partial_bytes(Nout, Kw, s) // 4, device=dev)
+    pp, _ = ops.gemm_problem(g, Xw[:, :Kw], C=W2, partial=part, splits=s, **kw)
+    ops.gemm_group([pp], ws)
+    ops.gemm_group([ops.reduce_problem(pp)], ws)
+    torch.cuda.synchronize()
+    assert torch.equal(W1, W2)
+    gd, Xd = g.double().cpu(), Xw[:, :Kw].double().cpu()
+    got = (W0 - W1).double().cpu() / 0.5
+    ok, msg = gemm_close(got[:, :Kw].numpy(), (gd.t() @ Xd).numpy(),
+                         (gd.abs().t() @ Xd.abs()).numpy(), Bt + 8)
+    assert ok, msg
+    ok, msg = gemm_close(got[:, Kw].numpy(), gd.sum(0).numpy(), gd.abs().sum(0).numpy(), Bt + 8)
+    assert ok, msg
