@@ -1062,7 +1062,7 @@ def test_gemm_x6l_body(ops, split, monkeypatch):
     ok, msg = gemm_close(dX.numpy(), ref.numpy(), (G.double().abs() @ W.double().abs()).numpy(), N)
     assert ok, msg
     # wgrad + fused SGD + bias row sums: FULL in-launch vs PARTIAL + REDUCE (bitwise)
-    Bt, Nout, Kw = 2048, 512, 256
+    Bt, Nout, Kw = 2048, 1024, 512  # >= 2^18 outputs: the x6l planner takes it
     g = torch.randn(Bt, Nout, device=dev)
     Xw = torch.randn(Bt, Kw + 4, device=dev)
     W0 = torch.randn(Nout, Kw + 4, device=dev)
@@ -1070,7 +1070,7 @@ def test_gemm_x6l_body(ops, split, monkeypatch):
     W1 = W0.clone()
     pr, _ = ops.gemm_problem(g, Xw[:, :Kw], C=W1, **kw)
     ops.gemm_group([pr], ws)
-    s = ops.gemm_splits(pr, partial=True)
+    s = ops.gemm_splits(pr)  # the FULL plan's split, repeated by the PARTIAL problem
     W2 = W0.clone()
     part = torch.empty(ops.gemm_partial_bytes(Nout, Kw, s) // 4, device=dev)
     pp, _ = ops.gemm_problem(g, Xw[:, :Kw], C=W2, partial=part, splits=s, **kw)
