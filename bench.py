@@ -156,12 +156,13 @@ def _sleep_cycles_for(ms: float) -> int:
     return int(per_ms * ms)
 
 
-def pmc_traffic():
-    """HBM bytes per step of the GEMM group from the newest committed PMC summary
-    (profiles/rNN_pmc_traffic.json, made by tools/pmc_summary.py from rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench); None when absent."""
+def pmc_traffic(config: str):
+    """HBM bytes per step of the GEMM group from the newest committed PMC summary of this
+    bench config (profiles/rNN_pmc_traffic.json, made by tools/pmc_summary.py from
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench); None when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+             if json.load(open(f)).get("_config", "terabyte") == config]
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -250,28 +251,28 @@ def preheat_device(dev, ms: float) -> float:
     """Setup, not measurement: a 4096^3 GEMM loop on scratch buffers (no model state read or
     written) for ~ms milliseconds.  From idle the chip needs ~50 steps (~25 ms) of load to
     reach its steady clocks (tools/ramp_probe.py, profiles/r03_ramp_probe.txt: the first 50
-    steps average 487 us against 451 us after), which a 5-step warm-up does not give."""
-    from dlrm_hip import ops
+    steps average 487 us against 451 us after), which a 5-step warm-up does not give.  It runs
+    on torch.matmul (hipBLASLt), so a kernel trace of the bench keeps the library's GEMM
+    kernels to the step's own launches."""
     n = 4096
     A = torch.randn(n, n, device=dev)
     C = torch.empty(n, n, device=dev)
-    ws = torch.zeros(ops.gemm_group_workspace_size([ops.gemm_problem(A, A, C=C)[0]]) + 256,
-                     dtype=torch.uint8, device=dev)
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < ms:
         for _ in range(4):
-            ops.gemm(A, A, C=C, workspace=ws)
+            torch.matmul(A, A, out=C)
         torch.cuda.synchronize()
     el = (time.perf_counter() - t0) * 1e3
-    del A, C, ws
+    del A, C
     return round(el, 1)
 
 
 def box_calibration(dev):
-    """Fixed-work probes that separate box-to-box variance from code regressions: the
-    library's own f32 MFMA GEMM at 4096^3 (TFLOP/s), a 1 GiB device-to-device copy (GB/s,
-    read + write), and the clocks the SMI reports (rocm-smi; may be absent)."""
-    from dlrm_hip import ops
+    """Fixed-work probes that separate box-to-box variance from code regressions: a 4096^3
+    f32 GEMM on hipBLASLt (torch.matmul, TFLOP/s; a kernel the step never runs, so the
+    bench's kernel trace keeps the library's GEMM kernels to the step), a 1 GiB
+    device-to-device copy (GB/s, read + write), and the clocks the SMI reports (rocm-smi;
+    may be absent)."""
     out = {}
     try:
         g = torch.Generator(device=dev).manual_seed(3)
@@ -279,10 +280,8 @@ def box_calibration(dev):
         A = torch.randn(n, n, device=dev, generator=g)
         Bm = torch.randn(n, n, device=dev, generator=g)
         C = torch.empty(n, n, device=dev)
-        ws = torch.zeros(ops.gemm_group_workspace_size([ops.gemm_problem(A, Bm, C=C)[0]]) + 256,
-                         dtype=torch.uint8, device=dev)
-        us = _graph_time_us(lambda: ops.gemm(A, Bm, C=C, workspace=ws), n=5, reps=4)
-        out["gemm_f32_4096_tflops"] = round(2 * n ** 3 / us / 1e6, 2)
+        us = _graph_time_us(lambda: torch.matmul(A, Bm, out=C), n=5, reps=4)
+        out["gemm_f32_4096_tflops_hipblaslt"] = round(2 * n ** 3 / us / 1e6, 2)
         src = torch.empty(1 << 28, device=dev)  # 1 GiB
         dst = torch.empty_like(src)
         us = _graph_time_us(lambda: dst.copy_(src), n=5, reps=4)
@@ -644,7 +643,7 @@ def main():
         gemm_ms = tot.get("gemm", 0.0)
         if gemm_ms > 0:
             ach = flops / (gemm_ms * 1e-3) / 1e12
-            traffic, tsrc = pmc_traffic() if world == 1 else (None, None)
+            traffic, tsrc = pmc_traffic(args.config) if world == 1 else (None, None)
             roofline = {"bound": "mfma", "kernel": "gemm_f32_mfma (all MLP GEMM launches)",
                         "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS,
                         "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFS, 4),
