@@ -40,14 +40,17 @@ CONFIGS = {
                      bot=[13, 512, 256, 128], top=[1024, 1024, 512, 256, 1], B=2048, L=1,
                      loss="bce", lr=1.0, optimizer="sgd"),
     # C4: --qr-flag --qr-collisions=4 --qr-operation=mult --qr-threshold=200
-    # --optimizer=rwsadagrad.  lr 1e-3: with the QR init U[sqrt(1/n), 1]
+    # --optimizer=rwsadagrad.  lr 1e-4: with the QR init U[sqrt(1/n), 1]
     # the reference's model saturates its sigmoid after one RWSAdagrad step at lr >= 0.01
-    # (BCE ~50, no recovery) and trains at 1e-3 (tools/c4_lr_probe.py on the oracle,
-    # profiles/r03_c4_lr_probe.txt); the step's work does not depend on lr
+    # (BCE ~50: every output exactly 0 or 1, zero gradient, no recovery; tools/c4_lr_probe.py
+    # on the oracle), and at 1e-3 it recovers or not depending on the init seed; at 1e-4 the
+    # loss stays near 0.69 and falls for every seed tried (tools/c4_trajectory.py on the
+    # engine at full size, profiles/r03_c4_trajectory.txt).  The step's work does not
+    # depend on lr.
     "terabyte_qr_rwsadagrad": dict(workload="mlperf_terabyte_synthetic+qr+rwsadagrad",
                                    rows=TERABYTE_ROWS, D=128, bot=[13, 512, 256, 128],
                                    top=[1024, 1024, 512, 256, 1], B=2048, L=1, loss="bce",
-                                   lr=0.001, optimizer="rwsadagrad",
+                                   lr=0.0001, optimizer="rwsadagrad",
                                    qr=dict(collisions=4, operation="mult", threshold=200)),
     "small": dict(workload="synthetic_small", rows=[100000] * 8, D=64, bot=[512, 512, 64],
                   top=[1024, 1024, 1024, 1], B=2048, L=100, loss="mse", lr=0.1, optimizer="sgd"),

@@ -485,3 +485,45 @@ def test_gather_fused_step_matches_pooled_path(graph):
         assert not tr.gather_fused
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_c4_terabyte_widths_trajectory_vs_oracle():
+    """C4 (QR mult, 4 collisions, threshold 200 + RWSAdagrad) at the Terabyte widths (D = 128,
+    bot 13-512-256-128, top 479-1024-1024-512-256-1) with the 26 tables capped at 20k rows,
+    B = 256, lr 1e-3: 10 steps on 10 batches against the oracle's QREmbeddingBag +
+    RWSAdagrad.  The reference's own trajectory at this lr swings (saturated sigmoid after
+    step 1, recovery by step ~10: tools/c4_lr_probe.py); the engine must follow it."""
+    import bench
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = bench.CONFIGS["terabyte_qr_rwsadagrad"]
+    rows = [min(r, 20000) for r in c["rows"]]
+    D, bot = c["D"], c["bot"]
+    ln_top = [_num_int(len(rows), D)] + c["top"]
+    B, lr, thr = 256, 1e-3, c["qr"]["threshold"]
+    np.random.seed(0)
+    torch.manual_seed(0)
+    ref = O.OracleDLRM(D, rows, bot, ln_top, loss_function="bce")
+    for k, n in enumerate(rows):
+        if n > thr:
+            ref.emb_l[k] = O.QREmbeddingBagOracle(n, D, 4, "mult")
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=bot, ln_top=ln_top, loss_function="bce",
+                        learning_rate=lr, optimizer="rwsadagrad", qr_flag=True, qr_collisions=4,
+                        qr_operation="mult", qr_threshold=thr)
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    opt = O.RWSAdagradOracle(ref.parameters(), lr=lr)
+    rng = np.random.RandomState(1)
+    losses = []
+    for s in range(10):
+        X, lS_o, lS_i, T = _rand_batch(rng, rows, B, 1, bot[0], "bce")
+        Xt, ot, it, Tt = (torch.tensor(X), torch.tensor(lS_o), [torch.tensor(i) for i in lS_i],
+                          torch.tensor(T))
+        Zr = ref(Xt, ot, it)
+        Er = ref.loss_fn(Zr, Tt)
+        opt.zero_grad()
+        Er.backward()
+        opt.step()
+        Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
+        losses.append((round(E.item(), 4), round(Er.item(), 4)))
+        ok, msg = fp32_close(E.cpu().numpy(), [Er.item()], atol=1e-4)
+        assert ok, (s, losses, msg)
+    print("C4 losses (engine, oracle):", losses)
