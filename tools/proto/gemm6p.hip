@@ -243,6 +243,197 @@ __global__ __launch_bounds__(256, 1) void gemm6p_kernel(const P6 p) {
     }
 }
 
+
+// ---- DMA-ring variant (r03 probe 2): planes go global -> LDS by buffer_load ... lds through
+// an S-stage ring (S-1 K-tiles in flight, no staging registers, no ds_write); swizzled images
+// (tools: bank check in DESIGN) read by ds_read_b128 (KC) / ds_read_b64_tr_b16 (!KC).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff) {
+  const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)lds;
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(a),
+               "v"(voff), "s"(r)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int MN, bool KC>
+struct DI6 {
+  static constexpr int SLOTS = 4 * MN;    // 16-B slots per plane-stage (MN x 32 bf16)
+  static constexpr int BYTES = 16 * SLOTS;
+  static constexpr int CPR = MN / 8;      // !KC: chunks per k-row
+  static constexpr int BLK = SLOTS / 64;  // 1-KiB DMA blocks per plane
+  __device__ __forceinline__ static int swk(int r) { return (r >> 1) & 3; }
+  __device__ __forceinline__ static int swt(int k) {
+    return ((CPR >= 16 ? 2 : 1) * (k ^ (k >> 1))) % CPR;
+  }
+  __device__ __forceinline__ static void src(int slot, int& mn, int& k) {
+    if constexpr (KC) {
+      const int r = slot >> 2;
+      mn = r;
+      k = 8 * ((slot & 3) ^ swk(r));
+    } else {
+      k = slot / CPR;
+      mn = 8 * ((slot % CPR) ^ swt(k));
+    }
+  }
+  // fragment of 16 rows/cols at mn0 for lane (l16, kq): 8 bf16 along k
+  __device__ __forceinline__ static bf16x8 frag(const char* plane, int mn0, int l16, int kq) {
+    if constexpr (KC) {
+      const int r = mn0 + l16;
+      return __builtin_bit_cast(
+          bf16x8, *reinterpret_cast<const uint4*>(plane + 16 * (4 * r + (kq ^ swk(r)))));
+    } else {
+      const int q = l16 >> 2, p = l16 & 3;
+      const int ch = mn0 / 8 + (p >> 1);
+      const int k0 = 8 * kq + q, k1 = k0 + 4;
+      const char* a0 = plane + 16 * (k0 * CPR + (ch ^ swt(k0))) + 8 * (p & 1);
+      const char* a1 = plane + 16 * (k1 * CPR + (ch ^ swt(k1))) + 8 * (p & 1);
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+      using s16x8 = __attribute__((ext_vector_type(8))) short;
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+template <int BM, int BN, bool A_KC, bool B_KC, int S>
+__global__ __launch_bounds__(256, 1) void gemm6d_kernel(const P6 p) {
+  constexpr int WGM = 2, WGN = 2, NW = 4;
+  constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+  using IA = DI6<BM, A_KC>;
+  using IB = DI6<BN, B_KC>;
+  constexpr int STAGE = 3 * (IA::BYTES + IB::BYTES);
+  constexpr int NBA = 3 * IA::BLK, NBB = 3 * IB::BLK;
+  static_assert(NBA % NW == 0 && NBB % NW == 0, "blocks per wave");
+  constexpr int NIA = NBA / NW, NIB = NBB / NW, NI = NIA + NIB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / p.tiles_n, tn = tile - (tile / p.tiles_n) * p.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int wm0 = (wave / WGN) * WM, wn0 = (wave % WGN) * WN;
+  const int64_t a_ext = 2 * p.psa + (A_KC ? p.M * p.lda : p.K * p.lda);
+  const int64_t b_ext = 2 * p.psb + (B_KC ? p.N * p.ldb : p.K * p.ldb);
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)(a_ext * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)(b_ext * 2), 0x00020000);
+  int aoff[NIA], akp[NIA], boff[NIB], bkp[NIB];
+#pragma unroll
+  for (int i = 0; i < NIA; ++i) {
+    const int b = wave * NIA + i;
+    const int q = b / IA::BLK, bb = b % IA::BLK;
+    int mn, k;
+    IA::src(bb * 64 + lane, mn, k);
+    const int64_t g = m0 + mn;
+    aoff[i] = g < p.M ? (int)(2 * (q * p.psa + (A_KC ? g * p.lda + k : (int64_t)k * p.lda + g)))
+                      : -1;
+    akp[i] = k;
+  }
+#pragma unroll
+  for (int i = 0; i < NIB; ++i) {
+    const int b = wave * NIB + i;
+    const int q = b / IB::BLK, bb = b % IB::BLK;
+    int mn, k;
+    IB::src(bb * 64 + lane, mn, k);
+    const int64_t g = n0 + mn;
+    boff[i] = g < p.N ? (int)(2 * (q * p.psb + (B_KC ? g * p.ldb + k : (int64_t)k * p.ldb + g)))
+                      : -1;
+    bkp[i] = k;
+  }
+  const int a_step = A_KC ? 2 * kBK : (int)(2 * kBK * p.lda);
+  const int b_step = B_KC ? 2 * kBK : (int)(2 * kBK * p.ldb);
+  const int K32 = (int)p.K;
+  const int nk = (K32 + kBK - 1) / kBK;
+  auto issue = [&](int t) {
+    char* st = smem + (t % S) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NIA; ++i) {
+      const int b = wave * NIA + i;
+      const bool ok = aoff[i] >= 0 && t * kBK + akp[i] < K32;
+      dma16(ra, st + (b / IA::BLK) * IA::BYTES + (b % IA::BLK) * 1024,
+            ok ? aoff[i] + t * a_step : 0x7ffffff0);
+    }
+#pragma unroll
+    for (int i = 0; i < NIB; ++i) {
+      const int b = wave * NIB + i;
+      const bool ok = boff[i] >= 0 && t * kBK + bkp[i] < K32;
+      dma16(rb, st + 3 * IA::BYTES + (b / IB::BLK) * IB::BYTES + (b % IB::BLK) * 1024,
+            ok ? boff[i] + t * b_step : 0x7ffffff0);
+    }
+  };
+  struct Frag {
+    bf16x8 q[3];
+  };
+  auto read = [&](int t, Frag (&a)[FM], Frag (&b)[FN]) {
+    const char* st = smem + (t % S) * STAGE;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i].q[q] = IA::frag(st + q * IA::BYTES, wm0 + i * 16, l16, kq);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j].q[q] = IB::frag(st + 3 * IA::BYTES + q * IB::BYTES, wn0 + j * 16, l16, kq);
+    }
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto products = [&](int s0, int s1, const Frag (&ca)[FM], const Frag (&cb)[FN]) {
+    constexpr int PA[6] = {0, 2, 1, 0, 1, 0};
+    constexpr int PB[6] = {2, 0, 1, 1, 0, 0};
+#pragma unroll
+    for (int s = s0; s < s1; ++s)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i].q[PA[s]], cb[j].q[PB[s]],
+                                                              acc[i][j], 0, 0, 0);
+  };
+  Frag ca[FM], cb[FN], na[FM], nb[FN];
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t) issue(t);
+  wait_vm<(S - 2) * NI>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read(0, ca, cb);
+  auto step = [&](int t, const Frag (&a)[FM], const Frag (&b)[FN], Frag (&a2)[FM],
+                  Frag (&b2)[FN]) {
+    products(0, 3, a, b);
+    wait_vm<(S - 3) * NI>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(t + S - 1);
+    read(t + 1, a2, b2);
+    products(3, 6, a, b);
+  };
+  for (int t = 0; t < nk; t += 2) {
+    step(t, ca, cb, na, nb);
+    if (t + 1 >= nk) break;
+    step(t + 1, na, nb, ca, cb);
+  }
+  wait_vm<0>();
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t col = n0 + wn0 + j * 16 + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
+        if (row < p.M && col < p.N) p.C[row * p.ldc + col] = p.alpha * acc[i][j][r];
+      }
+    }
+}
+
 // X [rows][cols] fp32 (ld) -> planes [3][rows][ldp] bf16 (plane stride ps), 8 per thread.
 __global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ X,
                                                            int64_t rows, int64_t cols,
@@ -298,9 +489,22 @@ extern "C" int dlrm_x6p_gemm(int32_t layout, int32_t tile, int64_t M, int64_t N,
     else if (layout == 1) hipLaunchKernelGGL((gemm6p_kernel<BM, BN, true, false>), g, dim3(256), 0, st, p); \
     else hipLaunchKernelGGL((gemm6p_kernel<BM, BN, false, false>), g, dim3(256), 0, st, p); \
   } while (0)
+#define GOD(BM, BN, S)                                                                        \
+  do {                                                                                        \
+    p.tiles_n = (int)dlrm::ceil_div(N, BN);                                                   \
+    const dim3 g((unsigned)(dlrm::ceil_div(M, BM) * p.tiles_n));                              \
+    const size_t sm = (size_t)S * 3 * 64 * (BM + BN);                                         \
+    if (layout == 0) { (void)hipFuncSetAttribute((const void*)gemm6d_kernel<BM, BN, true, true, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); hipLaunchKernelGGL((gemm6d_kernel<BM, BN, true, true, S>), g, dim3(256), sm, st, p); } \
+    else if (layout == 1) { (void)hipFuncSetAttribute((const void*)gemm6d_kernel<BM, BN, true, false, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); hipLaunchKernelGGL((gemm6d_kernel<BM, BN, true, false, S>), g, dim3(256), sm, st, p); } \
+    else { (void)hipFuncSetAttribute((const void*)gemm6d_kernel<BM, BN, false, false, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); hipLaunchKernelGGL((gemm6d_kernel<BM, BN, false, false, S>), g, dim3(256), sm, st, p); } \
+  } while (0)
   if (tile == 2) GO(128, 64);
+  else if (tile == 3) GOD(128, 64, 4);
+  else if (tile == 4) GOD(64, 64, 4);
+  else if (tile == 5) GOD(64, 64, 3);
   else GO(64, 64);
 #undef GO
+#undef GOD
   DLRM_LAUNCH_CHECK("dlrm_x6p_gemm");
   return DLRM_OK;
 }

@@ -42,6 +42,10 @@ def planes_of(X):
     return Pl, ldp, r * ldp
 
 
+TILES = (0, 2, 3, 4, 5)
+TNAME = {0: "x6p64x64", 2: "x6p128x64", 3: "dma128x64s4", 4: "dma64x64s4", 5: "dma64x64s3"}
+
+
 def main():
     dev = "cuda"
     torch.manual_seed(0)
@@ -62,7 +66,7 @@ def main():
         Bp, ldb, psb = planes_of(B)
         split_us = timeit(lambda: (planes_of(A), planes_of(B)), n=10) * 1e6
         res = {}
-        for tile in (0, 2):
+        for tile in TILES:
             C = torch.empty(M, N, device=dev)
 
             def go():
@@ -72,7 +76,7 @@ def main():
             go()
             torch.cuda.synchronize()
             err = float(((C.double() - ref).abs() / bound).max())
-            res[f"x6p{'128x64' if tile == 2 else '64x64'}"] = (timeit(go) * 1e6, err)
+            res[TNAME[tile]] = (timeit(go) * 1e6, err)
         Cf = torch.empty(M, N, device=dev)
         ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
 
