@@ -17,6 +17,6 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace dlrm
 
-extern "C" int dlrm_abi_version(void) { return 3; }
+extern "C" int dlrm_abi_version(void) { return 4; }
 
 extern "C" const char* dlrm_last_error(void) { return dlrm::g_last_error; }

@@ -73,6 +73,13 @@ struct GemmParams {
   int pub;           // split-K hand-off: 0 = release/acquire fences, 1 = write-through (sc1)
   int mode;          // DLRM_GEMM_FULL / _PARTIAL (split partials -> part) / _REDUCE
   float* part;       // PARTIAL/REDUCE: [splits][M][N] fp32, then [splits][M] row sums
+  // split-bf16 planes (x6d body): [3][rows][ld] bf16 of the stored A / B / C matrices
+  const __bf16* Ap;
+  int64_t ldap, psa;
+  const __bf16* Bp;
+  int64_t ldbp, psb;
+  __bf16* Cp;        // optional: every epilogue write of C is also split into Cp
+  int64_t ldcp, psc;
 };
 
 struct GemmGroup {
@@ -257,6 +264,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// v -> three bf16 planes at Cp (v = h + m + l exactly: round to nearest at each level).
+__device__ __forceinline__ void store_planes(const GemmParams& p, int64_t row, int64_t col,
+                                             float v) {
+  const __bf16 h = (__bf16)v;
+  const float r = v - (float)h;
+  const __bf16 m = (__bf16)r;
+  const __bf16 l = (__bf16)(r - (float)m);
+  __bf16* d = p.Cp + row * p.ldcp + col;
+  d[0] = h;
+  d[p.psc] = m;
+  d[2 * p.psc] = l;
+}
+
 // C = epilogue(v) where v = alpha * acc (already scaled).
 __device__ __forceinline__ void apply_epilogue(const GemmParams& p, int64_t row, int64_t col,
                                                float v) {
@@ -284,6 +304,7 @@ __device__ __forceinline__ void apply_epilogue(const GemmParams& p, int64_t row,
       break;
   }
   *cp = v;
+  if (p.Cp) store_planes(p, row, col, v);
 }
 
 
@@ -1476,6 +1497,241 @@ __device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
   }
 }
 
+// -------------------------------------------------- pre-split split-bf16 body (x6d) --
+// The fp32 GEMM on the bf16 matrix core from operands that arrive ALREADY split into
+// their (h, m, l) bf16 planes (dlrm_gemm_problem.a_planes / b_planes; the producing GEMM
+// writes them in its epilogue, c_planes): no conversion in the main loop.  Plane panels
+// go global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave instruction)
+// through an S-stage ring, S - 1 K-tiles in flight; one barrier per 32-deep K-tile, the
+// fragments of tile t+1 read under the second half of tile t's six products
+// (v_mfma_f32_16x16x32_bf16: hh, hm, mh, hl, lh, mm; the map of pipe_body6).
+// LDS images, one per plane and stage (bank maps checked offline for every fragment read:
+// conflict-free):
+//   KC  (MN x 32, k-contiguous):  16-B chunk c of row r in slot 4r + (c ^ ((r >> 1) & 3)),
+//        fragments by ds_read_b128;
+//   !KC (32 x MN, mn-contiguous): chunk c of k-row k in slot k(MN/8) + (c ^ f(k)),
+//        f(k) = (MN/8 >= 16 ? 2 : 1)(k ^ (k >> 1)) mod MN/8, fragments by two
+//        ds_read_b64_tr_b16 (hardware transpose).
+// 128x64 tiles run 4 stages (144 KiB: one workgroup per CU), 64x64 tiles 3 (72 KiB: two).
+template <int MN, bool KC>
+struct PImg {
+  static constexpr int SLOTS = 4 * MN;  // 16-B slots per plane and stage (MN x 32 bf16)
+  static constexpr int BYTES = 16 * SLOTS;
+  static constexpr int CPR = MN / 8;    // !KC: chunks per k-row
+  static constexpr int BLK = SLOTS / 64;  // 1-KiB DMA blocks per plane
+  __device__ __forceinline__ static int swk(int r) { return (r >> 1) & 3; }
+  __device__ __forceinline__ static int swt(int k) {
+    return ((CPR >= 16 ? 2 : 1) * (k ^ (k >> 1))) % CPR;
+  }
+  // (mn, k) of the 16-B chunk that fills slot `slot` (k: first of its 8 k, KC; the k-row, !KC)
+  __device__ __forceinline__ static void src(int slot, int& mn, int& k) {
+    if constexpr (KC) {
+      const int r = slot >> 2;
+      mn = r;
+      k = 8 * ((slot & 3) ^ swk(r));
+    } else {
+      k = slot / CPR;
+      mn = 8 * ((slot % CPR) ^ swt(k));
+    }
+  }
+  // 8 bf16 along k of row / column mn0 + l16 (lane group kq holds k = 8kq .. 8kq+7)
+  __device__ __forceinline__ static bf16x8 frag(const char* plane, int mn0, int l16, int kq) {
+    if constexpr (KC) {
+      const int r = mn0 + l16;
+      return __builtin_bit_cast(
+          bf16x8, *reinterpret_cast<const uint4*>(plane + 16 * (4 * r + (kq ^ swk(r)))));
+    } else {
+      const int q = l16 >> 2, pp = l16 & 3;
+      const int ch = mn0 / 8 + (pp >> 1);
+      const int k0 = 8 * kq + q, k1 = k0 + 4;
+      const char* a0 = plane + 16 * (k0 * CPR + (ch ^ swt(k0))) + 8 * (pp & 1);
+      const char* a1 = plane + 16 * (k1 * CPR + (ch ^ swt(k1))) + 8 * (pp & 1);
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+      using s16x8 = __attribute__((ext_vector_type(8))) short;
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+template <int BM, int BN>
+constexpr int x6d_stages() {
+  return BM * BN > 4096 ? 4 : 3;
+}
+template <int BM, int BN>
+constexpr int x6d_smem_bytes() {
+  return x6d_stages<BM, BN>() * 3 * 64 * (BM + BN);
+}
+
+// Sum of the 8 bf16 of a fragment (exact bf16 -> f32 widening, fixed order).
+__device__ __forceinline__ float frag_sum(const bf16x8& f) {
+  const uint4 u = __builtin_bit_cast(uint4, f);
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s = add_f32(s, __builtin_bit_cast(float, w[i] << 16));
+    s = add_f32(s, __builtin_bit_cast(float, w[i] & 0xffff0000u));
+  }
+  return s;
+}
+
+template <int BM, int BN, bool A_KC, bool B_KC, bool RS>
+__device__ __forceinline__ void pipe_body_x6d(const GemmParams& p, int lb, char* smem) {
+  constexpr int S = x6d_stages<BM, BN>();
+  constexpr int WGM = 2, WGN = 2, NW = 4;
+  constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+  using IA = PImg<BM, A_KC>;
+  using IB = PImg<BN, B_KC>;
+  constexpr int STAGE = 3 * (IA::BYTES + IB::BYTES);
+  constexpr int NBA = 3 * IA::BLK, NBB = 3 * IB::BLK;
+  static_assert(NBA % NW == 0 && NBB % NW == 0, "DMA blocks per wave");
+  constexpr int NIA = NBA / NW, NIB = NBB / NW, NI = NIA + NIB;
+
+  const int tile = lb / p.splits;
+  const int split = lb - tile * p.splits;
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t K8 = (p.K + 7) / 8 * 8;
+  const int64_t kbeg = (int64_t)split * p.kchunk;
+  const int64_t kend = (kbeg + p.kchunk < K8) ? kbeg + p.kchunk : K8;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int wm0 = (wave / WGN) * WM, wn0 = (wave % WGN) * WN;
+  const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
+
+  const int64_t a_ext = 2 * p.psa + (A_KC ? p.M * p.ldap : K8 * p.ldap);
+  const int64_t b_ext = 2 * p.psb + (B_KC ? p.N * p.ldbp : K8 * p.ldbp);
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.Ap, (short)0, (int)(a_ext * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.Bp, (short)0, (int)(b_ext * 2), 0x00020000);
+  // per DMA instruction of this wave: byte offset at the split's first K-tile (-1: row /
+  // column outside the operand) and the chunk's k within a K-tile
+  int aoff[NIA], akp[NIA], boff[NIB], bkp[NIB];
+#pragma unroll
+  for (int i = 0; i < NIA; ++i) {
+    const int b = wave * NIA + i;
+    const int q = b / IA::BLK, bb = b - q * IA::BLK;
+    int mn, k;
+    IA::src(bb * 64 + lane, mn, k);
+    const int64_t g = m0 + mn, gk = kbeg + k;
+    aoff[i] = g < p.M ? (int)(2 * (q * p.psa + (A_KC ? g * p.ldap + gk : gk * p.ldap + g))) : -1;
+    akp[i] = k;
+  }
+#pragma unroll
+  for (int i = 0; i < NIB; ++i) {
+    const int b = wave * NIB + i;
+    const int q = b / IB::BLK, bb = b - q * IB::BLK;
+    int mn, k;
+    IB::src(bb * 64 + lane, mn, k);
+    const int64_t g = n0 + mn, gk = kbeg + k;
+    boff[i] = g < p.N ? (int)(2 * (q * p.psb + (B_KC ? g * p.ldbp + gk : gk * p.ldbp + g))) : -1;
+    bkp[i] = k;
+  }
+  const int a_step = A_KC ? 2 * kBK : (int)(2 * kBK * p.ldap);
+  const int b_step = B_KC ? 2 * kBK : (int)(2 * kBK * p.ldbp);
+  const int krem = (int)(kend - kbeg);
+  // DMA of K-tile t into stage t % S; chunks past the split's K range (and tiles t >= nk)
+  // load zeros (out-of-descriptor offset), so every wave issues the same count
+  auto issue = [&](int t) {
+    char* st = smem + (t % S) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NIA; ++i) {
+      const int b = wave * NIA + i;
+      const bool ok = aoff[i] >= 0 && t * kBK + akp[i] < krem;
+      dma16(ra, reinterpret_cast<const float*>(st + (b / IA::BLK) * IA::BYTES +
+                                               (b % IA::BLK) * 1024),
+            ok ? aoff[i] + t * a_step : 0x7ffffff0);
+    }
+#pragma unroll
+    for (int i = 0; i < NIB; ++i) {
+      const int b = wave * NIB + i;
+      const bool ok = boff[i] >= 0 && t * kBK + bkp[i] < krem;
+      dma16(rb, reinterpret_cast<const float*>(st + 3 * IA::BYTES + (b / IB::BLK) * IB::BYTES +
+                                               (b % IB::BLK) * 1024),
+            ok ? boff[i] + t * b_step : 0x7ffffff0);
+    }
+  };
+  struct Frag {
+    bf16x8 q[3];
+  };
+  auto read = [&](int t, Frag (&a)[FM], Frag (&b)[FN]) {
+    const char* st = smem + (t % S) * STAGE;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i].q[q] = IA::frag(st + q * IA::BYTES, wm0 + i * 16, l16, kq);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j].q[q] = IB::frag(st + 3 * IA::BYTES + q * IB::BYTES, wn0 + j * 16, l16, kq);
+    }
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rs[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) rs[i] = 0.f;
+  auto products = [&](int s0, int s1, const Frag (&ca)[FM], const Frag (&cb)[FN]) {
+    constexpr int PA[6] = {0, 2, 1, 0, 1, 0};  // (a, b) planes: hl, lh, mm, hm, mh, hh
+    constexpr int PB[6] = {2, 0, 1, 1, 0, 0};
+#pragma unroll
+    for (int s = s0; s < s1; ++s)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i].q[PA[s]], cb[j].q[PB[s]],
+                                                              acc[i][j], 0, 0, 0);
+  };
+  auto rowsums = [&](const Frag (&ca)[FM]) {
+    if constexpr (RS) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        rs[i] = add_f32(rs[i], add_f32(add_f32(frag_sum(ca[i].q[0]), frag_sum(ca[i].q[1])),
+                                       frag_sum(ca[i].q[2])));
+    }
+  };
+  Frag ca[FM], cb[FN], na[FM], nb[FN];
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t) issue(t);
+  wait_vm<(S - 2) * NI>();       // tile 0 landed (this wave)
+  __builtin_amdgcn_s_barrier();  // (a bare barrier: __syncthreads' fence would drain the DMAs)
+  asm volatile("" ::: "memory");
+  read(0, ca, cb);
+  auto step = [&](int t, const Frag (&a)[FM], const Frag (&b)[FN], Frag (&a2)[FM],
+                  Frag (&b2)[FN]) {
+    products(0, 3, a, b);
+    wait_vm<(S - 3) * NI>();       // tile t+1 landed (this wave)
+    __builtin_amdgcn_s_barrier();  // every wave's has; every wave is done with tile t-1's stage
+    asm volatile("" ::: "memory");
+    issue(t + S - 1);  // into tile t-1's stage
+    read(t + 1, a2, b2);
+    products(3, 6, a, b);
+    rowsums(a);
+  };
+  for (int t = 0; t < nk; t += 2) {
+    step(t, ca, cb, na, nb);
+    if (t + 1 >= nk) break;
+    step(t + 1, na, nb, ca, cb);
+  }
+  wait_vm<0>();  // the trailing DMAs land before smem is reused or released
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    rs[i] += __shfl_xor(rs[i], 16, 64);
+    rs[i] += __shfl_xor(rs[i], 32, 64);
+  }
+  finish_tile<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0,
+                                    reinterpret_cast<float*>(smem));
+}
+
 template <int BM, int BN>
 constexpr int group_smem_floats() {
   // the largest LDS image over the four operand layouts (double-buffered A and B panels)
@@ -1598,6 +1854,57 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_group6L_kernel(const G
     if (kind == 3) return pipe_body6L<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
   if constexpr ((KINDS & 16) != 0)
     if (kind == 4) return pipe_body6L<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
+}
+
+// The same grouped launch on the pre-split body (pipe_body_x6d): LDS from the dynamic
+// segment (up to 144 KiB), one workgroup per CU at 128x64, two at 64x64.
+template <int BM, int BN, int KINDS>
+__global__ __launch_bounds__(256, 1) void gemm_group6d_kernel(const GemmGroup g) {
+  extern __shared__ __attribute__((aligned(1024))) char smem6d[];
+  const int b = blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxGroup; ++i)
+    if (i < g.n && b >= g.p[i].block0) q = i;
+  const GemmParams& p = g.p[q];
+  const int nq = (q + 1 < g.n ? g.p[q + 1].block0 : g.total) - p.block0;
+  const int lb = xcd_remap(b - p.block0, nq);
+  if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
+  const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
+  if constexpr ((KINDS & 1) != 0)
+    if (kind == 0) return pipe_body_x6d<BM, BN, true, true, false>(p, lb, smem6d);
+  if constexpr ((KINDS & 2) != 0)
+    if (kind == 1) return pipe_body_x6d<BM, BN, true, false, false>(p, lb, smem6d);
+  if constexpr ((KINDS & 4) != 0)
+    if (kind == 2) return pipe_body_x6d<BM, BN, false, false, false>(p, lb, smem6d);
+  if constexpr ((KINDS & 8) != 0)
+    if (kind == 3) return pipe_body_x6d<BM, BN, false, true, false>(p, lb, smem6d);
+  if constexpr ((KINDS & 16) != 0)
+    if (kind == 4) return pipe_body_x6d<BM, BN, false, false, true>(p, lb, smem6d);
+}
+
+// X [rows][cols] fp32 -> planes [3][rows][ldp] bf16, 8 elements per thread (columns
+// [cols, ldp) untouched).
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ X,
+                                                           int64_t rows, int64_t cols, int64_t ld,
+                                                           __bf16* __restrict__ P, int64_t ldp,
+                                                           int64_t ps) {
+  const int64_t c8 = (cols + 7) / 8;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * c8) return;
+  const int64_t r = i / c8, c = 8 * (i - r * c8);
+  __bf16* dst = P + r * ldp + c;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (c + u >= cols) break;
+    const float v = X[r * ld + c + u];
+    const __bf16 h = (__bf16)v;
+    const float rr = v - (float)h;
+    const __bf16 m = (__bf16)rr;
+    dst[u] = h;
+    dst[u + ps] = m;
+    dst[u + 2 * ps] = (__bf16)(rr - (float)m);
+  }
 }
 
 // Fallback for operands the pipelined body cannot take (unaligned rows, ragged float4
@@ -1734,6 +2041,12 @@ struct Desc {  // one problem as the host sees it
   int32_t mode = DLRM_GEMM_FULL;
   int32_t splits = 0;
   float* part = nullptr;
+  const __bf16* Ap = nullptr;  // split-bf16 planes (dlrm_gemm_problem.a/b/c_planes)
+  int64_t ldap = 0, psa = 0;
+  const __bf16* Bp = nullptr;
+  int64_t ldbp = 0, psb = 0;
+  __bf16* Cp = nullptr;
+  int64_t ldcp = 0, psc = 0;
 };
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1751,6 +2064,25 @@ bool pipe_ok(const Desc& d) {
 int layout_of(const Desc& d) {
   const bool a_kc = !d.trans_a, b_kc = d.trans_b != 0;
   return a_kc ? (b_kc ? 0 : 1) : (b_kc ? 3 : 2);
+}
+
+// The pre-split body (pipe_body_x6d) takes a problem when both operands come with planes
+// in whole 16-B chunks: pitches and plane strides % 8 (bf16), 16-B aligned bases, an
+// mn-contiguous operand's extent % 8 and its K % 8 (its k-rows are read in 8-row chunks),
+// 32-bit byte offsets.  DLRM_GEMM_PLANES=0 ignores the planes (A/B; read per call).
+bool planes_ok(const Desc& d) {
+  if (!d.Ap || !d.Bp || d.mode == DLRM_GEMM_REDUCE) return false;
+  const char* v = getenv("DLRM_GEMM_PLANES");
+  if (v && strcmp(v, "0") == 0) return false;
+  const bool a_kc = !d.trans_a, b_kc = d.trans_b != 0;
+  const int64_t K8 = (d.K + 7) / 8 * 8;
+  auto ok = [&](const __bf16* P, int64_t ld, int64_t ps, bool kc, int64_t mn) {
+    const int64_t ext = 2 * ps + (kc ? mn * ld : K8 * ld);
+    return aligned16(P) && ld % 8 == 0 && ps % 8 == 0 && ps >= 0 &&
+           (kc ? ld >= K8 : (mn % 8 == 0 && d.K % 8 == 0 && ld >= mn)) &&
+           ext * 2 < 0x7ff00000LL;
+  };
+  return d.K > 0 && ok(d.Ap, d.ldap, d.psa, a_kc, d.M) && ok(d.Bp, d.ldbp, d.psb, b_kc, d.N);
 }
 
 struct PlanEntry {
@@ -1780,7 +2112,7 @@ bool tile_ok(int bm, int bn, int wm, int wn) {
 
 struct Tile {
   int bm = 64, bn = 32, wm = 2, wn = 2;
-  int x6 = 0;   // math vote of a problem / the launch's math
+  int x6 = 0;   // math vote of a problem / the launch's math (3: pre-split planes, x6d)
   int dma = 0;  // f32 body vote of a problem / the launch's body (1: LDS-DMA)
   bool operator==(const Tile& o) const {
     return bm == o.bm && bn == o.bn && wm == o.wm && wn == o.wn;
@@ -1817,6 +2149,26 @@ void x6l_override(const Desc& d, Tile& t, Plan& pl) {
   pl = make_plan(s, d.K);
 }
 
+// Pre-split problems: 128x64 tiles when they fill the CUs once (>= 240 tiles), else 64x64;
+// K split until >= 256 blocks with K chunks >= 256 (PARTIAL: the caller's count, if any).
+void plan_x6d(const Desc& d, Tile& t, Plan& pl) {
+  const int64_t t128 = dlrm::ceil_div(d.M, 128) * dlrm::ceil_div(d.N, 64);
+  t = t128 >= 240 ? Tile{128, 64, 2, 2, 3} : Tile{64, 64, 2, 2, 3};
+  if (d.mode == DLRM_GEMM_PARTIAL && d.splits > 0) {
+    pl = make_plan(d.splits, d.K);
+    return;
+  }
+  const int force_split = env_int("DLRM_GEMM_SPLIT", 0);  // (A/B sweeps)
+  if (force_split > 0) {
+    pl = make_plan(force_split, d.K);
+    return;
+  }
+  const int64_t tiles = dlrm::ceil_div(d.M, t.bm) * dlrm::ceil_div(d.N, t.bn);
+  int64_t s = 1;
+  while (tiles * s < 256 && dlrm::ceil_div(d.K, s + 1) >= 256 && s < kMaxSplit) ++s;
+  pl = make_plan(s, d.K);
+}
+
 void plan_one(const Desc& d, Tile& t, Plan& pl) {
   t = Tile{64, 64, 2, 2};
   if (d.mode == DLRM_GEMM_REDUCE) {  // elementwise job: no tiles, no K
@@ -1824,6 +2176,7 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
     pl.kchunk = 0;
     return;
   }
+  if (planes_ok(d)) return plan_x6d(d, t, pl);
   if (d.mode == DLRM_GEMM_PARTIAL && d.splits > 0) {  // caller-sized partial buffer
     Desc q = d;
     q.mode = DLRM_GEMM_FULL;
@@ -1869,7 +2222,7 @@ void plan_one(const Desc& d, Tile& t, Plan& pl) {
 void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   bool first = true;
   t = Tile{64, 64, 2, 2};
-  int votes = 0, gemms = 0, dvotes = 0, lvotes = 0;
+  int votes = 0, gemms = 0, dvotes = 0, lvotes = 0, pvotes = 0;
   for (int i = 0; i < n; ++i) {
     Tile a;
     plan_one(d[i], a, pl[i]);
@@ -1877,6 +2230,7 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
     ++gemms;
     votes += a.x6 == 1;
     lvotes += a.x6 == 2;
+    pvotes += a.x6 == 3;
     dvotes += a.dma;
     if (first) {
       t = a;
@@ -1885,6 +2239,21 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
       t = Tile{64, 32, 2, 2};
     }
   }
+  if (gemms > 0 && pvotes == gemms) {  // every GEMM has planes: the pre-split body
+    t.x6 = 3;
+    if (!(t.bm == 128 && t.bn == 64)) t = Tile{64, 64, 2, 2, 3};
+    return;
+  }
+  if (pvotes > 0)  // mixed: the f32 body for all (pre-split problems re-planned for it)
+    for (int i = 0; i < n; ++i)
+      if (d[i].mode != DLRM_GEMM_REDUCE && planes_ok(d[i])) {
+        Desc q = d[i];
+        q.Ap = q.Bp = nullptr;
+        Tile a;
+        Plan keep = pl[i];
+        plan_one(q, a, pl[i]);
+        if (d[i].mode == DLRM_GEMM_PARTIAL) pl[i] = keep;  // the REDUCE repeats this count
+      }
   const int env = gemm_math_env();
   // 128x128 split-bf16 only when every GEMM of the launch asks for it (their tiles agree)
   t.x6 = gemms > 0 && lvotes == gemms ? 2 : env == 1 ? 1 : env == 0 ? 0
@@ -1911,7 +2280,7 @@ size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
 
 // Body of a launch: kBodyReg (register-staged f32 pipe_body), kBodyX6 (split-bf16),
 // kBodyDma (LDS-DMA f32 pipe_body_dma, where the plan asks for it).
-constexpr int kBodyReg = 0, kBodyX6 = 1, kBodyDma = 2, kBodyX6L = 3;
+constexpr int kBodyReg = 0, kBodyX6 = 1, kBodyDma = 2, kBodyX6L = 3, kBodyX6D = 4;
 
 // f32 body of a launch: the plan's vote, or DLRM_GEMM_BODY=reg / dma everywhere (A/B; read
 // per call).
@@ -1920,6 +2289,21 @@ int f32_body(int plan_dma) {
   if (v && strcmp(v, "reg") == 0) return kBodyReg;
   if (v && strcmp(v, "dma") == 0) return kBodyDma;
   return plan_dma ? kBodyDma : kBodyReg;
+}
+
+template <int BM, int BN>
+int launch_x6d_all(const GemmGroup& g, hipStream_t st) {
+  constexpr int SM = x6d_smem_bytes<BM, BN>();
+  static bool attr = false;
+  if (!attr) {
+    DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, 31>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SM),
+                  "dlrm_gemm_f32 (x6d)");
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, 31>), dim3(g.total), dim3(256), SM, st, g);
+  DLRM_LAUNCH_CHECK("dlrm_gemm_f32 (x6d)");
+  return DLRM_OK;
 }
 
 template <int BM, int BN, int BODY = kBodyDma, int WGM = 2, int WGN = 2>
@@ -1941,6 +2325,9 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
     p.pub = pub;
     p.mode = d[i].mode;
     p.part = d[i].part;
+    p.Ap = d[i].Ap, p.ldap = d[i].ldap, p.psa = d[i].psa;
+    p.Bp = d[i].Bp, p.ldbp = d[i].ldbp, p.psb = d[i].psb;
+    p.Cp = d[i].Cp, p.ldcp = d[i].ldcp, p.psc = d[i].psc;
     p.tiles_m = (int)dlrm::ceil_div(p.M, BM);
     p.tiles_n = (int)dlrm::ceil_div(p.N, BN);
     p.splits = pl[i].splits;
@@ -1970,7 +2357,27 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
   // row sums, two wgrads), else all kinds
-  if constexpr (BODY == kBodyX6L) {
+  if constexpr (BODY == kBodyX6D) {
+    constexpr int SM = x6d_smem_bytes<BM, BN>();
+#define K_(M_)                                                                              \
+  case M_: {                                                                               \
+    static bool attr = false;                                                              \
+    if (!attr) {                                                                           \
+      DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, M_>,      \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, SM),   \
+                    "dlrm_gemm_f32 (x6d)");                                                \
+      attr = true;                                                                         \
+    }                                                                                      \
+    hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, M_>), grid, block, SM, st, g);         \
+    break;                                                                                 \
+  }
+    switch (kinds) {
+      K_(0) K_(1) K_(2) K_(4) K_(16) K_(2 | 16) K_(2 | 4)
+      default:
+        return launch_x6d_all<BM, BN>(g, st);
+    }
+#undef K_
+  } else if constexpr (BODY == kBodyX6L) {
     switch (kinds) {
 #define K_(M_)                                                                            \
   case M_:                                                                               \
@@ -2067,6 +2474,8 @@ int check_desc(const Desc& d) {
              "dlrm_gemm_f32: PARTIAL splits=%d is not a normalized count for K=%lld "
              "(use dlrm_gemm_f32_splits)", (int)d.splits, (long long)d.K);
   }
+  DLRM_ARG(!d.Cp || (d.ldcp >= d.ldc && d.psc >= 0),
+           "dlrm_gemm_f32: c_planes need ldc_planes >= ldc");
   DLRM_ARG(d.M >= 0 && d.N >= 0 && d.K >= 0, "dlrm_gemm_f32: negative size");
   if (d.M == 0 || (d.N == 0 && d.ones_col < 0)) return DLRM_OK;
   DLRM_ARG(d.C, "dlrm_gemm_f32: null C");
@@ -2126,6 +2535,10 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
     for (int i = 0; i < m; ++i)
       if (q[i].mode == DLRM_GEMM_FULL) pl[i] = make_plan(1, q[i].K);
   }
+  if (t.x6 == 3) {  // pre-split planes
+    if (t.bm == 128) return launch_group<128, 64, kBodyX6D>(m, q, pl, ws, ws_bytes, st);
+    return launch_group<64, 64, kBodyX6D>(m, q, pl, ws, ws_bytes, st);
+  }
   // 128x128 split-bf16 on 2x4 waves (64x32 per wave, two waves per SIMD; the 2x2 layout,
   // one wave per SIMD, measured 1.15x slower: profiles/r03_x6l_ab.txt)
   if (t.x6 == 2) return launch_group<128, 128, kBodyX6L, 2, 4>(m, q, pl, ws, ws_bytes, st);
@@ -2157,6 +2570,9 @@ Desc desc_of(const dlrm_gemm_problem& g) {
   d.C = g.C, d.ldc = g.ldc, d.epi = g.epilogue, d.bias = g.bias;
   d.aux = g.aux, d.ldaux = g.ld_aux, d.ones_col = g.ones_col;
   d.mode = g.mode, d.splits = g.splits, d.part = g.partial;
+  d.Ap = static_cast<const __bf16*>(g.a_planes), d.ldap = g.lda_planes, d.psa = g.a_plane_stride;
+  d.Bp = static_cast<const __bf16*>(g.b_planes), d.ldbp = g.ldb_planes, d.psb = g.b_plane_stride;
+  d.Cp = static_cast<__bf16*>(g.c_planes), d.ldcp = g.ldc_planes, d.psc = g.c_plane_stride;
   return d;
 }
 
@@ -2218,4 +2634,20 @@ extern "C" int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem) {
 extern "C" size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits) {
   if (M <= 0 || N <= 0 || splits <= 0) return 0;
   return (size_t)splits * (size_t)(M * N + M) * sizeof(float);
+}
+
+extern "C" int dlrm_split_planes(const float* X, int64_t rows, int64_t cols, int64_t ld,
+                                 void* planes, int64_t ld_planes, int64_t plane_stride,
+                                 dlrm_stream_t stream) {
+  DLRM_ARG(rows >= 0 && cols >= 0 && ld >= cols && ld_planes % 8 == 0 && ld_planes >= cols &&
+               plane_stride >= 0,
+           "dlrm_split_planes: bad sizes");
+  const int64_t n = rows * ((cols + 7) / 8);
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(X && planes, "dlrm_split_planes: null pointer");
+  hipLaunchKernelGGL(split_planes_kernel, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0,
+                     dlrm::as_stream(stream), X, rows, cols, ld, static_cast<__bf16*>(planes),
+                     ld_planes, plane_stride);
+  DLRM_LAUNCH_CHECK("dlrm_split_planes");
+  return DLRM_OK;
 }

@@ -20,10 +20,10 @@
 // Skewed rows (the 3- and 4-row Terabyte tables receive ~700 lookups per row per
 // batch) are thus split over many lane-groups instead of serialising one of them, and
 // the summation order is fixed by the sort: bitwise reproducible run to run.
-#include <hipcub/hipcub.hpp>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 
 #include "mlp_rows.hpp"
 #include "tbe_common.hpp"
@@ -807,6 +807,8 @@ struct TiledPass {
   uint32_t* hist;       // [T][2^DB][J]
   uint32_t sentinel;    // global sentinel key (last pass)
   int32_t* err;
+  int global;           // one segment [0, n_all) of global keys read from kin/pin in pass 0
+  int64_t n_all;
 };
 
 template <int DB>
@@ -831,7 +833,7 @@ __device__ __forceinline__ void tiled_load(const TiledPass& a, const IdxT* __res
     const int64_t e = (int64_t)j * kTile + w * (kTileItems * 64) + u * 64 + l;
     ok[u] = e < n;
     const int64_t p = s + (ok[u] ? e : 0);
-    if (a.first) {
+    if (a.first && !a.global) {
       const int64_t r = (int64_t)idx[p];
       key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
       pos[u] = (int32_t)p;
@@ -845,6 +847,11 @@ __device__ __forceinline__ void tiled_load(const TiledPass& a, const IdxT* __res
 template <typename OffT>
 __device__ __forceinline__ bool tiled_range(const TiledPass& a, const OffT* __restrict__ off, int t,
                                             int64_t& s, int64_t& n) {
+  if (a.global) {
+    s = 0;
+    n = a.n_all;
+    return n <= (int64_t)a.J * kTile;
+  }
   s = (int64_t)off[(int64_t)t * a.B];
   n = (int64_t)off[(int64_t)(t + 1) * a.B] - s;
   return n <= (int64_t)a.J * kTile;  // false: the table overflows its tiles
@@ -1060,7 +1067,7 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scatter_kernel(
     const uint32_t k = sm.key[i];
     const uint32_t d = (k >> a.shift) & (NB - 1);
     const int64_t dst = s + h[d] + (i - sm.dstart[d]);
-    if (a.last)
+    if (a.last && !a.global)
       a.kout[dst] = k < (uint32_t)nrows ? (uint32_t)(rb + k) : a.sentinel;
     else
       a.kout[dst] = k;
@@ -1105,6 +1112,41 @@ void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base
   }
 }
 
+// The device-wide sort (no max_lookups_per_table bound): the tiled passes over ONE segment,
+// the whole lookup array [0, N), of global keys (row_base[t] + row; sentinel for invalid
+// and outside-bag lookups, written with their positions by the keys kernel into (k_x,
+// p_x)).  Passes ping-pong between (k_x, p_x) and (k_y, p_y); returns true when the sorted
+// pairs end in (k_y, p_y).  Stable: equal keys stay in position order, as a stable
+// device-wide radix sort leaves them.
+template <typename IdxT, typename OffT, int DB>
+bool launch_global_sort(const IdxT* idx, const OffT* off, const int64_t* row_base, int64_t N,
+                        int bits, uint32_t* k_x, int32_t* p_x, uint32_t* k_y, int32_t* p_y,
+                        uint32_t* hist, uint32_t sentinel, int32_t* err, hipStream_t st) {
+  const int npass = (bits + DB - 1) / DB;
+  TiledPass a{};
+  a.row_base = row_base, a.T = 1, a.B = 1, a.hist = hist, a.sentinel = sentinel, a.err = err;
+  a.J = (int)dlrm::ceil_div(N, (int64_t)kTile);
+  a.global = 1;
+  a.n_all = N;
+  for (int ps = 0; ps < npass; ++ps) {
+    const bool fwd = (ps & 1) == 0;  // x -> y on even passes
+    a.shift = ps * DB;
+    a.first = ps == 0;
+    a.last = ps == npass - 1;
+    a.kin = fwd ? k_x : k_y;
+    a.pin = fwd ? p_x : p_y;
+    a.kout = fwd ? k_y : k_x;
+    a.pout = fwd ? p_y : p_x;
+    hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(a.J), dim3(kTileThreads), 0,
+                       st, idx, off, a);
+    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(1), dim3(kTileThreads), 0, st, a,
+                       static_cast<const void*>(off), (int)sizeof(OffT) * 8);
+    hipLaunchKernelGGL((tbe_tiled_scatter_kernel<IdxT, OffT, DB>), dim3(a.J), dim3(kTileThreads),
+                       0, st, idx, off, a);
+  }
+  return (npass & 1) == 1;
+}
+
 template <typename KeyT>
 struct BwdWs {
   KeyT* keys_in;
@@ -1112,9 +1154,7 @@ struct BwdWs {
   int32_t* pos_in;
   int32_t* pos_out;
   int32_t* bag_of;
-  float* partial;
-  void* temp;
-  size_t temp_bytes;
+  float* partial;  // block partials; the sorts' digit histograms before the block kernel
   size_t total;
 };
 
@@ -1127,13 +1167,10 @@ BwdWs<KeyT> carve_bwd_ws(void* base, int64_t N, int64_t D, int end_bit) {
   w.pos_in = c.take<int32_t>(N);
   w.pos_out = c.take<int32_t>(N);
   w.bag_of = c.take<int32_t>(N);
-  w.partial = c.take<float>((size_t)2 * ((N + CH - 1) / CH) * D);
-  size_t s1 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s1, (KeyT*)nullptr, (KeyT*)nullptr,
-                                           (int32_t*)nullptr, (int32_t*)nullptr, (int)N, 0,
-                                           end_bit);
-  w.temp_bytes = s1 + 256;
-  w.temp = c.take<char>(w.temp_bytes);
+  (void)end_bit;
+  const size_t part = (size_t)2 * ((N + CH - 1) / CH) * D;
+  const size_t hist = (size_t)((N + kTile - 1) / kTile) * 1024;  // global sort, 10-bit digits
+  w.partial = c.take<float>(part > hist ? part : hist);
   w.total = c.used + 256;
   return w;
 }
@@ -1154,7 +1191,7 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   // block kernel's partial buffer (free until the sort is done)
   const int64_t tiles_j = dlrm::ceil_div(max_seg > 0 ? max_seg : 1, (int64_t)kTile);
   const int tdb = tiled_digit_bits(end_bit);
-  const char* tenv = getenv("DLRM_TBE_TILED_SORT");  // "0": device-wide sort (A/B only)
+  const char* tenv = getenv("DLRM_TBE_TILED_SORT");  // "0": global sort (A/B only)
   const bool tiled = !per_table && sizeof(KeyT) == 4 && max_seg > kSegCap &&
                      N < (int64_t)0x7fffffff && (int64_t)T * tiles_j < (int64_t)INT32_MAX &&
                      (int64_t)T * tiles_j * (1 << tdb) <=
@@ -1200,10 +1237,23 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
                        static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_in,
                        w.pos_in, w.bag_of, err);
     DLRM_LAUNCH_CHECK(name);
-    size_t tb = w.temp_bytes;
-    DLRM_HIP_CALL(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in,
-                                                     w.pos_out, (int)N, 0, end_bit, st),
-                  name);
+    auto* ki = reinterpret_cast<uint32_t*>(w.keys_in);
+    auto* ko = reinterpret_cast<uint32_t*>(w.keys_out);
+    auto* hist = reinterpret_cast<uint32_t*>(w.partial);
+    const bool in_y =
+        tdb == 10 ? launch_global_sort<IdxT, OffT, 10>(static_cast<const IdxT*>(idx),
+                                                       static_cast<const OffT*>(off), row_base, N,
+                                                       end_bit, ki, w.pos_in, ko, w.pos_out, hist,
+                                                       (uint32_t)sentinel, err, st)
+                  : launch_global_sort<IdxT, OffT, 8>(static_cast<const IdxT*>(idx),
+                                                      static_cast<const OffT*>(off), row_base, N,
+                                                      end_bit, ki, w.pos_in, ko, w.pos_out, hist,
+                                                      (uint32_t)sentinel, err, st);
+    DLRM_LAUNCH_CHECK(name);
+    if (!in_y) {  // an even pass count left the sorted pairs in the input buffers
+      std::swap(w.keys_in, w.keys_out);
+      std::swap(w.pos_in, w.pos_out);
+    }
   }
 
   const bool vec4 = (D % 4 == 0) &&
@@ -1286,21 +1336,17 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
   DLRM_ARG(gbs >= (int64_t)T * D, "%s: grad_batch_stride < T*D", name);
   DLRM_ARG(ws || N == 0, "%s: null workspace", name);
   hipStream_t st = dlrm::as_stream(stream);
-  const bool k32 = (uint64_t)total_rows < 0xFFFFFFFFull;
+  // 32-bit row keys: the sorts key on global rows (< 2^32 - 1 rows per call, e.g. 2^32
+  // rows of D = 16 fp32 is 275 GB, beyond one GPU's table budget; shard across calls)
+  DLRM_REQUIRE((uint64_t)total_rows < 0xFFFFFFFFull, DLRM_ERR_UNSUPPORTED,
+               "%s: %lld rows in one call (at most 2^32 - 2)", name, (long long)total_rows);
 #define BWD(K, I, O)                                                                     \
   return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
                              gout, gbs, lr, eps, ws, ws_bytes, max_seg, err, presorted, st, name)
-  if (k32) {
-    if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
-    if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
-    if (ib == 64 && ob == 32) BWD(uint32_t, int64_t, int32_t);
-    BWD(uint32_t, int64_t, int64_t);
-  } else {
-    if (ib == 32 && ob == 32) BWD(uint64_t, int32_t, int32_t);
-    if (ib == 32 && ob == 64) BWD(uint64_t, int32_t, int64_t);
-    if (ib == 64 && ob == 32) BWD(uint64_t, int64_t, int32_t);
-    BWD(uint64_t, int64_t, int64_t);
-  }
+  if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
+  if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
+  if (ib == 64 && ob == 32) BWD(uint32_t, int64_t, int32_t);
+  BWD(uint32_t, int64_t, int64_t);
 #undef BWD
 }
 
@@ -1311,9 +1357,7 @@ extern "C" size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t 
   if (num_lookups <= 0) return 256;
   if (D < 1) D = 1;
   const int end_bit = bit_width_u64((uint64_t)(total_rows > 0 ? total_rows : 1));
-  if ((uint64_t)total_rows < 0xFFFFFFFFull)
-    return carve_bwd_ws<uint32_t>(nullptr, num_lookups, D, end_bit).total;
-  return carve_bwd_ws<uint64_t>(nullptr, num_lookups, D, end_bit).total;
+  return carve_bwd_ws<uint32_t>(nullptr, num_lookups, D, end_bit).total;
 }
 
 extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base,

@@ -505,16 +505,53 @@ def gemm_workspace_size(M: int, N: int, K: int, trans_a: bool = False,
 GEMM_FULL, GEMM_PARTIAL, GEMM_REDUCE = 0, 1, 2  # dlrm_gemm_mode
 
 
+def planes_empty(rows: int, cols: int, device) -> torch.Tensor:
+    """Zeroed split-bf16 planes [3, rows, roundup(cols, 8)] for an fp32 [rows, cols] matrix
+    (the padding columns stay zero: the GEMM reads k-contiguous rows up to roundup(K, 8))."""
+    return torch.zeros((3, rows, (cols + 7) // 8 * 8), dtype=torch.bfloat16, device=device)
+
+
+def split_planes(X: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """X (2-D fp32, unit inner stride) -> planes [3, rows, >= cols] bf16 with
+    X = P[0] + P[1] + P[2] exactly (dlrm_split_planes)."""
+    _check_cuda(X, out)
+    if X.dim() != 2 or X.stride(1) != 1 or X.dtype != torch.float32:
+        raise ValueError("split_planes: X must be 2-D fp32 with unit inner stride")
+    rows, cols = X.shape
+    if out is None:
+        out = planes_empty(rows, cols, X.device)
+    if (out.dim() != 3 or out.shape[0] != 3 or out.shape[1] < rows or out.stride(2) != 1
+            or out.dtype != torch.bfloat16 or out.stride(1) < cols):
+        raise ValueError("split_planes: out must be bf16 [3, >= rows, >= cols]")
+    _lib.call("dlrm_split_planes", _p(X), rows, cols, X.stride(0), _p(out), out.stride(1),
+              out.stride(0), _stream(X.device))
+    return out
+
+
+def _plane_args(P: Optional[torch.Tensor]):
+    if P is None:
+        return None, 0, 0
+    if P.dim() != 3 or P.shape[0] != 3 or P.dtype != torch.bfloat16 or P.stride(2) != 1:
+        raise ValueError("planes must be bf16 [3, rows, ld] with unit inner stride")
+    return P.data_ptr(), P.stride(1), P.stride(0)
+
+
 def gemm_problem(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False,
                  trans_b: bool = False, C: Optional[torch.Tensor] = None, alpha: float = 1.0,
                  epilogue: int = EPI_STORE, bias: Optional[torch.Tensor] = None,
                  aux: Optional[torch.Tensor] = None, ones_col: int = -1,
-                 partial: Optional[torch.Tensor] = None, splits: int = 0):
+                 partial: Optional[torch.Tensor] = None, splits: int = 0,
+                 a_planes: Optional[torch.Tensor] = None,
+                 b_planes: Optional[torch.Tensor] = None,
+                 c_planes: Optional[torch.Tensor] = None):
     """One dlrm_gemm_problem: C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D
     operands (unit inner stride); ones_col >= 0 also writes C[:, ones_col] =
     epilogue(alpha * op(A).sum(1)) (a Linear bias gradient).  With ``partial`` the problem
     is a PARTIAL one: K split ``splits`` ways, raw partials into ``partial``, C untouched
-    until reduce_problem(...) runs in a later launch.  Returns (struct, C)."""
+    until reduce_problem(...) runs in a later launch.  ``a_planes`` / ``b_planes``: the
+    split-bf16 planes of the stored A / B (split_planes; both or neither) - the GEMM then
+    runs on the bf16 matrix core from them; ``c_planes``: also split every written C
+    element into these planes.  Returns (struct, C)."""
     _check_cuda(A, B, C, bias, aux)
     if A.stride(1) != 1 or B.stride(1) != 1:
         raise ValueError("gemm operands need unit inner stride")
@@ -537,7 +574,8 @@ def gemm_problem(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False,
                           aux.data_ptr() if aux is not None else None,
                           aux.stride(0) if aux is not None else 0, int(ones_col),
                           GEMM_PARTIAL if partial is not None else GEMM_FULL, int(splits),
-                          partial.data_ptr() if partial is not None else None)
+                          partial.data_ptr() if partial is not None else None,
+                          *_plane_args(a_planes), *_plane_args(b_planes), *_plane_args(c_planes))
     return pr, C
 
 

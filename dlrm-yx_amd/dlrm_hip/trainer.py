@@ -201,6 +201,16 @@ class DLRMTrainer:
         self.bot = self.layers[:self.n_bot]
         self.top = self.layers[self.n_bot:]
         self._bufs = {}
+        # Split-bf16 planes of the top MLP (one GPU, SGD fused into the backward): every top
+        # GEMM reads its operands as exact (h, m, l) bf16 planes and runs on the bf16 matrix
+        # core (dlrm_gemm_problem.a/b_planes); each producer writes the planes of what it
+        # writes (c_planes: forward activations, data gradients, the SGD-updated weights),
+        # two producers outside the GEMMs split theirs in one launch each (the interaction
+        # output R, the head's input gradient).  DLRM_GEMM_PLANES=0: the exact-f32 path.
+        self.use_planes = (os.environ.get("DLRM_GEMM_PLANES", "1") != "0" and world_size == 1
+                           and self.grads is None and len(self.top) > 1)
+        self.Wp = ([ops.planes_empty(L.N, L.Kp, self.dev) for L in self.top[:-1]]
+                   if self.use_planes else None)
         # independent kernels of a step run on a side stream (see step())
         self.concurrent = True
         # which overlaps to use: "fwd" (bottom MLP || lookup), "top" (wgrad || next dgrad),
@@ -255,6 +265,14 @@ class DLRMTrainer:
                 L.W.zero_()
                 L.W[:, :L.K].normal_(0.0, math.sqrt(2.0 / (L.N + L.K)), generator=g)
                 L.b.normal_(0.0, math.sqrt(1.0 / L.N), generator=g)
+        self._split_weight_planes()
+
+    def _split_weight_planes(self):
+        """(Re)derive the top weights' planes from the fp32 weights (after any host-side
+        write of the weights; the step itself keeps them in step)."""
+        if self.use_planes:
+            for L, P in zip(self.top[:-1], self.Wp):
+                ops.split_planes(L.W, out=P)
 
     def load_dense(self, mlp_params: Sequence[tuple], tables: Optional[Sequence] = None):
         """Copy (W [N,K], b [N]) per layer (bottom then top) and optionally GLOBAL tables."""
@@ -271,6 +289,7 @@ class DLRMTrainer:
                     if self.phys_kind[p] != 0:
                         src = src[self.phys_kind[p] - 1]
                     self.weights[s:e].copy_(torch.as_tensor(src))
+        self._split_weight_planes()
 
     @classmethod
     def from_oracle(cls, cfg: TrainerConfig, ref, device="cuda:0", **kw):
@@ -480,6 +499,12 @@ class DLRMTrainer:
         bufs["prob"] = torch.zeros(Bl, **f32)
         bufs["dz"] = torch.zeros(Bl, **f32)
         bufs["loss"] = torch.zeros(1, **f32)
+        if self.use_planes:  # planes of R, the top activations (1-columns: h = 1) and g
+            bufs["Rp"] = ops.planes_empty(Bl, self.ldR, dev)
+            bufs["top_actp"] = [ops.planes_empty(Bl, L.Np, dev) for L in self.top[:-1]]
+            for P, L in zip(bufs["top_actp"], self.top[:-1]):
+                P[0, :, L.N] = 1.0
+            bufs["gp"] = [ops.planes_empty(Bl, wmax, dev) for _ in range(3)]
         self._bufs[key] = bufs
         return bufs
 
@@ -612,10 +637,17 @@ class DLRMTrainer:
                 else:
                     ops.interact_forward(cfg.arch_interaction_op, x, feats,
                                          cfg.arch_interaction_itself, out=bufs["R"])
+                pl = self.use_planes
+                if pl:
+                    ops.split_planes(bufs["R"], out=bufs["Rp"])
             h = bufs["R"]
-            for L, out in zip(self.top[:-1], bufs["top_act"]):
-                self._gemm([self._fwd(L, h, out)])
-                h = out
+            hp = bufs["Rp"] if pl else None
+            nt = len(self.top) - 1
+            for li, (L, out) in enumerate(zip(self.top[:-1], bufs["top_act"])):
+                # the last GEMM layer's output feeds only the head (fp32): no planes
+                op = bufs["top_actp"][li] if pl and li < nt - 1 else None
+                self._gemm([self._fwd(L, h, out, hp, self.Wp[li] if pl else None, op)])
+                h, hp = out, op
             last = self.top[-1]
             # head: last layer + sigmoid + loss + dz + input grad + [dw | db] (bias folded:
             # [h | 1] . [w | b]) in two launches; the update follows every read of w
@@ -631,13 +663,21 @@ class DLRMTrainer:
                               lr=lr if fused_opt else 0.0,
                               workspace=self._ws_head_step(Bl, last.Kp))
             g = gview
+            GP = bufs["gp"] if pl else [None] * 3
+            if pl:  # the head's input gradient as planes for the top backward
+                with prof("head"):
+                    ops.split_planes(g[:, :self.top[-2].N], out=GP[gi])
             rq = []  # reduce jobs riding on the next launch; G rotates over three buffers
             for li in range(len(self.top) - 2, -1, -1):
                 L = self.top[li]
                 inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
+                inpp = (bufs["top_actp"][li - 1] if li > 0 else bufs["Rp"]) if pl else None
                 gn = (gi + 1) % 3
-                dg = self._dgrad(L, g, inp if li > 0 else None, G[gn])
-                w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li))
+                pk = dict(gp=GP[gi], wp=self.Wp[li], outp=GP[gn] if li > 0 else None) \
+                    if pl else {}
+                dg = self._dgrad(L, g, inp if li > 0 else None, G[gn], **pk)
+                wk = dict(planes=(GP[gi], inpp, self.Wp[li])) if pl else {}
+                w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li), **wk)
                 if r is not None and self.group_wgrad:
                     # the split wgrad only writes partials (its update rides on the next
                     # launch's reduce job), so it may run beside the dgrad reading W
@@ -849,58 +889,65 @@ class DLRMTrainer:
 
     # -------------------------------------------------------------- pieces --
     @staticmethod
-    def _fwd(L: _Layer, h, out):
-        """[h | 1] . [W | b]^T with ReLU (bias folded into the last k-term)."""
-        return ops.gemm_problem(h[:, :L.Kp], L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)[0]
+    def _fwd(L: _Layer, h, out, hp=None, wp=None, outp=None):
+        """[h | 1] . [W | b]^T with ReLU (bias folded into the last k-term); with planes
+        (hp, wp) on the bf16 matrix core, outp = the planes of out (or None)."""
+        return ops.gemm_problem(h[:, :L.Kp], L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU,
+                                a_planes=hp, b_planes=wp, c_planes=outp)[0]
 
     @staticmethod
-    def _dgrad(L: _Layer, g, inp, out):
+    def _dgrad(L: _Layer, g, inp, out, gp=None, wp=None, outp=None):
         """dX = g W (x ReLU'(inp) when inp is given).  Widths that are not a multiple of 4
-        run over Kp (the bias column's gradient lands in a column nobody reads)."""
+        run over Kp (the bias column's gradient lands in a column nobody reads).  Planes:
+        gp / wp of g / W, outp = the planes of dX (or None)."""
         n = L.K if L.K % 4 == 0 else L.Kp
+        pk = dict(a_planes=gp, b_planes=wp, c_planes=outp)
         if inp is not None:
             return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n], epilogue=ops.EPI_DRELU,
-                                    aux=inp)[0]
-        return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n])[0]
+                                    aux=inp, **pk)[0]
+        return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n], **pk)[0]
 
     @staticmethod
-    def _wgrad(L: _Layer, g, inp, fused_opt, lr, **part):
+    def _wgrad(L: _Layer, g, inp, fused_opt, lr, planes=None, **part):
         """[dW | db] = g^T [inp | 1]; fused SGD on one GPU.  With K % 4 == 0 the bias
         gradient is the row sum of g^T (ones_col) and the GEMM covers only the K weight
-        columns; otherwise the constant-1 column of inp is multiplied like a weight column."""
+        columns; otherwise the constant-1 column of inp is multiplied like a weight column.
+        planes = (planes of g, of inp, of W): read g / inp from them, keep W's in step."""
         C = L.W if fused_opt else L.gW
         kw = dict(alpha=lr, epilogue=ops.EPI_SGD) if fused_opt else {}
+        if planes is not None:
+            kw.update(a_planes=planes[0], b_planes=planes[1], c_planes=planes[2])
         if L.K % 4 == 0:
             return ops.gemm_problem(g[:, :L.N], inp[:, :L.K], trans_a=True, C=C, ones_col=L.K,
                                     **kw, **part)[0]
         return ops.gemm_problem(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=C, **kw, **part)[0]
 
-    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key, last=False):
+    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key, last=False, planes=None):
         """The wgrad of L as (problem, reduce job or None): split-K wgrads write partials
         into a per-layer buffer and their reduction (+ SGD) runs in the NEXT launch.  The
         last GEMM of the step (last=True) has no next launch to carry a reduce job: its
         K split, if any, is reduced inside its own launch (FULL mode)."""
         if last and self.full_last_wgrad:
-            return self._wgrad(L, g, inp, fused_opt, lr), None
+            return self._wgrad(L, g, inp, fused_opt, lr, planes), None
         bufs = self._cur
         sp = bufs.setdefault("splits", {})
         if key not in sp:
-            sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr), partial=True)
+            sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr, planes), partial=True)
             # tuning override (A/B sweeps only): DLRM_WG_SPLITS="top1:4,bot0:2"
             for item in os.environ.get("DLRM_WG_SPLITS", "").split(","):
                 name, _, val = item.partition(":")
                 if name == f"{key[0]}{key[1]}" and val.isdigit() and int(val) >= 1:
-                    sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr),
+                    sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr, planes),
                                               partial=True, requested=int(val))
         s = sp[key]
         if s <= 1:
-            return self._wgrad(L, g, inp, fused_opt, lr), None
+            return self._wgrad(L, g, inp, fused_opt, lr, planes), None
         parts = bufs.setdefault("partials", {})
         M, N = L.N, (L.K if L.K % 4 == 0 else L.Kp)
         need = ops.gemm_partial_bytes(M, N, s)
         if key not in parts or parts[key].numel() * 4 < need:
             parts[key] = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
-        pr = self._wgrad(L, g, inp, fused_opt, lr, partial=parts[key], splits=s)
+        pr = self._wgrad(L, g, inp, fused_opt, lr, planes, partial=parts[key], splits=s)
         return pr, ops.reduce_problem(pr)
 
     def _gemm(self, problems, side=False):

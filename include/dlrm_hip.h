@@ -93,7 +93,9 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
 /* ---------------------------------------------------------------- library -- */
 /* 2: the TBE backward entry points take an error_flag (round 2).
  * 3: dlrm_qr_expand_csr takes phys_capacity + error_flag; a PARTIAL split count must be
- *    normalized (dlrm_gemm_f32_splits) (round 3). */
+ *    normalized (dlrm_gemm_f32_splits) (round 3).
+ * 4: dlrm_gemm_problem carries split-bf16 planes; dlrm_split_planes; the TBE backward's
+ *    rows per call must be < 2^32 - 1 (round 3). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 
@@ -469,7 +471,31 @@ typedef struct dlrm_gemm_problem {
   int32_t mode;     /* dlrm_gemm_mode */
   int32_t splits;   /* PARTIAL / REDUCE */
   float* partial;   /* PARTIAL / REDUCE */
+  /* Split-bf16 planes (ABI v4; all NULL = the exact-f32 MFMA path).  The planes of an
+   * fp32 matrix X stored [rows][ld] are three bf16 matrices h, m, l at
+   * planes + q * plane_stride (q = 0, 1, 2), row pitch ld_planes (a multiple of 8), with
+   * X = h + m + l exactly (dlrm_split_planes).  With a_planes AND b_planes set, the GEMM
+   * reads op(A), op(B) from the planes (A / B still describe the same matrices and must
+   * hold them) and computes on the bf16 matrix core: six products per k-step
+   * (hh, hm, mh, hl, lh, mm), fp32 accumulation, accuracy at or below the exact-f32 path
+   * (tests/test_gpu_kernels.py::test_gemm_planes_*).  Needs K and every mn-contiguous
+   * extent % 8 == 0 after padding: a k-contiguous operand's rows are read up to
+   * roundup(K, 8), so the plane columns [K, roundup(K, 8)) must be zero in A or in B.
+   * c_planes (optional, any mode that writes C): every C element the epilogue writes is
+   * also split into c_planes, so the next GEMM can read it as planes. */
+  const void* a_planes;
+  int64_t lda_planes, a_plane_stride;
+  const void* b_planes;
+  int64_t ldb_planes, b_plane_stride;
+  void* c_planes;
+  int64_t ldc_planes, c_plane_stride;
 } dlrm_gemm_problem;
+
+/* X [rows][cols] fp32 (row pitch ld) -> planes [3][rows][ld_planes] bf16 (plane stride
+ * plane_stride): X = h + m + l exactly (round to nearest at each level), the layout the
+ * GEMM's a_planes / b_planes / c_planes use.  ld_planes % 8 == 0, ld_planes >= cols. */
+int dlrm_split_planes(const float* X, int64_t rows, int64_t cols, int64_t ld, void* planes,
+                      int64_t ld_planes, int64_t plane_stride, dlrm_stream_t stream);
 size_t dlrm_gemm_f32_group_workspace_size(int32_t n, const dlrm_gemm_problem* problems);
 /* The planner's K split for one problem as if launched alone, in its mode (FULL: an
  * in-launch split; PARTIAL: the split a deferred REDUCE will finish).  PARTIAL with

@@ -1085,3 +1085,161 @@ def test_gemm_x6l_body(ops, split, monkeypatch):
     assert ok, msg
     ok, msg = gemm_close(got[:, Kw].numpy(), gd.sum(0).numpy(), gd.abs().sum(0).numpy(), Bt + 8)
     assert ok, msg
+
+
+# ------------------------------------------------------ pre-split planes (x6d body) --
+def _planes(ops, X):
+    return ops.split_planes(X.contiguous())
+
+
+@pytest.mark.gpu
+def test_split_planes_exact(ops):
+    """dlrm_split_planes: x = h + m + l exactly (fp64 sum), each plane bf16 round-to-nearest,
+    padding columns untouched (zero)."""
+    torch.manual_seed(0)
+    X = (torch.randn(300, 77) * torch.logspace(-20, 20, 77)).to(dev)
+    X[0, :5] = torch.tensor([0.0, -0.0, 1.0, 1e38, -1e-30])
+    P = ops.split_planes(X)
+    assert P.shape == (3, 300, 80)
+    Pd = P.double()
+    Xp = torch.zeros(300, 80, dtype=torch.float64, device=dev)
+    Xp[:, :77] = X.double()
+    assert torch.equal(Pd[0] + Pd[1] + Pd[2], Xp)
+    assert torch.equal(P[0][:, :77], X.to(torch.bfloat16))
+    assert int(P[:, :, 77:].abs().sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(1000, 296, 136), (2048, 1024, 1024), (2048, 1024, 1028),
+                                   (520, 64, 2048)])
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_planes_layouts(ops, M, N, K, ta, tb):
+    """The pre-split body: every operand layout within the fp32 dot-product bound of the
+    fp64 product (as accurate as the exact-f32 MFMA path), tile shapes 128x64 / 64x64,
+    ragged edges, K % 8 == 4 on k-contiguous operands (zero plane padding)."""
+    if K % 8 and (ta or not tb):
+        pytest.skip("an mn-contiguous operand needs K % 8 == 0")
+    torch.manual_seed(M + N + K + 3 * ta + tb)
+    A = (torch.randn(K, M) if ta else torch.randn(M, K)).to(dev)
+    Bm = (torch.randn(N, K) if tb else torch.randn(K, N)).to(dev)
+    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
+    pr, C = ops.gemm_problem(A, Bm, bool(ta), bool(tb), a_planes=_planes(ops, A),
+                             b_planes=_planes(ops, Bm))
+    ops.gemm_group([pr], ws)
+    opA = A.double().t() if ta else A.double()
+    opB = Bm.double().t() if tb else Bm.double()
+    ok, msg = gemm_close(C.cpu().numpy(), (opA @ opB).cpu().numpy(),
+                         (opA.abs() @ opB.abs()).cpu().numpy(), K)
+    assert ok, (M, N, K, ta, tb, msg)
+    Cf = ops.gemm(A, Bm, bool(ta), bool(tb), workspace=ws)  # the f32 path, for reference
+    assert not torch.equal(C, Cf) or K < 32  # (a different math actually ran)
+
+
+@pytest.mark.gpu
+def test_gemm_planes_epilogues_and_c_planes(ops):
+    """Forward (ReLU) and dgrad (ReLU') from planes write c_planes bitwise equal to
+    split_planes of the C they write; a wgrad with fused SGD and bias row sums (ones_col)
+    runs FULL and as PARTIAL + REDUCE (bitwise equal), both keeping the weight planes in
+    step with the weights; DLRM_GEMM_PLANES=0 runs the f32 body on the same problem."""
+    torch.manual_seed(5)
+    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
+    Bt, K, Nout = 2048, 1024, 512
+    X = torch.randn(Bt, K + 4, device=dev)
+    X[:, K] = 1.0
+    X[:, K + 1:] = 0.0
+    W = torch.randn(Nout, K + 4, device=dev) * 0.05
+    W[:, K + 1:] = 0.0
+    XP, WP = _planes(ops, X), _planes(ops, W)
+    Y = torch.zeros(Bt, Nout, device=dev)
+    YP = ops.planes_empty(Bt, Nout, dev)
+    pr, _ = ops.gemm_problem(X, W, trans_b=True, C=Y, epilogue=ops.EPI_RELU, a_planes=XP,
+                             b_planes=WP, c_planes=YP)
+    ops.gemm_group([pr], ws)
+    ref = torch.relu(X.double() @ W.double().t())
+    ok, msg = gemm_close(Y.cpu().numpy(), ref.cpu().numpy(),
+                         (X.double().abs() @ W.double().abs().t()).cpu().numpy(), K + 4)
+    assert ok, msg
+    assert torch.equal(YP, _planes(ops, Y))
+    # dgrad with ReLU' of X
+    G = torch.randn(Bt, Nout, device=dev)
+    GP = _planes(ops, G)
+    dX = torch.zeros(Bt, K, device=dev)
+    dXP = ops.planes_empty(Bt, K, dev)
+    pd, _ = ops.gemm_problem(G, W[:, :K], C=dX, epilogue=ops.EPI_DRELU, aux=X, a_planes=GP,
+                             b_planes=WP, c_planes=dXP)
+    ops.gemm_group([pd], ws)
+    ref = (G.double() @ W[:, :K].double()) * (X[:, :K] > 0)
+    ok, msg = gemm_close(dX.cpu().numpy(), ref.cpu().numpy(),
+                         (G.double().abs() @ W[:, :K].double().abs()).cpu().numpy(), Nout)
+    assert ok, msg
+    assert torch.equal(dXP, _planes(ops, dX))
+    # wgrad + SGD + bias row sums: FULL vs PARTIAL + REDUCE, weight planes kept in step
+    kw = dict(trans_a=True, alpha=0.5, epilogue=ops.EPI_SGD, ones_col=K, a_planes=GP,
+              b_planes=XP)
+    W1, W1P = W.clone(), WP.clone()
+    pw, _ = ops.gemm_problem(G, X[:, :K], C=W1, c_planes=W1P, **kw)
+    ops.gemm_group([pw], ws)
+    s = max(2, ops.gemm_splits(pw, partial=True))
+    W2, W2P = W.clone(), WP.clone()
+    part = torch.empty(ops.gemm_partial_bytes(Nout, K, s) // 4, device=dev)
+    pp, _ = ops.gemm_problem(G, X[:, :K], C=W2, c_planes=W2P, partial=part,
+                             splits=ops.gemm_splits(pw, partial=True, requested=s), **kw)
+    ops.gemm_group([pp], ws)
+    ops.gemm_group([ops.reduce_problem(pp)], ws)
+    torch.cuda.synchronize()
+    assert torch.equal(W1P, _planes(ops, W1)) and torch.equal(W2P, _planes(ops, W2))
+    gd, Xd = G.double().cpu(), X[:, :K].double().cpu()
+    for Wn in (W1, W2):
+        got = (W - Wn).double().cpu() / 0.5
+        ok, msg = gemm_close(got[:, :K].numpy(), (gd.t() @ Xd).numpy(),
+                             (gd.abs().t() @ Xd.abs()).numpy(), Bt + 8)
+        assert ok, msg
+        ok, msg = gemm_close(got[:, K].numpy(), gd.sum(0).numpy(), gd.abs().sum(0).numpy(),
+                             Bt + 8)
+        assert ok, msg
+
+
+@pytest.mark.gpu
+def test_gemm_planes_group_and_env_off(ops, monkeypatch):
+    """A grouped launch of pre-split problems (dgrad + PARTIAL wgrad + an earlier layer's
+    REDUCE) equals the same problems launched alone, bitwise; DLRM_GEMM_PLANES=0 gives the
+    exact-f32 result bitwise."""
+    torch.manual_seed(7)
+    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
+    Bt, K, N = 2048, 512, 1024
+    G = torch.randn(Bt, N, device=dev)
+    X = torch.relu(torch.randn(Bt, K + 4, device=dev))
+    W = torch.randn(N, K + 4, device=dev) * 0.05
+    GP, XP, WP = _planes(ops, G), _planes(ops, X), _planes(ops, W)
+
+    def problems(dX, W_, WP_, part):
+        pd, _ = ops.gemm_problem(G, W[:, :K], C=dX, epilogue=ops.EPI_DRELU, aux=X,
+                                 a_planes=GP, b_planes=WP)
+        pw0, _ = ops.gemm_problem(G, X[:, :K], trans_a=True, C=W_, alpha=0.1,
+                                  epilogue=ops.EPI_SGD, ones_col=K, a_planes=GP, b_planes=XP,
+                                  c_planes=WP_)
+        s = max(2, ops.gemm_splits(pw0, partial=True))
+        pw, _ = ops.gemm_problem(G, X[:, :K], trans_a=True, C=W_, alpha=0.1,
+                                 epilogue=ops.EPI_SGD, ones_col=K, a_planes=GP, b_planes=XP,
+                                 c_planes=WP_, partial=part, splits=s)
+        return pd, pw
+    part = torch.empty(ops.gemm_partial_bytes(N, K, 32) // 4, device=dev)
+    dX1, W1, W1P = torch.zeros(Bt, K, device=dev), W.clone(), WP.clone()
+    pd, pw = problems(dX1, W1, W1P, part)
+    ops.gemm_group([pd, pw], ws)
+    ops.gemm_group([ops.reduce_problem(pw)], ws)
+    dX2, W2, W2P = torch.zeros(Bt, K, device=dev), W.clone(), WP.clone()
+    pd, pw = problems(dX2, W2, W2P, part)
+    ops.gemm_group([pd], ws)
+    ops.gemm_group([pw], ws)
+    ops.gemm_group([ops.reduce_problem(pw)], ws)
+    torch.cuda.synchronize()
+    assert torch.equal(dX1, dX2) and torch.equal(W1, W2) and torch.equal(W1P, W2P)
+    monkeypatch.setenv("DLRM_GEMM_PLANES", "0")
+    dX3 = torch.zeros(Bt, K, device=dev)
+    pd, _ = ops.gemm_problem(G, W[:, :K], C=dX3, epilogue=ops.EPI_DRELU, aux=X, a_planes=GP,
+                             b_planes=WP)
+    ops.gemm_group([pd], ws)
+    dX4 = ops.gemm(G, W[:, :K], epilogue=ops.EPI_DRELU, aux=X, workspace=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(dX3, dX4)
