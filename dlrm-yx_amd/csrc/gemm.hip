@@ -264,22 +264,58 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
-// v -> three bf16 planes at Cp (v = h + m + l exactly: round to nearest at each level).
+// v -> (h, m, l) bf16 bit patterns, v = h + m + l exactly (round to nearest at each level).
+__device__ __forceinline__ void split3(float v, unsigned short& h, unsigned short& m,
+                                       unsigned short& l) {
+  const __bf16 hb = (__bf16)v;
+  const float r = v - (float)hb;
+  const __bf16 mb = (__bf16)r;
+  const __bf16 lb = (__bf16)(r - (float)mb);
+  h = __builtin_bit_cast(unsigned short, hb);
+  m = __builtin_bit_cast(unsigned short, mb);
+  l = __builtin_bit_cast(unsigned short, lb);
+}
+
+// v -> the three bf16 planes at Cp (one element).
 __device__ __forceinline__ void store_planes(const GemmParams& p, int64_t row, int64_t col,
                                              float v) {
-  const __bf16 h = (__bf16)v;
-  const float r = v - (float)h;
-  const __bf16 m = (__bf16)r;
-  const __bf16 l = (__bf16)(r - (float)m);
-  __bf16* d = p.Cp + row * p.ldcp + col;
+  unsigned short h, m, l;
+  split3(v, h, m, l);
+  unsigned short* d = reinterpret_cast<unsigned short*>(p.Cp) + row * p.ldcp + col;
   d[0] = h;
   d[p.psc] = m;
   d[2 * p.psc] = l;
 }
 
-// C = epilogue(v) where v = alpha * acc (already scaled).
-__device__ __forceinline__ void apply_epilogue(const GemmParams& p, int64_t row, int64_t col,
-                                               float v) {
+// N consecutive values (N = 4 or 8) -> the planes at Cp + row*ldcp + col, one 8- / 16-B
+// store per plane (col % N == 0; the host guarantees 16-B aligned planes, ldcp % 8 == 0).
+template <int N>
+__device__ __forceinline__ void store_planes_vec(const GemmParams& p, int64_t row, int64_t col,
+                                                 const float* v) {
+  unsigned w[3][N / 2];
+#pragma unroll
+  for (int u = 0; u < N / 2; ++u) {
+    unsigned short h0, m0, l0, h1, m1, l1;
+    split3(v[2 * u], h0, m0, l0);
+    split3(v[2 * u + 1], h1, m1, l1);
+    w[0][u] = h0 | ((unsigned)h1 << 16);
+    w[1][u] = m0 | ((unsigned)m1 << 16);
+    w[2][u] = l0 | ((unsigned)l1 << 16);
+  }
+  __bf16* d = p.Cp + row * p.ldcp + col;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if constexpr (N == 8)
+      *reinterpret_cast<uint4*>(d + q * p.psc) = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
+    else
+      *reinterpret_cast<uint2*>(d + q * p.psc) = make_uint2(w[q][0], w[q][1]);
+  }
+}
+
+// C = epilogue(v) where v = alpha * acc (already scaled); returns the value written.
+// planes = false: the caller writes the C planes itself (vectorized).
+__device__ __forceinline__ float apply_epilogue(const GemmParams& p, int64_t row, int64_t col,
+                                                float v, bool planes = true) {
   float* cp = p.C + row * p.ldc + col;
   switch (p.epi) {
     case DLRM_EPI_BIAS:
@@ -304,7 +340,8 @@ __device__ __forceinline__ void apply_epilogue(const GemmParams& p, int64_t row,
       break;
   }
   *cp = v;
-  if (p.Cp) store_planes(p, row, col, v);
+  if (planes && p.Cp) store_planes(p, row, col, v);
+  return v;
 }
 
 
@@ -479,6 +516,11 @@ __device__ __forceinline__ void finish_tile(const GemmParams& p, const f32x4 (&a
   }
   if (!splitk_reduce<BM, BN, NV, FM>(p, tile, split, v, rs, wm0 + l16, 16, rs_owner, smem))
     return;
+  // C planes: the written tile is staged in LDS (free now) and split in 8-column chunks,
+  // one 16-B store per plane (a lane's accumulators are 4 rows of one column)
+  constexpr int LDT = BN + 4;
+  const bool stage = p.Cp != nullptr;
+  if (stage) __syncthreads();  // every wave is done with the main loop's LDS
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -487,10 +529,30 @@ __device__ __forceinline__ void finish_tile(const GemmParams& p, const f32x4 (&a
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t row = m0 + wm0 + i * 16 + 4 * kq + r;
-        if (row < p.M && col < p.N)
-          apply_epilogue(p, row, col, p.alpha * v[(i * FN + j) * 4 + r]);
+        if (row < p.M && col < p.N) {
+          const float w = apply_epilogue(p, row, col, p.alpha * v[(i * FN + j) * 4 + r], false);
+          if (stage) smem[(wm0 + i * 16 + 4 * kq + r) * LDT + wn0 + j * 16 + l16] = w;
+        }
       }
     }
+  if (stage) {
+    __syncthreads();
+    constexpr int NT = WGM * WGN * 64, CPRW = BN / 8;
+    for (int c = tid; c < BM * CPRW; c += NT) {
+      const int r = c / CPRW, c8 = 8 * (c - r * CPRW);
+      const int64_t row = m0 + r, col = n0 + c8;
+      if (row >= p.M || col >= p.N) continue;
+      const float* src = smem + r * LDT + c8;
+      if (col + 8 <= p.N) {
+        float w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = src[u];
+        store_planes_vec<8>(p, row, col, w);
+      } else {
+        for (int u = 0; u < 8 && col + u < p.N; ++u) store_planes(p, row, col + u, src[u]);
+      }
+    }
+  }
   if (rs_owner) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -1484,10 +1546,12 @@ __device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
         }
     }
     const int64_t e = 4 * i, row = e / p.N, col = e - row * p.N;
-    apply_epilogue(p, row, col, p.alpha * acc.x);
-    apply_epilogue(p, row, col + 1, p.alpha * acc.y);
-    apply_epilogue(p, row, col + 2, p.alpha * acc.z);
-    apply_epilogue(p, row, col + 3, p.alpha * acc.w);
+    float w[4];
+    w[0] = apply_epilogue(p, row, col, p.alpha * acc.x, false);
+    w[1] = apply_epilogue(p, row, col + 1, p.alpha * acc.y, false);
+    w[2] = apply_epilogue(p, row, col + 2, p.alpha * acc.z, false);
+    w[3] = apply_epilogue(p, row, col + 3, p.alpha * acc.w, false);
+    if (p.Cp) store_planes_vec<4>(p, row, col, w);
   } else if (p.ones_col >= 0 && i - n4 < p.M) {
     const int64_t row = i - n4;
     const float* rsrc = p.part + (int64_t)S * MN + row;
@@ -1512,7 +1576,7 @@ __device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
 //   !KC (32 x MN, mn-contiguous): chunk c of k-row k in slot k(MN/8) + (c ^ f(k)),
 //        f(k) = (MN/8 >= 16 ? 2 : 1)(k ^ (k >> 1)) mod MN/8, fragments by two
 //        ds_read_b64_tr_b16 (hardware transpose).
-// 128x64 tiles run 4 stages (144 KiB: one workgroup per CU), 64x64 tiles 3 (72 KiB: two).
+// 4 stages: 144 KiB at 128x64, 96 KiB at 64x64 (one workgroup per CU).
 template <int MN, bool KC>
 struct PImg {
   static constexpr int SLOTS = 4 * MN;  // 16-B slots per plane and stage (MN x 32 bf16)
@@ -1557,7 +1621,8 @@ struct PImg {
 
 template <int BM, int BN>
 constexpr int x6d_stages() {
-  return BM * BN > 4096 ? 4 : 3;
+  return 4;  // (64x64 on 3 stages, two workgroups per CU: 20-45 % slower on the long-K
+             //  wgrads, profiles/r03_x6p_dma_probe.txt)
 }
 template <int BM, int BN>
 constexpr int x6d_smem_bytes() {
@@ -1857,7 +1922,7 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_group6L_kernel(const G
 }
 
 // The same grouped launch on the pre-split body (pipe_body_x6d): LDS from the dynamic
-// segment (up to 144 KiB), one workgroup per CU at 128x64, two at 64x64.
+// segment (96 or 144 KiB: one workgroup per CU).
 template <int BM, int BN, int KINDS>
 __global__ __launch_bounds__(256, 1) void gemm_group6d_kernel(const GemmGroup g) {
   extern __shared__ __attribute__((aligned(1024))) char smem6d[];
@@ -2432,6 +2497,7 @@ int launch_generic(const Desc& d, hipStream_t st) {
   p.A = d.A, p.lda = d.lda, p.B = d.B, p.ldb = d.ldb;
   p.C = d.C, p.ldc = d.ldc, p.epi = d.epi, p.bias = d.bias;
   p.aux = d.aux, p.ldaux = d.ldaux, p.ones_col = d.ones_col;
+  p.Cp = d.Cp, p.ldcp = d.ldcp, p.psc = d.psc;  // (c_planes are kept on every path)
   p.tiles_m = (int)dlrm::ceil_div(p.M, 64);
   p.tiles_n = (int)dlrm::ceil_div(p.N, 64);
   p.splits = 1;
@@ -2474,8 +2540,10 @@ int check_desc(const Desc& d) {
              "dlrm_gemm_f32: PARTIAL splits=%d is not a normalized count for K=%lld "
              "(use dlrm_gemm_f32_splits)", (int)d.splits, (long long)d.K);
   }
-  DLRM_ARG(!d.Cp || (d.ldcp >= d.ldc && d.psc >= 0),
-           "dlrm_gemm_f32: c_planes need ldc_planes >= ldc");
+  DLRM_ARG(!d.Cp || (d.ldcp >= d.ldc && d.psc >= 0 && d.ldcp % 8 == 0 && d.psc % 8 == 0 &&
+                     aligned16(d.Cp)),
+           "dlrm_gemm_f32: c_planes need 16-B aligned planes, ldc_planes >= ldc, "
+           "ldc_planes and plane_stride %% 8 == 0");
   DLRM_ARG(d.M >= 0 && d.N >= 0 && d.K >= 0, "dlrm_gemm_f32: negative size");
   if (d.M == 0 || (d.N == 0 && d.ones_col < 0)) return DLRM_OK;
   DLRM_ARG(d.C, "dlrm_gemm_f32: null C");

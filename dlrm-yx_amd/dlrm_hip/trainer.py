@@ -206,8 +206,9 @@ class DLRMTrainer:
         # core (dlrm_gemm_problem.a/b_planes); each producer writes the planes of what it
         # writes (c_planes: forward activations, data gradients, the SGD-updated weights),
         # two producers outside the GEMMs split theirs in one launch each (the interaction
-        # output R, the head's input gradient).  DLRM_GEMM_PLANES=0: the exact-f32 path.
-        self.use_planes = (os.environ.get("DLRM_GEMM_PLANES", "1") != "0" and world_size == 1
+        # output R, the head's input gradient).  Opt-in (DLRM_GEMM_PLANES=1): measured
+        # slower than the exact-f32 path in the C3 step (profiles/r03_planes_*.txt).
+        self.use_planes = (os.environ.get("DLRM_GEMM_PLANES", "0") == "1" and world_size == 1
                            and self.grads is None and len(self.top) > 1)
         self.Wp = ([ops.planes_empty(L.N, L.Kp, self.dev) for L in self.top[:-1]]
                    if self.use_planes else None)

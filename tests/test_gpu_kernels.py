@@ -1243,3 +1243,18 @@ def test_gemm_planes_group_and_env_off(ops, monkeypatch):
     dX4 = ops.gemm(G, W[:, :K], epilogue=ops.EPI_DRELU, aux=X, workspace=ws)
     torch.cuda.synchronize()
     assert torch.equal(dX3, dX4)
+
+
+@pytest.mark.gpu
+def test_gemm_c_planes_on_the_generic_path(ops):
+    """Unaligned operands (the generic kernel, and its row-sum kernel for ones_col) keep
+    c_planes in step with C too: a weight updated there must not leave stale planes."""
+    torch.manual_seed(11)
+    G, X = torch.randn(6, 3, device=dev), torch.randn(6, 7, device=dev)
+    W = torch.randn(3, 8, device=dev)
+    WP = _planes(ops, W)
+    pw, _ = ops.gemm_problem(G, X, trans_a=True, C=W, alpha=0.1, epilogue=ops.EPI_SGD,
+                             ones_col=7, c_planes=WP)
+    ops.gemm_group([pw])
+    torch.cuda.synchronize()
+    assert torch.equal(WP, _planes(ops, W))

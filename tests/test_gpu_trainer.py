@@ -92,7 +92,11 @@ def _rand_batch(rng, rows, B, L, m_den, loss):
 
 
 @pytest.mark.parametrize("name", list(CASES))
-def test_step_vs_oracle(name):
+@pytest.mark.parametrize("planes", ["0", "1"])
+def test_step_vs_oracle(name, planes, monkeypatch):
+    """Two steps vs the oracle, on the exact-f32 GEMMs and with the top MLP on split-bf16
+    planes (DLRM_GEMM_PLANES=1: pre-split x6d body, c_planes kept by every producer)."""
+    monkeypatch.setenv("DLRM_GEMM_PLANES", planes)
     DLRMTrainer, TrainerConfig = _trainer()
     c = CASES[name]
     D, rows = c["D"], c["rows"]
@@ -102,6 +106,7 @@ def test_step_vs_oracle(name):
     cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"], ln_top=ln_top,
                         loss_function=c["loss"], learning_rate=c["lr"])
     tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    assert tr.use_planes == (planes == "1")
     rng = np.random.RandomState(3)
     for s in range(2):
         X, lS_o, lS_i, T = _rand_batch(rng, rows, c["B"], c["L"], c["bot"][0], c["loss"])
