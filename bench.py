@@ -398,6 +398,36 @@ def input_pipeline_rate(tr, c, B, dev, steps=60, warmup=5, nb=16):
         os.unlink(path)
 
 
+def skew_rate(tr, c, B, uniform_ms, steps=200, warmup=20, nb=10, a=1.05):
+    """SURVEY.md §8d's skew-sensitivity run: the same step on batches whose indices are
+    Zipf(1.05) ranks folded onto each table's rows (hot rows: long runs of equal rows in the
+    sorted backward), graph-replayed like the headline loop; reported beside ``value``."""
+    try:
+        batches = [tr.synthetic_batch(B, c["L"], seed=500 + i, dist="zipf", zipf_a=a)
+                   for i in range(nb)]
+        idx = batches[0].indices.cpu().numpy()
+        hot = float((idx == 0).mean())
+        tr.step(batches[0])
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        graphs = [tr.capture(b, pool=pool) for b in batches]
+        for k in range(warmup):
+            graphs[k % nb]()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            graphs[k % nb]()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ms = el / steps * 1000.0
+        return {"value": round(B * steps / el, 1), "unit": "samples/s",
+                "ms_per_step": round(ms, 4), "vs_uniform": round(uniform_ms / ms, 4),
+                "steps": steps, "dist": f"zipf({a}) ranks mod rows, per table",
+                "row0_share_of_lookups": round(hot, 4)}
+    except Exception as e:  # noqa: BLE001 - reported, the headline line must still print
+        return {"error": repr(e)}
+
+
 def socket0_physical_cores(limit: int):
     """One hardware thread per physical core of CPU package 0, within this process's allowed
     CPUs (bench/dlrm_s_benchmark.sh:20-25 binds `numactl --physcpubind=<socket 0 physical
@@ -698,6 +728,9 @@ def main():
     pipe_rate = None
     if world == 1 and not args.no_kernel_timing:
         pipe_rate = input_pipeline_rate(tr, c, B, dev)
+    skew = None
+    if world == 1 and not args.no_kernel_timing and not args.no_graph:
+        skew = skew_rate(tr, c, B, uniform_ms=elapsed / args.steps * 1000.0)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -726,6 +759,7 @@ def main():
             "box_calibration": calib,
             "setup_preheat_ms": preheat,
             "input_pipeline": pipe_rate,
+            "skew_zipf": skew,
             "cpu_baseline": cpu,
         }
         if cpu and "value" in cpu:

@@ -437,10 +437,15 @@ class DLRMTrainer:
             t = self._rec_off[B] = torch.empty(self.T * B + 1, dtype=torch.int32, device=self.dev)
         return t
 
-    def synthetic_batch(self, B: int, L: int, seed: int) -> Batch:
+    def synthetic_batch(self, B: int, L: int, seed: int, dist: str = "uniform",
+                        zipf_a: float = 1.05) -> Batch:
         """Device-generated synthetic batch of the reference's shape: X ~ log(1+U[0,1))
         (dlrm_data_pytorch.py:727), L uniform indices per bag per table, targets U[0,1)
-        (rounded for bce)."""
+        (rounded for bce).  dist="zipf": the skew-sensitivity run of SURVEY.md §8d - each
+        table's indices are Zipf(zipf_a) ranks - 1 folded onto its rows (row 0 hottest),
+        drawn on the host (numpy) and uploaded."""
+        if dist not in ("uniform", "zipf"):
+            raise ValueError(f"dist {dist!r}: uniform or zipf")
         Bl = self.local_batch_size(B)
         L0 = self.bot[0]
         g = torch.Generator(device=self.dev)
@@ -450,9 +455,15 @@ class DLRMTrainer:
         Xp[:, L0.K] = 1.0  # bias column
         Tl = self.T_local
         indices = torch.empty(Tl * B * L, dtype=torch.int32, device=self.dev)
+        rng = np.random.RandomState(seed) if dist == "zipf" else None
         for j, t in enumerate(self.local_tables):
-            ops.uniform_int_fill_(indices[j * B * L:(j + 1) * B * L], int(self.cfg.ln_emb[t]),
-                                  seed * 1000003 + t * 7 + 1)
+            n = int(self.cfg.ln_emb[t])
+            if rng is not None:
+                z = (rng.zipf(zipf_a, B * L) - 1) % n
+                indices[j * B * L:(j + 1) * B * L] = torch.from_numpy(z.astype(np.int32))
+            else:
+                ops.uniform_int_fill_(indices[j * B * L:(j + 1) * B * L], n,
+                                      seed * 1000003 + t * 7 + 1)
         offsets = torch.arange(0, Tl * B * L + 1, L, dtype=torch.int32, device=self.dev)
         tg = torch.rand(Bl, generator=g, device=self.dev)
         if self.cfg.loss_function == "bce":

@@ -81,10 +81,13 @@ CASES = {
 }
 
 
-def _rand_batch(rng, rows, B, L, m_den, loss):
+def _rand_batch(rng, rows, B, L, m_den, loss, dist="uniform"):
     X = np.log1p(rng.rand(B, m_den).astype(np.float32))
     lS_o = np.array([np.arange(B) * L for _ in rows], dtype=np.int64)
-    lS_i = [rng.randint(0, n, size=B * L).astype(np.int64) for n in rows]
+    if dist == "zipf":  # SURVEY.md §8d skew run: Zipf(1.05) ranks folded onto the rows
+        lS_i = [((rng.zipf(1.05, size=B * L) - 1) % n).astype(np.int64) for n in rows]
+    else:
+        lS_i = [rng.randint(0, n, size=B * L).astype(np.int64) for n in rows]
     T = rng.rand(B, 1).astype(np.float32)
     if loss == "bce":
         T = np.round(T)
@@ -532,3 +535,39 @@ def test_c4_terabyte_widths_trajectory_vs_oracle():
         ok, msg = fp32_close(E.cpu().numpy(), [Er.item()], atol=1e-4)
         assert ok, (s, losses, msg)
     print("C4 losses (engine, oracle):", losses)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_c3_zipf_hot_rows_vs_oracle(graph):
+    """C3 widths with Zipf(1.05) indices (hot rows: row 0 takes ~5 % of every table's
+    lookups, runs of equal rows across many backward blocks) on the bench's path (presort
+    launch, gather-fused interaction, sorted block + combine backward), eager and
+    graph-replayed, three steps vs the oracle."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES["c3_small"]
+    D, rows = c["D"], c["rows"]
+    ln_top = [_num_int(len(rows), D)] + c["top"]
+    np.random.seed(11)
+    ref = O.OracleDLRM(D, rows, c["bot"], ln_top, loss_function=c["loss"])
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"], ln_top=ln_top,
+                        loss_function=c["loss"], learning_rate=c["lr"])
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    rng = np.random.RandomState(13)
+    B = 1024
+    for s in range(3):
+        X, lS_o, lS_i, T = _rand_batch(rng, rows, B, 1, c["bot"][0], c["loss"], dist="zipf")
+        assert max(float((i == 0).mean()) for i in lS_i) > 0.03
+        Zr, Er = ref.train_step(torch.tensor(X), torch.tensor(lS_o),
+                                [torch.tensor(i) for i in lS_i], torch.tensor(T), c["lr"])
+        b = tr.make_batch(X, lS_o, lS_i, T)
+        if graph and s > 0:  # (the first step of a batch size runs eagerly: allocations)
+            tr.capture(b)()
+            Z, E = tr._cur["prob"], tr._cur["loss"]
+        else:
+            Z, E = tr.step(b)
+        assert tr.gather_fused
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
+        assert ok, (s, msg)
+        ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
+        assert ok, (s, msg)
+    _compare_state(tr, ref)
