@@ -58,9 +58,9 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
     const int64_t a = (int64_t)off[0], e = (int64_t)off[nb];
     const int64_t stride = (int64_t)kOutsideBlocks * blockDim.x;
     const int64_t g = ((int64_t)blockIdx.x - bag_blocks) * blockDim.x + threadIdx.x;
-    auto mark = [&](int64_t p) {
-      keys[p] = sentinel;
-      pos[p] = (int32_t)p;
+    auto mark = [&](int64_t p) {  // (the tiled sort keeps these: -1 reads as "no bag" too
+      keys[p] = sentinel;          //  when the sorted values are bags)
+      pos[p] = KEYS ? (int32_t)p : -1;
       bag_of[p] = -1;
     };
     for (int64_t p = g; p < a && p < N; p += stride) mark(p);
@@ -584,8 +584,8 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
           if (psw) my_w = psw[pos[base + gl]];
         } else {
           const int32_t p = pos[base + gl];
-          bag = bag_of[p];
-          if (psw) my_w = psw[p];
+          bag = p >= 0 ? bag_of[p] : -1;
+          if (psw && p >= 0) my_w = psw[p];
         }
         if (bag >= 0) {
           const int t = bag / B;
@@ -809,6 +809,9 @@ struct TiledPass {
   int32_t* err;
   int global;           // one segment [0, n_all) of global keys read from kin/pin in pass 0
   int64_t n_all;
+  const int32_t* bag_of;  // non-null: the sorted values are BAGS (bag_of[position], read
+                          // coalesced in pass 0) instead of positions, so the block kernel
+                          // reads each lookup's bag in sorted order (no dependent gather)
 };
 
 template <int DB>
@@ -836,10 +839,10 @@ __device__ __forceinline__ void tiled_load(const TiledPass& a, const IdxT* __res
     if (a.first && !a.global) {
       const int64_t r = (int64_t)idx[p];
       key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
-      pos[u] = (int32_t)p;
+      pos[u] = a.bag_of ? a.bag_of[p] : (int32_t)p;
     } else {
       key[u] = a.kin[p];
-      pos[u] = a.pin[p];
+      pos[u] = (a.first && a.bag_of) ? a.bag_of[p] : a.pin[p];  // (global pass 0: pin[p] = p)
     }
   }
 }
@@ -1087,11 +1090,12 @@ template <typename IdxT, typename OffT, int DB>
 void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base, int T, int B,
                        int J, int bits, uint32_t* k_a, int32_t* p_a, uint32_t* k_out,
                        int32_t* p_out, uint32_t* hist, uint32_t sentinel, int32_t* err,
-                       int off_bits, hipStream_t st) {
+                       int off_bits, const int32_t* bag_of, hipStream_t st) {
   const int npass = (bits + DB - 1) / DB;
   TiledPass a{};
   a.row_base = row_base, a.T = T, a.B = B, a.J = J, a.hist = hist, a.sentinel = sentinel;
   a.err = err;
+  a.bag_of = bag_of;
   // ping-pong so the last pass lands in (k_out, p_out)
   uint32_t* kb[2] = {(npass & 1) ? k_out : k_a, (npass & 1) ? k_a : k_out};
   int32_t* pb[2] = {(npass & 1) ? p_out : p_a, (npass & 1) ? p_a : p_out};
@@ -1121,10 +1125,12 @@ void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base
 template <typename IdxT, typename OffT, int DB>
 bool launch_global_sort(const IdxT* idx, const OffT* off, const int64_t* row_base, int64_t N,
                         int bits, uint32_t* k_x, int32_t* p_x, uint32_t* k_y, int32_t* p_y,
-                        uint32_t* hist, uint32_t sentinel, int32_t* err, hipStream_t st) {
+                        uint32_t* hist, uint32_t sentinel, int32_t* err, const int32_t* bag_of,
+                        hipStream_t st) {
   const int npass = (bits + DB - 1) / DB;
   TiledPass a{};
   a.row_base = row_base, a.T = 1, a.B = 1, a.hist = hist, a.sentinel = sentinel, a.err = err;
+  a.bag_of = bag_of;
   a.J = (int)dlrm::ceil_div(N, (int64_t)kTile);
   a.global = 1;
   a.n_all = N;
@@ -1197,6 +1203,11 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
                      (int64_t)T * tiles_j * (1 << tdb) <=
                          (int64_t)2 * dlrm::ceil_div(N, (int64_t)CH) * D &&
                      !(tenv && strcmp(tenv, "0") == 0);
+  // the tiled and global sorts carry each lookup's bag (not its position) when no
+  // per-sample weights need the position: the block kernel then reads bags in sorted order
+  const char* benv = getenv("DLRM_TBE_SORT_BAGS");  // "0": sort positions (A/B only)
+  const int32_t* bags =
+      (!per_table && psw == nullptr && !(benv && strcmp(benv, "0") == 0)) ? w.bag_of : nullptr;
   if (per_table && presorted) {
     // this batch's per-table sort already ran inside dlrm_tbe_forward_presort
   } else if (per_table) {
@@ -1224,12 +1235,12 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
       launch_tiled_sort<IdxT, OffT, 10>(static_cast<const IdxT*>(idx),
                                         static_cast<const OffT*>(off), row_base, T, B,
                                         (int)tiles_j, end_bit, ki, w.pos_in, ko, w.pos_out, hist,
-                                        (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, st);
+                                        (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, bags, st);
     else
       launch_tiled_sort<IdxT, OffT, 8>(static_cast<const IdxT*>(idx),
                                        static_cast<const OffT*>(off), row_base, T, B,
                                        (int)tiles_j, end_bit, ki, w.pos_in, ko, w.pos_out, hist,
-                                       (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, st);
+                                       (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, bags, st);
     DLRM_LAUNCH_CHECK(name);
   } else {
     hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT, true>), dim3(keys_grid(T, B)),
@@ -1244,11 +1255,11 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
         tdb == 10 ? launch_global_sort<IdxT, OffT, 10>(static_cast<const IdxT*>(idx),
                                                        static_cast<const OffT*>(off), row_base, N,
                                                        end_bit, ki, w.pos_in, ko, w.pos_out, hist,
-                                                       (uint32_t)sentinel, err, st)
+                                                       (uint32_t)sentinel, err, bags, st)
                   : launch_global_sort<IdxT, OffT, 8>(static_cast<const IdxT*>(idx),
                                                       static_cast<const OffT*>(off), row_base, N,
                                                       end_bit, ki, w.pos_in, ko, w.pos_out, hist,
-                                                      (uint32_t)sentinel, err, st);
+                                                      (uint32_t)sentinel, err, bags, st);
     DLRM_LAUNCH_CHECK(name);
     if (!in_y) {  // an even pass count left the sorted pairs in the input buffers
       std::swap(w.keys_in, w.keys_out);
@@ -1274,10 +1285,11 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   if (blocks < 1) blocks = 1;
 #define LAUNCH2(LPB, VW, MV, MODE)                                                             \
   do {                                                                                         \
-    if (per_table)                                                                             \
+    if (per_table || bags)                                                                     \
       hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE, true>), dim3(blocks),  \
-                         dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw, \
-                         gout, gbs, N, lr, eps, sentinel, w.partial, ch);                      \
+                         dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out,                \
+                         per_table ? w.bag_of : w.pos_out, psw, gout, gbs, N, lr, eps,         \
+                         sentinel, w.partial, ch);                                             \
     else                                                                                       \
       hipLaunchKernelGGL((tbe_bwd_block_kernel<LPB, VW, MV, KeyT, MODE, false>), dim3(blocks), \
                          dim3(256), 0, st, W, mom, D, B, w.keys_out, w.pos_out, w.bag_of, psw, \
