@@ -523,7 +523,8 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
   const int gl = lane - g * LPB;
   const int nchunks = (int)(D / VW);
   const int64_t nblocks = (N + ch - 1) / ch;
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t wave_id = (int64_t)xcd_contiguous(blockIdx.x, gridDim.x) * (blockDim.x / kWave) +
+                          threadIdx.x / kWave;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
 
   for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {
@@ -675,7 +676,8 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
   const int gl = lane - g * LPB;
   const int nchunks = (int)(D / VW);
   const int64_t nblocks = (N + ch - 1) / ch;
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t wave_id = (int64_t)xcd_contiguous(blockIdx.x, gridDim.x) * (blockDim.x / kWave) +
+                          threadIdx.x / kWave;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
 
   for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {

@@ -162,4 +162,14 @@ __device__ __forceinline__ void tbe_fwd_body(
 
 
 
+// Bijective workgroup remap so each of the 8 XCDs (private 4 MiB L2 each; workgroups are
+// dealt to XCDs round-robin) runs a CONTIGUOUS range of workgroup ids: over a sorted lookup
+// array an XCD then works on one stretch of rows (C1: about one table), so the gradient
+// rows and weight rows it touches stay in its own L2.
+__device__ __forceinline__ int xcd_contiguous(int bid, int nwg) {
+  const int xcd = bid % 8;
+  const int q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
 }  // namespace
