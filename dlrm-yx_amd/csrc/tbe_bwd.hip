@@ -572,42 +572,58 @@ __global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
       }
     };
 
-    for (int64_t base = i0; base < i1; base += LPB) {
-      const int n = (int)((i1 - base) < LPB ? (i1 - base) : LPB);
-      KeyT my_key = sentinel;
-      int64_t my_off = -1;
-      float my_w = 1.f;
-      if (gl < n) {
-        my_key = keys[base + gl];
-        int32_t bag;
-        if constexpr (SB) {
-          bag = bag_of[base + gl];
-          if (psw) my_w = psw[pos[base + gl]];
-        } else {
-          const int32_t p = pos[base + gl];
-          bag = p >= 0 ? bag_of[p] : -1;
-          if (psw && p >= 0) my_w = psw[p];
-        }
-        if (bag >= 0) {
-          const int t = bag / B;
-          const int b = bag - t * B;
-          my_off = (int64_t)b * gbs + (int64_t)t * D;
+    // a sub-batch is SUB lookups (>= 16: narrow rows keep 16 gradient rows in flight), each
+    // lane of the group holding R = SUB / LPB of them
+    constexpr int SUB = LPB >= 16 ? LPB : 16;
+    constexpr int R = SUB / LPB;
+    for (int64_t base = i0; base < i1; base += SUB) {
+      const int n = (int)((i1 - base) < SUB ? (i1 - base) : SUB);
+      KeyT my_key[R];
+      int64_t my_off[R];
+      float my_w[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        my_key[r] = sentinel;
+        my_off[r] = -1;
+        my_w[r] = 1.f;
+        const int li = r * LPB + gl;
+        if (li < n) {
+          my_key[r] = keys[base + li];
+          int32_t bag;
+          if constexpr (SB) {
+            bag = bag_of[base + li];
+            if (psw) my_w[r] = psw[pos[base + li]];
+          } else {
+            const int32_t p = pos[base + li];
+            bag = p >= 0 ? bag_of[p] : -1;
+            if (psw && p >= 0) my_w[r] = psw[p];
+          }
+          if (bag >= 0) {
+            const int t = bag / B;
+            const int b = bag - t * B;
+            my_off[r] = (int64_t)b * gbs + (int64_t)t * D;
+          }
         }
       }
-      constexpr int U = LPB < CH ? LPB : CH;  // gradient rows in flight per group (ch >= CH)
+      constexpr int U = SUB < CH ? SUB : CH;  // gradient rows in flight per group (ch >= CH)
       for (int j = 0; j < n; j += U) {
         KeyT ku[U];
         int64_t ou[U];
         float wu[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int src = g * LPB + ((j + u) < LPB ? (j + u) : 0);
+          // lookup li of the sub-batch: lane li % LPB of the group, its register li / LPB
+          // (R > 1 only for LPB < 16, where U == SUB and j == 0: li is a constant)
+          static_assert(R == 1 || U == SUB, "narrow rows: one pass per sub-batch");
+          const int li = R == 1 ? ((j + u) < LPB ? (j + u) : 0) : u;
+          const int src = g * LPB + (R == 1 ? li : li % LPB);
+          const int rr = R == 1 ? 0 : li / LPB;
           if constexpr (sizeof(KeyT) == 8)
-            ku[u] = (KeyT)__shfl((long long)my_key, src, kWave);
+            ku[u] = (KeyT)__shfl((long long)my_key[rr], src, kWave);
           else
-            ku[u] = (KeyT)__shfl((int)my_key, src, kWave);
-          ou[u] = __shfl(my_off, src, kWave);
-          wu[u] = __shfl(my_w, src, kWave);
+            ku[u] = (KeyT)__shfl((int)my_key[rr], src, kWave);
+          ou[u] = __shfl(my_off[rr], src, kWave);
+          wu[u] = __shfl(my_w[rr], src, kWave);
           if (j + u >= n) ou[u] = -1;
         }
         V gv[U][MAXV];
