@@ -36,6 +36,7 @@
 // s = 0..S-1 would give - and applies the epilogue.  No reduce launch.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -1642,17 +1643,21 @@ __device__ __forceinline__ float frag_sum(const bf16x8& f) {
   return s;
 }
 
-template <int BM, int BN, bool A_KC, bool B_KC, bool RS>
+// WGM x WGN waves (2x2: one wave per SIMD; 4x2: two, each on a 32x32 / 16x32 sub-tile, so a
+// wave waiting on its DMA or LDS counters leaves the SIMD to its partner).  The plane
+// images' 1-KiB DMA blocks (A's 3 planes, then B's, block b at LDS byte b * 1024 of the
+// stage) are dealt round-robin over the waves: wave w issues blocks w, w + NW, ...
+template <int BM, int BN, bool A_KC, bool B_KC, bool RS, int WGM = 2, int WGN = 2>
 __device__ __forceinline__ void pipe_body_x6d(const GemmParams& p, int lb, char* smem) {
   constexpr int S = x6d_stages<BM, BN>();
-  constexpr int WGM = 2, WGN = 2, NW = 4;
+  constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1, "wave sub-tile");
   using IA = PImg<BM, A_KC>;
   using IB = PImg<BN, B_KC>;
   constexpr int STAGE = 3 * (IA::BYTES + IB::BYTES);
-  constexpr int NBA = 3 * IA::BLK, NBB = 3 * IB::BLK;
-  static_assert(NBA % NW == 0 && NBB % NW == 0, "DMA blocks per wave");
-  constexpr int NIA = NBA / NW, NIB = NBB / NW, NI = NIA + NIB;
+  constexpr int NBA = 3 * IA::BLK, NBB = 3 * IB::BLK, NB = NBA + NBB;
+  constexpr int NI_LO = NB / NW, NI_HI = (NB + NW - 1) / NW, NREM = NB % NW;
 
   const int tile = lb / p.splits;
   const int split = lb - tile * p.splits;
@@ -1667,6 +1672,7 @@ __device__ __forceinline__ void pipe_body_x6d(const GemmParams& p, int lb, char*
   const int kq = lane >> 4, l16 = lane & 15;
   const int wm0 = (wave / WGN) * WM, wn0 = (wave % WGN) * WN;
   const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
+  const bool hi = NREM == 0 || wave < NREM;  // this wave issues NI_HI blocks (else NI_LO)
 
   const int64_t a_ext = 2 * p.psa + (A_KC ? p.M * p.ldap : K8 * p.ldap);
   const int64_t b_ext = 2 * p.psb + (B_KC ? p.N * p.ldbp : K8 * p.ldbp);
@@ -1674,52 +1680,59 @@ __device__ __forceinline__ void pipe_body_x6d(const GemmParams& p, int lb, char*
       __builtin_amdgcn_make_buffer_rsrc((void*)p.Ap, (short)0, (int)(a_ext * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.Bp, (short)0, (int)(b_ext * 2), 0x00020000);
-  // per DMA instruction of this wave: byte offset at the split's first K-tile (-1: row /
-  // column outside the operand) and the chunk's k within a K-tile
-  int aoff[NIA], akp[NIA], boff[NIB], bkp[NIB];
+  // per DMA block of this wave: byte offset at the split's first K-tile (-1: row / column
+  // outside the operand, or no such block) and the chunk's k within a K-tile
+  int doff[NI_HI], dkp[NI_HI];
 #pragma unroll
-  for (int i = 0; i < NIA; ++i) {
-    const int b = wave * NIA + i;
-    const int q = b / IA::BLK, bb = b - q * IA::BLK;
-    int mn, k;
-    IA::src(bb * 64 + lane, mn, k);
-    const int64_t g = m0 + mn, gk = kbeg + k;
-    aoff[i] = g < p.M ? (int)(2 * (q * p.psa + (A_KC ? g * p.ldap + gk : gk * p.ldap + g))) : -1;
-    akp[i] = k;
-  }
-#pragma unroll
-  for (int i = 0; i < NIB; ++i) {
-    const int b = wave * NIB + i;
-    const int q = b / IB::BLK, bb = b - q * IB::BLK;
-    int mn, k;
-    IB::src(bb * 64 + lane, mn, k);
-    const int64_t g = n0 + mn, gk = kbeg + k;
-    boff[i] = g < p.N ? (int)(2 * (q * p.psb + (B_KC ? g * p.ldbp + gk : gk * p.ldbp + g))) : -1;
-    bkp[i] = k;
+  for (int i = 0; i < NI_HI; ++i) {
+    const int b = wave + NW * i;
+    doff[i] = -1;
+    dkp[i] = 0;
+    if (b < NBA) {
+      const int q = b / IA::BLK, bb = b - q * IA::BLK;
+      int mn, k;
+      IA::src(bb * 64 + lane, mn, k);
+      const int64_t g = m0 + mn, gk = kbeg + k;
+      doff[i] = g < p.M ? (int)(2 * (q * p.psa + (A_KC ? g * p.ldap + gk : gk * p.ldap + g)))
+                        : -1;
+      dkp[i] = k;
+    } else if (b < NB) {
+      const int q = (b - NBA) / IB::BLK, bb = (b - NBA) - q * IB::BLK;
+      int mn, k;
+      IB::src(bb * 64 + lane, mn, k);
+      const int64_t g = n0 + mn, gk = kbeg + k;
+      doff[i] = g < p.N ? (int)(2 * (q * p.psb + (B_KC ? g * p.ldbp + gk : gk * p.ldbp + g)))
+                        : -1;
+      dkp[i] = k;
+    }
   }
   const int a_step = A_KC ? 2 * kBK : (int)(2 * kBK * p.ldap);
   const int b_step = B_KC ? 2 * kBK : (int)(2 * kBK * p.ldbp);
   const int krem = (int)(kend - kbeg);
   // DMA of K-tile t into stage t % S; chunks past the split's K range (and tiles t >= nk)
-  // load zeros (out-of-descriptor offset), so every wave issues the same count
+  // load zeros (out-of-descriptor offset); a wave's block count is fixed for the kernel
   auto issue = [&](int t) {
     char* st = smem + (t % S) * STAGE;
 #pragma unroll
-    for (int i = 0; i < NIA; ++i) {
-      const int b = wave * NIA + i;
-      const bool ok = aoff[i] >= 0 && t * kBK + akp[i] < krem;
-      dma16(ra, reinterpret_cast<const float*>(st + (b / IA::BLK) * IA::BYTES +
-                                               (b % IA::BLK) * 1024),
-            ok ? aoff[i] + t * a_step : 0x7ffffff0);
+    for (int i = 0; i < NI_HI; ++i) {
+      const int b = wave + NW * i;  // uniform
+      if (i < NI_LO || hi) {
+        const bool isa = b < NBA;
+        const bool ok = doff[i] >= 0 && t * kBK + dkp[i] < krem;
+        const int off = ok ? doff[i] + t * (isa ? a_step : b_step) : 0x7ffffff0;
+        if (isa)
+          dma16(ra, reinterpret_cast<const float*>(st + b * 1024), off);
+        else
+          dma16(rb, reinterpret_cast<const float*>(st + b * 1024), off);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < NIB; ++i) {
-      const int b = wave * NIB + i;
-      const bool ok = boff[i] >= 0 && t * kBK + bkp[i] < krem;
-      dma16(rb, reinterpret_cast<const float*>(st + 3 * IA::BYTES + (b / IB::BLK) * IB::BYTES +
-                                               (b % IB::BLK) * 1024),
-            ok ? boff[i] + t * b_step : 0x7ffffff0);
-    }
+  };
+  auto wait_landed = [&](auto deep) {  // deep: tiles still allowed in flight after this one
+    constexpr int D = decltype(deep)::value;
+    if (hi)
+      wait_vm<D * NI_HI>();
+    else
+      wait_vm<D * NI_LO>();
   };
   struct Frag {
     bf16x8 q[3];
@@ -1766,14 +1779,14 @@ __device__ __forceinline__ void pipe_body_x6d(const GemmParams& p, int lb, char*
   Frag ca[FM], cb[FN], na[FM], nb[FN];
 #pragma unroll
   for (int t = 0; t < S - 1; ++t) issue(t);
-  wait_vm<(S - 2) * NI>();       // tile 0 landed (this wave)
+  wait_landed(std::integral_constant<int, S - 2>());  // tile 0 landed (this wave)
   __builtin_amdgcn_s_barrier();  // (a bare barrier: __syncthreads' fence would drain the DMAs)
   asm volatile("" ::: "memory");
   read(0, ca, cb);
   auto step = [&](int t, const Frag (&a)[FM], const Frag (&b)[FN], Frag (&a2)[FM],
                   Frag (&b2)[FN]) {
     products(0, 3, a, b);
-    wait_vm<(S - 3) * NI>();       // tile t+1 landed (this wave)
+    wait_landed(std::integral_constant<int, S - 3>());  // tile t+1 landed (this wave)
     __builtin_amdgcn_s_barrier();  // every wave's has; every wave is done with tile t-1's stage
     asm volatile("" ::: "memory");
     issue(t + S - 1);  // into tile t-1's stage
@@ -1923,8 +1936,8 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_group6L_kernel(const G
 
 // The same grouped launch on the pre-split body (pipe_body_x6d): LDS from the dynamic
 // segment (96 or 144 KiB: one workgroup per CU).
-template <int BM, int BN, int KINDS>
-__global__ __launch_bounds__(256, 1) void gemm_group6d_kernel(const GemmGroup g) {
+template <int BM, int BN, int KINDS, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_group6d_kernel(const GemmGroup g) {
   extern __shared__ __attribute__((aligned(1024))) char smem6d[];
   const int b = blockIdx.x;
   int q = 0;
@@ -1937,15 +1950,15 @@ __global__ __launch_bounds__(256, 1) void gemm_group6d_kernel(const GemmGroup g)
   if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
   const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
   if constexpr ((KINDS & 1) != 0)
-    if (kind == 0) return pipe_body_x6d<BM, BN, true, true, false>(p, lb, smem6d);
+    if (kind == 0) return pipe_body_x6d<BM, BN, true, true, false, WGM, WGN>(p, lb, smem6d);
   if constexpr ((KINDS & 2) != 0)
-    if (kind == 1) return pipe_body_x6d<BM, BN, true, false, false>(p, lb, smem6d);
+    if (kind == 1) return pipe_body_x6d<BM, BN, true, false, false, WGM, WGN>(p, lb, smem6d);
   if constexpr ((KINDS & 4) != 0)
-    if (kind == 2) return pipe_body_x6d<BM, BN, false, false, false>(p, lb, smem6d);
+    if (kind == 2) return pipe_body_x6d<BM, BN, false, false, false, WGM, WGN>(p, lb, smem6d);
   if constexpr ((KINDS & 8) != 0)
-    if (kind == 3) return pipe_body_x6d<BM, BN, false, true, false>(p, lb, smem6d);
+    if (kind == 3) return pipe_body_x6d<BM, BN, false, true, false, WGM, WGN>(p, lb, smem6d);
   if constexpr ((KINDS & 16) != 0)
-    if (kind == 4) return pipe_body_x6d<BM, BN, false, false, true>(p, lb, smem6d);
+    if (kind == 4) return pipe_body_x6d<BM, BN, false, false, true, WGM, WGN>(p, lb, smem6d);
 }
 
 // X [rows][cols] fp32 -> planes [3][rows][ldp] bf16, 8 elements per thread (columns
@@ -2356,17 +2369,18 @@ int f32_body(int plan_dma) {
   return plan_dma ? kBodyDma : kBodyReg;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WGM, int WGN>
 int launch_x6d_all(const GemmGroup& g, hipStream_t st) {
   constexpr int SM = x6d_smem_bytes<BM, BN>();
   static bool attr = false;
   if (!attr) {
-    DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, 31>,
+    DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, 31, WGM, WGN>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SM),
                   "dlrm_gemm_f32 (x6d)");
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, 31>), dim3(g.total), dim3(256), SM, st, g);
+  hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, 31, WGM, WGN>), dim3(g.total),
+                     dim3(WGM * WGN * 64), SM, st, g);
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32 (x6d)");
   return DLRM_OK;
 }
@@ -2428,18 +2442,18 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   case M_: {                                                                               \
     static bool attr = false;                                                              \
     if (!attr) {                                                                           \
-      DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, M_>,      \
+      DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, M_, WGM, WGN>, \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, SM),   \
                     "dlrm_gemm_f32 (x6d)");                                                \
       attr = true;                                                                         \
     }                                                                                      \
-    hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, M_>), grid, block, SM, st, g);         \
+    hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, M_, WGM, WGN>), grid, block, SM, st, g); \
     break;                                                                                 \
   }
     switch (kinds) {
       K_(0) K_(1) K_(2) K_(4) K_(16) K_(2 | 16) K_(2 | 4)
       default:
-        return launch_x6d_all<BM, BN>(g, st);
+        return launch_x6d_all<BM, BN, WGM, WGN>(g, st);
     }
 #undef K_
   } else if constexpr (BODY == kBodyX6L) {
@@ -2604,8 +2618,13 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
       if (q[i].mode == DLRM_GEMM_FULL) pl[i] = make_plan(1, q[i].K);
   }
   if (t.x6 == 3) {  // pre-split planes
-    if (t.bm == 128) return launch_group<128, 64, kBodyX6D>(m, q, pl, ws, ws_bytes, st);
-    return launch_group<64, 64, kBodyX6D>(m, q, pl, ws, ws_bytes, st);
+    // 4x2 waves (two per SIMD) by default; DLRM_X6D_WAVES=4: the 2x2 layout (A/B)
+    if (env_int("DLRM_X6D_WAVES", 8) == 4) {
+      if (t.bm == 128) return launch_group<128, 64, kBodyX6D>(m, q, pl, ws, ws_bytes, st);
+      return launch_group<64, 64, kBodyX6D>(m, q, pl, ws, ws_bytes, st);
+    }
+    if (t.bm == 128) return launch_group<128, 64, kBodyX6D, 4, 2>(m, q, pl, ws, ws_bytes, st);
+    return launch_group<64, 64, kBodyX6D, 4, 2>(m, q, pl, ws, ws_bytes, st);
   }
   // 128x128 split-bf16 on 2x4 waves (64x32 per wave, two waves per SIMD; the 2x2 layout,
   // one wave per SIMD, measured 1.15x slower: profiles/r03_x6l_ab.txt)
