@@ -2369,16 +2369,25 @@ int f32_body(int plan_dma) {
   return plan_dma ? kBodyDma : kBodyReg;
 }
 
+// The x6d kernels' dynamic LDS (> 64 KiB) must be opted into once per kernel and DEVICE
+// (`mask`: one bit per device ordinal; idempotent, so a benign race between host threads).
+inline int x6d_smem_optin(const void* fn, int bytes, unsigned long long& mask) {
+  int dev = 0;
+  DLRM_HIP_CALL(hipGetDevice(&dev), "dlrm_gemm_f32 (x6d)");
+  const unsigned long long bit = dev < 64 ? (1ull << dev) : 0ull;
+  if (bit && (mask & bit)) return DLRM_OK;
+  DLRM_HIP_CALL(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes),
+                "dlrm_gemm_f32 (x6d)");
+  mask |= bit;
+  return DLRM_OK;
+}
+
 template <int BM, int BN, int WGM, int WGN>
 int launch_x6d_all(const GemmGroup& g, hipStream_t st) {
   constexpr int SM = x6d_smem_bytes<BM, BN>();
-  static bool attr = false;
-  if (!attr) {
-    DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, 31, WGM, WGN>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, SM),
-                  "dlrm_gemm_f32 (x6d)");
-    attr = true;
-  }
+  static unsigned long long mask = 0;
+  const int rc = x6d_smem_optin((const void*)gemm_group6d_kernel<BM, BN, 31, WGM, WGN>, SM, mask);
+  if (rc != DLRM_OK) return rc;
   hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, 31, WGM, WGN>), dim3(g.total),
                      dim3(WGM * WGN * 64), SM, st, g);
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32 (x6d)");
@@ -2440,13 +2449,10 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
     constexpr int SM = x6d_smem_bytes<BM, BN>();
 #define K_(M_)                                                                              \
   case M_: {                                                                               \
-    static bool attr = false;                                                              \
-    if (!attr) {                                                                           \
-      DLRM_HIP_CALL(hipFuncSetAttribute((const void*)gemm_group6d_kernel<BM, BN, M_, WGM, WGN>, \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, SM),   \
-                    "dlrm_gemm_f32 (x6d)");                                                \
-      attr = true;                                                                         \
-    }                                                                                      \
+    static unsigned long long mask = 0;                                                    \
+    const int rc =                                                                         \
+        x6d_smem_optin((const void*)gemm_group6d_kernel<BM, BN, M_, WGM, WGN>, SM, mask);  \
+    if (rc != DLRM_OK) return rc;                                                          \
     hipLaunchKernelGGL((gemm_group6d_kernel<BM, BN, M_, WGM, WGN>), grid, block, SM, st, g); \
     break;                                                                                 \
   }
