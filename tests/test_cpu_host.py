@@ -39,6 +39,10 @@ def test_abi_rejects_bad_arguments_without_gpu():
         _lib.call("dlrm_tbe_forward", None, 4, None, 1, 1, None, 16, None, 32, None, None, 4,
                   None, None)
     assert e.value.code == 1
+    # split-bf16 planes: the pitch must hold whole 16-B chunks (checked before any launch)
+    with pytest.raises(_lib.DLRMHipError) as e:
+        _lib.call("dlrm_split_planes", None, 4, 7, 7, None, 7, 28, None)
+    assert e.value.code == 1
     # workspace queries are pure host arithmetic
     assert _lib.query("dlrm_tbe_backward_workspace_size", 53248, 54063992, 128) > 53248 * 20
     assert _lib.query("dlrm_gemm_f32_workspace_size", 1, 0, 1024, 1024, 2048) > 0
@@ -135,3 +139,19 @@ def test_gemm_partial_split_counts_are_normalized_or_rejected():
     with pytest.raises(_lib.DLRMHipError) as e:  # rejected on the host, before any launch
         _lib.call("dlrm_gemm_f32_group", 1, ctypes.cast(arr, ctypes.c_void_p), None, 0, None)
     assert e.value.code == 1 and "normalized" in str(e.value)
+
+
+def test_planes_host_api_checks_without_gpu():
+    """ops.split_planes / gemm_problem plane arguments are validated on the host: device
+    tensors only, bf16 [3, rows, ld] planes with unit inner stride."""
+    import torch
+    from dlrm_hip import ops
+    with pytest.raises(ValueError, match="device tensors"):
+        ops.split_planes(torch.zeros(4, 8))
+    P = torch.zeros(3, 4, 8, dtype=torch.bfloat16)
+    assert ops._plane_args(None) == (None, 0, 0)
+    assert ops._plane_args(P) == (P.data_ptr(), 8, 32)
+    with pytest.raises(ValueError, match="bf16"):
+        ops._plane_args(torch.zeros(3, 4, 8))
+    with pytest.raises(ValueError, match="bf16"):
+        ops._plane_args(P[:2])
