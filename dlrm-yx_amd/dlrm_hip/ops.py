@@ -186,13 +186,23 @@ def tbe_forward_presort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B
                         max_lookups_per_table: int, out: Optional[torch.Tensor] = None,
                         out_batch_stride: Optional[int] = None,
                         per_sample_weights: Optional[torch.Tensor] = None,
-                        error_flag: Optional[torch.Tensor] = None, bottom=None) -> torch.Tensor:
+                        error_flag: Optional[torch.Tensor] = None, bottom=None,
+                        lookup: bool = True) -> Optional[torch.Tensor]:
     """tbe_forward + this batch's backward sort in one launch (dlrm_tbe_forward_presort);
     follow with tbe_backward(..., workspace, presorted=True).  ``bottom``: an mlp_chain
-    (the bottom MLP forward) run as a third role of the same launch."""
+    (the bottom MLP forward) run as a third role of the same launch.
+
+    ``lookup=False``: the sort-only launch (the C-ABI's ``out = NULL``): no pooled output
+    is allocated or written, the lookup is done by its consumer (the gather-fused dot
+    interaction); returns None.  Only valid where the per-table sort applies (the library
+    returns DLRM_ERR_UNSUPPORTED otherwise)."""
     _check_cuda(weights, row_base, indices, offsets, workspace, per_sample_weights)
     D = weights.shape[1]
-    if out is None:
+    if not lookup:
+        if out is not None:
+            raise ValueError("tbe_forward_presort: lookup=False takes no out tensor")
+        out_batch_stride = T * D
+    elif out is None:
         out = torch.empty((B, T, D), dtype=torch.float32, device=weights.device)
         out_batch_stride = T * D
     elif out_batch_stride is None:

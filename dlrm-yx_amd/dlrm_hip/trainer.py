@@ -602,7 +602,7 @@ class DLRMTrainer:
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
                                             batch.max_per_table, out=None if gather else out,
-                                            error_flag=self.tbe_error_flag)
+                                            error_flag=self.tbe_error_flag, lookup=not gather)
                 elif self.T_local > 0:
                     ops.tbe_forward(self.weights, self.row_base, self.T_phys, B, idx, off,
                                     out=out, error_flag=self.tbe_error_flag)
@@ -626,7 +626,8 @@ class DLRMTrainer:
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
                                             batch.max_per_table, out=out,
-                                            error_flag=self.tbe_error_flag, bottom=chain)
+                                            error_flag=self.tbe_error_flag, bottom=chain,
+                                            lookup=not gather)
                     if self.qr_active:
                         self._qr_combine(bufs, B)
                 return

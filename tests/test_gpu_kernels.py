@@ -203,6 +203,71 @@ def test_tbe_forward_presort_matches_separate_sort(ops, mode, invalid, idx_dtype
     assert f0 == f1 == (ops.TBE_ERR_INDEX if invalid else 0)
 
 
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
+@pytest.mark.parametrize("invalid", [False, True])
+@pytest.mark.parametrize("with_bottom", [False, True])
+def test_tbe_presort_sort_only_matches_separate_sort(ops, mode, invalid, with_bottom):
+    """The sort-only presort launch (C-ABI out = NULL, ops lookup=False: the lookup is left
+    to the gather-fused interaction) followed by tbe_backward(presorted=True) applies the
+    same update, bit for bit, as the self-sorting backward; it writes no pooled output
+    and (with a bottom chain) the chain's output equals dlrm_mlp_chain_forward's."""
+    torch.manual_seed(12)
+    rows, D, B = [3, 5000, 4, 700, 1, 90000, 17], 128, 1024
+    T = len(rows)
+    lo = [torch.arange(B) for _ in rows]
+    li = [torch.randint(0, n, (B,)) for n in rows]
+    if invalid:
+        li[2][9] = 77
+    off, idx = O.batched_csr(lo, li)
+    idx, off = idx.to(torch.int32).to(dev), off.to(torch.int32).to(dev)
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    G = torch.randn(B, T, D, device=dev)
+    W0 = torch.randn(sum(rows), D, device=dev)
+    mom0 = torch.rand(sum(rows), device=dev)
+    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), sum(rows), D),
+                     dtype=torch.uint8, device=dev)
+    chain = layers = layers2 = None
+    if with_bottom:
+        X, layers = _mlp_setup(B, [13, 512, 256, 128])
+        layers2 = [(w, y.clone(), k) for w, y, k in layers]
+        chain = ops.mlp_chain(X, layers)
+        ops.mlp_chain_forward(ops.mlp_chain(X.clone(), layers2))
+    res = []
+    for pre in (False, True):
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ws.zero_()
+        if pre:
+            r = ops.tbe_forward_presort(W0, row_base, T, B, idx, off, ws, B, error_flag=flag,
+                                        bottom=chain, lookup=False)
+            assert r is None
+        W = W0.clone()
+        mom = mom0.clone()
+        ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8, momentum=mom,
+                         workspace=ws, max_lookups_per_table=B, error_flag=flag, presorted=pre)
+        res.append((W.cpu(), mom.cpu(), flag.item()))
+    (w0, m0, f0), (w1, m1, f1) = res
+    assert torch.equal(w0, w1) and torch.equal(m0, m1)
+    assert f0 == f1 == (ops.TBE_ERR_INDEX if invalid else 0)
+    if with_bottom:
+        torch.cuda.synchronize()
+        for (_, y1, _), (_, y2, _) in zip(layers, layers2):
+            assert torch.equal(y1, y2)
+
+
+def test_tbe_presort_sort_only_rejected_without_per_table_bound(ops):
+    """out = NULL needs the per-table sort: with no lookup bound the library refuses
+    (DLRM_ERR_UNSUPPORTED) instead of silently running a lookup into nothing."""
+    rows, D, B = [10, 20], 16, 8
+    off = torch.arange(0, 2 * B + 1, dtype=torch.int32, device=dev)
+    idx = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+    row_base = torch.tensor([0, 10, 30], dtype=torch.int64, device=dev)
+    W = torch.randn(30, D, device=dev)
+    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), 30, D), dtype=torch.uint8,
+                     device=dev)
+    with pytest.raises(Exception, match="needs the per-table sort"):
+        ops.tbe_forward_presort(W, row_base, 2, B, idx, off, ws, 0, lookup=False)
+
+
 def test_tbe_out_of_range_flag(ops):
     W = torch.randn(10, 8, device=dev)
     row_base = torch.tensor([0, 10], dtype=torch.int64, device=dev)

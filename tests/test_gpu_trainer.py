@@ -471,8 +471,12 @@ def test_gather_fused_step_matches_pooled_path(graph):
         tr = DLRMTrainer(cfg, device=dev, seed=11)
         tr.fuse_gather = fuse
         batches = [tr.synthetic_batch(512, 1, seed=s) for s in range(3)]
+        poison = None
         if graph:
             tr.step(batches[0])  # eager warm-up step (allocations), then capture
+            if fuse:  # the gather-fused step must never write the pooled E
+                poison = tr._bufs[(512, 512)]["E"]
+                poison.fill_(float("nan"))
             run = tr.capture(batches[0])
             for b in batches:
                 for src, dst in zip((b.X, b.offsets, b.indices, b.target),
@@ -482,9 +486,15 @@ def test_gather_fused_step_matches_pooled_path(graph):
                         dst.copy_(src)
                 run()
         else:
-            for b in batches:
+            for i, b in enumerate(batches):
                 tr.step(b)
+                if fuse and i == 0:
+                    poison = tr._bufs[(512, 512)]["E"]
+                    poison.fill_(float("nan"))
         assert tr.gather_fused == fuse
+        if fuse:  # sort-only lookup launch: E untouched, no other [B, T, D] buffer made
+            torch.cuda.synchronize()
+            assert bool(torch.isnan(poison).all())
         torch.cuda.synchronize()
         tr.check_errors()
         res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),

@@ -1,18 +1,19 @@
 #!/bin/bash
-# Round-3 GPU sessions (one stage per gpurun call):
-#   bash tools/gpu_r03_final.sh tests   - pytest -m gpu (per-test timeout) + smoke()
-#   bash tools/gpu_r03_final.sh bench   - default bench line + rocprofv3 kernel trace + PMC
-#   bash tools/gpu_r03_final.sh configs - bench lines of C1 (small), C2 (kaggle), C4
+# Round-4 GPU sessions (one stage per gpurun call):
+#   bash tools/gpu_r04.sh tests   - pytest -m gpu (per-test timeout) + smoke()
+#   bash tools/gpu_r04.sh bench   - default bench line + rocprofv3 kernel trace + PMC
+#   bash tools/gpu_r04.sh configs - bench lines of C1 (small), C2 (kaggle), C4
 set -o pipefail
 STAGE=$1
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/r03final
+OUT=$ROOT/gpurun_out/${OUTNAME:-r04}
 mkdir -p "$OUT"
 cd "$ROOT" || exit 1
 case $STAGE in
 tests)
+  # optional: K="expr" selects a subset (pytest -k)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-    -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -20 "$OUT/pytest_gpu.log"; exit 1; }
+    -p no:cacheprovider ${K:+-k "$K"} > "$OUT/pytest_gpu.log" 2>&1 || { tail -20 "$OUT/pytest_gpu.log"; exit 1; }
   tail -2 "$OUT/pytest_gpu.log"
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
     || { tail -5 "$OUT/smoke.log"; exit 1; }
@@ -40,7 +41,7 @@ configs)
   done
   ;;
 esac
-# (pmc only: bash tools/gpu_r03_final.sh pmc)
+# (pmc only: bash tools/gpu_r04.sh pmc)
 if [ "$STAGE" = pmc ]; then
   cd /tmp && export TMPDIR=/tmp
   for C in FETCH_SIZE WRITE_SIZE; do
