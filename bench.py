@@ -428,6 +428,54 @@ def skew_rate(tr, c, B, uniform_ms, steps=200, warmup=20, nb=10, a=1.05):
         return {"error": repr(e)}
 
 
+def comm_timing(tr, Bl: int, B: int, reps: int = 20):
+    """Multi-GPU only: the step's three collectives timed on their own, on the step's own
+    buffers and splits (after the timed loop; the all-reduce then scrambles the gradient
+    bucket, which nothing reads any more): the pooled-embedding all-to-all forward
+    ([B, T_r*D] -> rank-major [B/W, T*D], All2All_Req extend_distributed.py:405-444), its
+    reverse (All2All_Wait.backward :489-508) and the dense all-reduce (DDP :1626-1633).
+    HIP events on the current stream around `reps` blocking collectives; per-rank values
+    are gathered so rank 0 reports every rank (the slowest rank bounds the step)."""
+    import torch.distributed as dist
+    bufs = tr._bufs[(Bl, B)]
+    send, recv = tr._split_sizes(Bl)
+    pg = tr.pg
+
+    def t(fn):
+        fn()
+        torch.cuda.synchronize()
+        dist.barrier(group=pg)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps * 1000.0
+
+    a2a_f = t(lambda: dist.all_to_all_single(bufs["recv"], bufs["E"].view(-1)[:sum(send)],
+                                             recv, send, group=pg))
+    a2a_b = t(lambda: dist.all_to_all_single(bufs["dE"].view(-1)[:sum(send)], bufs["drecv"],
+                                             send, recv, group=pg))
+    ar = t(lambda: dist.all_reduce(tr.grads, group=pg))
+    mine = torch.tensor([a2a_f, a2a_b, ar, 4.0 * sum(send), 4.0 * sum(recv)], dtype=torch.float64,
+                        device=tr.dev)
+    allv = [torch.zeros_like(mine) for _ in range(tr.world)]
+    dist.all_gather(allv, mine, group=pg)
+    rows = [v.tolist() for v in allv]
+    ar_bytes = 4 * tr.grads.numel()
+    return {"reps": reps, "a2a_fwd_us": [round(r[0], 2) for r in rows],
+            "a2a_bwd_us": [round(r[1], 2) for r in rows],
+            "allreduce_us": [round(r[2], 2) for r in rows],
+            "a2a_send_bytes": [int(r[3]) for r in rows], "a2a_recv_bytes": [int(r[4]) for r in rows],
+            "allreduce_bytes": ar_bytes,
+            "allreduce_busbw_gbs": round(2 * (tr.world - 1) / tr.world * ar_bytes
+                                         / (max(r[2] for r in rows) * 1e-6) / 1e9, 1),
+            "note": "each collective alone, blocking, on the step's buffers; in the step the "
+                    "forward all-to-all overlaps the bottom MLP, the reverse the bottom-MLP "
+                    "backward and the all-reduce the embedding backward"}
+
+
 def socket0_physical_cores(limit: int):
     """One hardware thread per physical core of CPU package 0, within this process's allowed
     CPUs (bench/dlrm_s_benchmark.sh:20-25 binds `numactl --physcpubind=<socket 0 physical
@@ -547,6 +595,8 @@ def main():
                     help="setup: ms of a model-independent 4096^3 GEMM loop before the warm-up "
                          "steps, so the clocks have left their idle state (tools/ramp_probe.py)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
+    ap.add_argument("--bot-sched", default="", help="A/B: bottom-MLP backward schedule "
+                    "(partial | full | chain; default: the trainer's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -589,6 +639,8 @@ def main():
                         qr_operation=qr["operation"] if qr else "mult",
                         qr_threshold=qr["threshold"] if qr else 200)
     tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, process_group=pg, seed=1)
+    if args.bot_sched:
+        tr.bot_sched = args.bot_sched
     nb = 10  # the reference cycles 10 pre-generated batches (dlrm_data_pytorch.py:631)
     batches = [tr.synthetic_batch(B, c["L"], seed=100 + i) for i in range(nb)]
     torch.cuda.synchronize()
@@ -708,13 +760,37 @@ def main():
         b_ms = tot.get("tbe_bwd", 0.0)
         if f_ms > 0 and b_ms > 0:
             emb_roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                        "fwd_achieved": round(fwd_bytes / (f_ms * 1e-3) / 1e9, 1),
-                        "fwd_frac": round(fwd_bytes / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "fwd_bytes": fwd_bytes, "fwd_us": round(f_ms * 1000.0, 2),
                         "bwd_achieved_upper": round(bwd_bytes / (b_ms * 1e-3) / 1e9, 1),
                         "bwd_bytes_upper": bwd_bytes, "bwd_us": round(b_ms * 1000.0, 2),
-                        "fwd_note": "fwd_us is the step's lookup launch, which also runs the "
-                                    "backward's index sort and the bottom MLP forward"}
+                        "gather_fused": bool(tr.gather_fused)}
+            if tr.gather_fused:
+                # one-hot batches: the lookup launch only sorts (and runs the bottom MLP);
+                # the rows are gathered by the interaction forward, which also reads x and
+                # writes R: the gather's bytes are attributed to that kernel's time
+                i_ms = tot.get("interaction_fwd", 0.0)
+                D_ = c["D"]
+                F_ = tr.T_phys + 1
+                n_look = tr.T_phys * B * c["L"]
+                i_bytes = n_look * (4 * D_ + 4) + Bl * 4 * (D_ + D_ + F_ * (F_ - 1) // 2)
+                emb_roof.update({
+                    "lookup_launch_us": round(f_ms * 1000.0, 2),
+                    "lookup_launch_note": "sort-only lookup launch (dlrm_tbe_forward_presort "
+                                          "out=NULL) + the bottom MLP forward role",
+                    "fwd_bytes": fwd_bytes,
+                    "fwd_in_interaction_us": round(i_ms * 1000.0, 2),
+                    "fwd_in_interaction_bytes": i_bytes,
+                    "fwd_achieved": round(i_bytes / (i_ms * 1e-3) / 1e9, 1) if i_ms else None,
+                    "fwd_frac": round(i_bytes / (i_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                    if i_ms else None,
+                    "fwd_note": "the gather runs inside interaction_fwd (dlrm_interact_dot_"
+                                "forward_gather): bytes = gathered rows + indices + x + R"})
+            else:
+                emb_roof.update({
+                    "fwd_achieved": round(fwd_bytes / (f_ms * 1e-3) / 1e9, 1),
+                    "fwd_frac": round(fwd_bytes / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "fwd_bytes": fwd_bytes, "fwd_us": round(f_ms * 1000.0, 2),
+                    "fwd_note": "fwd_us is the step's lookup launch, which also runs the "
+                                "backward's index sort (and the bottom MLP forward)"})
         if rank == 0 and world == 1 and emb_roof is not None:
             emb_roof.update(gather_rooflines(tr, batches[0], B, c, dev))
             try:
@@ -731,6 +807,13 @@ def main():
     skew = None
     if world == 1 and not args.no_kernel_timing and not args.no_graph:
         skew = skew_rate(tr, c, B, uniform_ms=elapsed / args.steps * 1000.0)
+
+    comm = None
+    if world > 1:
+        try:
+            comm = comm_timing(tr, B // world, B)
+        except Exception as e:  # noqa: BLE001 - reported; the headline line must still print
+            comm = {"error": repr(e)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -749,8 +832,9 @@ def main():
                        "lookups_per_bag": c["L"], "bot": c["bot"], "top": ln_top,
                        "optimizer": c["optimizer"], "qr": c.get("qr"),
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
-                       "hip_graph": use_graph},
+                       "hip_graph": use_graph, "bot_sched": tr.bot_sched},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,
+            "comm": comm,
             "loss_before_timed": loss_first, "loss_last": loss, "lr": c["lr"],
             "roofline": roofline,
             "embedding_roofline": emb_roof,

@@ -12,6 +12,11 @@ namespace dlrm {
 // Thread-local last-error message (dlrm_last_error()).
 void set_error(const char* fmt, ...);
 
+// Thread-local plan overrides of dlrm_set_tuning (autotuning sweeps and coverage tests of
+// the alternative tiles / block lengths / sort paths); 0 = the planner's choice.  The
+// library reads no environment variables.
+int64_t tuning(int key);
+
 inline hipStream_t as_stream(dlrm_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 constexpr int kWave = 64;  // CDNA wavefront width (never 32)

@@ -193,141 +193,6 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_mfma(int B, int F, int D
   }
 }
 
-// ---------------------------------------------- MFMA backward (compile-time D) --
-// One wave per sample (persistent over samples): the sample's F x D rows are staged into
-// LDS with coalesced float4 loads (pitch D+4), then dT = S T with S = G + G^T built per
-// lane straight from dR (lane (i, h) owns S row i, columns [16h, 16h+16)) and the B
-// operand T[k][n0 + l32] read from LDS (conflict-free ds_read_b32).
-template <int D>
-__global__ __launch_bounds__(256) void interact_dot_bwd_v2(int B, int F, FeatArgs fa, int self,
-                                                           const float* __restrict__ gout,
-                                                           int64_t ld_g, GradArgs ga) {
-  constexpr int DP = D + 4;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int h = lane >> 5;
-  const int l32 = lane & 31;
-  float* Tl = lds + wave * 32 * DP;
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += nw) {
-    for (int q = lane; q < F * (D / 4); q += 64) {
-      const int f = q / (D / 4), c = q - f * (D / 4);
-      const float4 v = *reinterpret_cast<const float4*>(fa.ptr[f] + b * fa.bs[f] + 4 * c);
-      *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) = v;
-    }
-    // rows F..FK-1 of T must be zero (they meet S's zero columns, but 0 * garbage = NaN)
-    const int FK = (F + 1) & ~1;
-    for (int q = lane; q < (32 - F) * (D / 4); q += 64) {
-      const int f = F + q / (D / 4), c = q - (f - F) * (D / 4);
-      *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    const float* grow = gout + b * ld_g;
-    // S row l32, columns k = 16h + s (s < 16): symmetric scatter of dR's pair gradients
-    float sv[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int k = 16 * h + s;
-      const int i = l32;
-      float v = 0.f;
-      if (i < F && k < F) {
-        if (i == k)
-          v = self ? 2.f * grow[D + pair_index(i, i, true)] : 0.f;
-        else
-          v = grow[D + (i > k ? pair_index(i, k, self) : pair_index(k, i, self))];
-      }
-      sv[s] = v;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    (void)FK;
-#pragma unroll
-    for (int n0 = 0; n0 < D; n0 += 32) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const int n = n0 + l32;
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int k = 16 * h + s;
-        const float bv = (n < D) ? Tl[k * DP + n] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sv[s], bv, acc, 0, 0, 0);
-      }
-      if (n < D) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (i < F) {
-            float v = acc[r];
-            if (i == 0) v += grow[n];
-            ga.ptr[i][b * ga.bs[i] + n] = v;
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// ---------------------------------------------- MFMA forward (compile-time D) --
-// Register-only, one wave per sample: lane (f, h) loads its own operand row slice
-// T[f][h*D/2 ..] with float4 loads straight from HBM and feeds it as BOTH operands of
-// the 32x32x2 MFMA (T T^T); two accumulator chains alternate over k.  The tril gather
-// and the [x, Z] concat are fused into the tile epilogue.
-template <int D>
-__global__ __launch_bounds__(256) void interact_dot_fwd_v3(int B, int F, FeatArgs fa, int self,
-                                                           float* __restrict__ out,
-                                                           int64_t ld_out) {
-  constexpr int KH = D / 2;
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int h = lane >> 5;
-  const int l32 = lane & 31;
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const bool rowok = l32 < F;
-  // per-lane feature row base, selected from the uniform kernel arguments (a lane-indexed
-  // kernarg access would be a waterfall loop per use)
-  const float* base = fa.ptr[0];
-  int64_t bst = fa.bs[0];
-#pragma unroll
-  for (int f = 1; f < 32; ++f) {
-    if (f < F && l32 == f) {
-      base = fa.ptr[f];
-      bst = fa.bs[f];
-    }
-  }
-  for (int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += nw) {
-    const float* trow = base + b * bst + h * KH;
-    float4 v[KH / 4];
-#pragma unroll
-    for (int c = 0; c < KH / 4; ++c) {
-      v[c] = *reinterpret_cast<const float4*>(trow + 4 * c);
-      if (!rowok) v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    f32x16 acc0, acc1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
-#pragma unroll
-    for (int c = 0; c < KH / 4; ++c) {
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[c].x, v[c].x, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[c].y, v[c].y, acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[c].z, v[c].z, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[c].w, v[c].w, acc1, 0, 0, 0);
-    }
-    float* orow = out + b * ld_out;
-    if (l32 == 0) {  // x = row 0: the two half-wave lanes hold its two halves
-#pragma unroll
-      for (int c = 0; c < KH / 4; ++c) *reinterpret_cast<float4*>(orow + h * KH + 4 * c) = v[c];
-    }
-    const int j = l32;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (i < F && (self ? i >= j : i > j)) orow[D + pair_index(i, j, self)] = acc0[r] + acc1[r];
-    }
-  }
-}
-
 // ------------------------------------ LDS-staged kernels (compile-time D) --
 // One wave per sample, four waves per workgroup stepping through the batch together.
 // Loads and stores move whole feature rows as float4 with C4 = D/4 lanes per row, so a
@@ -734,10 +599,11 @@ extern "C" int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D,
   int rc = fill_feat(fa, F, feat_ptrs, feat_bstrides, name);
   if (rc) return rc;
   hipStream_t st = dlrm::as_stream(stream);
-  // v4 (LDS-staged, coalesced rows) for the compile-time D; v3 / v1 otherwise
+  // v4 (LDS-staged, coalesced rows) for the compile-time D; the runtime-D MFMA kernel or
+  // the elementwise one otherwise
   const bool fast = F <= 32 && (D == 16 || D == 32 || D == 64 || D == 128) &&
-                    aligned_feats(fa, F) && !getenv("DLRM_INTERACT_V1");
-  if (fast && !getenv("DLRM_INTERACT_V3")) {
+                    aligned_feats(fa, F);
+  if (fast) {
     const int width = D + npairs;
     const int vec_out = ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 4 == 0) ? 1 : 0;
     const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
@@ -747,16 +613,6 @@ extern "C" int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D,
                      self_interaction ? 1 : 0, out, ld_out, width, vec_out, GatherArgs{})
     if (D == 16) L4(16); else if (D == 32) L4(32); else if (D == 64) L4(64); else L4(128);
 #undef L4
-    DLRM_LAUNCH_CHECK(name);
-    return DLRM_OK;
-  }
-  if (fast) {
-    const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 4096);
-#define L3(DD)                                                                          \
-  hipLaunchKernelGGL(interact_dot_fwd_v3<DD>, dim3(grid), dim3(256), 0, st, B, F, fa,    \
-                     self_interaction ? 1 : 0, out, ld_out)
-    if (D == 16) L3(16); else if (D == 32) L3(32); else if (D == 64) L3(64); else L3(128);
-#undef L3
     DLRM_LAUNCH_CHECK(name);
     return DLRM_OK;
   }
@@ -794,14 +650,14 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
   rc = fill_grad(ga, F, grad_ptrs, grad_bstrides, name);
   if (rc) return rc;
   hipStream_t st = dlrm::as_stream(stream);
-  // v3 (LDS-staged T and dR, coalesced rows, ReLU' fused) for the compile-time D;
-  // v2 / v1 otherwise (ReLU' then as a separate pass)
+  // v3 (LDS-staged T and dR, coalesced rows, ReLU' fused) for the compile-time D; the
+  // runtime-D MFMA kernel or the elementwise one otherwise (ReLU' then as a separate pass)
   const bool fast = F <= 32 && (D == 16 || D == 32 || D == 64 || D == 128) &&
-                    aligned_feats(fa, F) && !getenv("DLRM_INTERACT_V1");
+                    aligned_feats(fa, F);
   bool grads_aligned = true;
   for (int f = 0; f < F; ++f)
     if ((reinterpret_cast<uintptr_t>(ga.ptr[f]) & 15) || (ga.bs[f] & 3)) grads_aligned = false;
-  if (fast && grads_aligned && !getenv("DLRM_INTERACT_V2")) {
+  if (fast && grads_aligned) {
     const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
     const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
     const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
@@ -814,26 +670,16 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
     DLRM_LAUNCH_CHECK(name);
     return DLRM_OK;
   }
-  if (fast) {
-    const size_t lds = 4 * 32 * (size_t)(D + 4) * sizeof(float);
-    const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 2048);
-#define L2(DD)                                                                               \
-  hipLaunchKernelGGL(interact_dot_bwd_v2<DD>, dim3(grid), dim3(256), lds, st, B, F, fa,       \
-                     self_interaction ? 1 : 0, grad_out, ld_gout, ga)
-    if (D == 16) L2(16); else if (D == 32) L2(32); else if (D == 64) L2(64); else L2(128);
-#undef L2
+  const size_t per_wave = (size_t)(F * (D + 1) + 32 * 33) * sizeof(float);
+  const int wpb = waves_for(per_wave);
+  if (F <= 32 && wpb > 0) {
+    hipLaunchKernelGGL(interact_dot_bwd_mfma, dim3(grid_for(B, wpb)), dim3(64 * wpb),
+                       per_wave * wpb, st, B, F, D, fa,
+                       self_interaction ? 1 : 0, grad_out, ld_gout, ga);
   } else {
-    const size_t per_wave = (size_t)(F * (D + 1) + 32 * 33) * sizeof(float);
-    const int wpb = waves_for(per_wave);
-    if (F <= 32 && wpb > 0) {
-      hipLaunchKernelGGL(interact_dot_bwd_mfma, dim3(grid_for(B, wpb)), dim3(64 * wpb),
-                         per_wave * wpb, st, B, F, D, fa,
-                         self_interaction ? 1 : 0, grad_out, ld_gout, ga);
-    } else {
-      const int64_t n = (int64_t)B * F * D;
-      hipLaunchKernelGGL(interact_dot_bwd_generic, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0, st,
-                         B, F, D, fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga);
-    }
+    const int64_t n = (int64_t)B * F * D;
+    hipLaunchKernelGGL(interact_dot_bwd_generic, dim3(dlrm::ceil_div(n, 256)), dim3(256), 0, st,
+                       B, F, D, fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga);
   }
   DLRM_LAUNCH_CHECK(name);
   if (relu_x) {

@@ -6,7 +6,8 @@
 //
 // Pipeline (all on the caller's stream, no host sync, graph-capturable):
 //  1. keys:    per lookup l, global row row_base[t] + idx[l] (or a sentinel) and its bag;
-//  2. sort:    stable LSD radix sort of (row, l) pairs on ceil(log2 rows) bits (hipCUB);
+//  2. sort:    stable LSD radix sort of (row, l) pairs on ceil(log2 rows) bits (hand-written:
+//              per-table LDS sort, tiled per-table passes, or device-wide passes; below);
 //  3. blocks:  the sorted lookups are cut into fixed blocks of 64.  One lane-group per
 //              block walks them in order (row ids / grad-row offsets loaded coalesced and
 //              broadcast by wave shuffles, four gradient rows in flight), summing the
@@ -118,8 +119,6 @@ struct SegSortLds {
 // this lane) plus the wave's running count of that digit in LDS; one scan over the
 // (digit, wave) counts gives every element its destination.  Order inside a digit is
 // (wave, item, lane) = element order: stable.
-// PRB (timing probes, tools/tbe_bwd_bench.py): 1 = ranking only, 2 = ranking + scan
-template <int PRB = 0>
 __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
                                                int32_t (&pos)[kSegItems], int bits,
                                                SegSortLds& sm) {
@@ -154,11 +153,6 @@ __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
       if (r == c - 1) sm.cnt[d * CS + w] = base + c;  // last peer publishes
     }
     __syncthreads();
-    if constexpr (PRB == 1) {
-#pragma unroll
-      for (int u = 0; u < kSegItems; ++u) key[u] ^= rank[u] & 1 ? 0u : 0u;
-      continue;
-    }
     // exclusive scan of cnt in (digit, wave) order
     uint32_t v[CPT];
     uint32_t tsum = 0;
@@ -187,7 +181,6 @@ __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
       run += v[k];
     }
     __syncthreads();
-    if constexpr (PRB == 2) continue;
 #pragma unroll
     for (int u = 0; u < kSegItems; ++u) {
       const uint32_t dst = sm.cnt[dig[u] * CS + w] + rank[u];
@@ -205,7 +198,7 @@ __device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
   }
 }
 
-template <typename IdxT, typename OffT, int PRB = 0>
+template <typename IdxT, typename OffT>
 __device__ __forceinline__ void segsort_body(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
@@ -283,7 +276,7 @@ __device__ __forceinline__ void segsort_body(
     }
   }
   __syncthreads();  // bags complete
-  seg_radix_sort<PRB>(key, pos, bits, sm);
+  seg_radix_sort(key, pos, bits, sm);
 #pragma unroll
   for (int u = 0; u < kSegItems; ++u) {
     const int i = w * (kSegItems * 64) + u * 64 + l;
@@ -295,13 +288,13 @@ __device__ __forceinline__ void segsort_body(
   }
 }
 
-template <typename IdxT, typename OffT, int PRB = 0>
+template <typename IdxT, typename OffT>
 __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
     int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
   __shared__ SegSortLds sm;
-  segsort_body<IdxT, OffT, PRB>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of,
+  segsort_body<IdxT, OffT>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of,
                                 err, blockIdx.x, sm);
 }
 
@@ -343,6 +336,12 @@ __global__ __launch_bounds__(kPreThreads) void tbe_fwd_presort_kernel(
 __global__ __launch_bounds__(kMlpWaves * 64) void mlp_chain_kernel(const MlpChain mc) {
   __shared__ __attribute__((aligned(16))) float lds[kMlpLdsFloats];
   mlp_rows_body(mc, blockIdx.x, lds);
+}
+
+__global__ __launch_bounds__(kMlpWaves * 64) void mlp_chain_bwd_kernel(const MlpChain mc,
+                                                                       const MlpGrad mg) {
+  __shared__ __attribute__((aligned(16))) float lds[kMlpLdsFloats];
+  mlp_rows_bwd_body(mc, mg, blockIdx.x, lds);
 }
 
 // MODE_SGD_F16: exact SGD on fp16 weights (the fbgemm TBE's FP16 tables): the row is read
@@ -776,12 +775,6 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
   }
 }
 
-// DLRM_SEGSORT_PROBE (timing probes of the per-table sort; tools/tbe_bwd_bench.py only)
-inline int env_probe() {
-  const char* e = getenv("DLRM_SEGSORT_PROBE");
-  return e ? atoi(e) : 0;
-}
-
 // The per-table LDS sort applies (and dlrm_tbe_forward_presort can run it early).
 inline bool presort_applies(size_t key_bytes, int64_t max_seg, int64_t N) {
   return key_bytes == 4 && max_seg > 0 && max_seg <= kSegCap && N < (int64_t)0x7fffffff;
@@ -1099,8 +1092,6 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scatter_kernel(
 // DB-bit digits, passes over `bits` key bits (local rows <= total_rows): 10-bit digits when
 // they save a pass over 8-bit ones.
 inline int tiled_digit_bits(int bits) {
-  const char* e = getenv("DLRM_TBE_TILED_DB");  // A/B override: 8 or 10
-  if (e && (atoi(e) == 8 || atoi(e) == 10)) return atoi(e);
   return (bits + 9) / 10 < (bits + 7) / 8 ? 10 : 8;
 }
 
@@ -1215,30 +1206,21 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   // block kernel's partial buffer (free until the sort is done)
   const int64_t tiles_j = dlrm::ceil_div(max_seg > 0 ? max_seg : 1, (int64_t)kTile);
   const int tdb = tiled_digit_bits(end_bit);
-  const char* tenv = getenv("DLRM_TBE_TILED_SORT");  // "0": global sort (A/B only)
   const bool tiled = !per_table && sizeof(KeyT) == 4 && max_seg > kSegCap &&
                      N < (int64_t)0x7fffffff && (int64_t)T * tiles_j < (int64_t)INT32_MAX &&
                      (int64_t)T * tiles_j * (1 << tdb) <=
                          (int64_t)2 * dlrm::ceil_div(N, (int64_t)CH) * D &&
-                     !(tenv && strcmp(tenv, "0") == 0);
+                     dlrm::tuning(DLRM_TUNE_TBE_SORT) != 1;
   // the tiled and global sorts carry each lookup's bag (not its position) when no
   // per-sample weights need the position: the block kernel then reads bags in sorted order
-  const char* benv = getenv("DLRM_TBE_SORT_BAGS");  // "0": sort positions (A/B only)
-  const int32_t* bags =
-      (!per_table && psw == nullptr && !(benv && strcmp(benv, "0") == 0)) ? w.bag_of : nullptr;
+  const int32_t* bags = (!per_table && psw == nullptr) ? w.bag_of : nullptr;
   if (per_table && presorted) {
     // this batch's per-table sort already ran inside dlrm_tbe_forward_presort
   } else if (per_table) {
-    const int prb = env_probe();
-#define SEG(P)                                                                                  \
-  hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT, P>), dim3(T + 1), dim3(kSegThreads), 0, \
-                     st, static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base,   \
-                     T, B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),         \
-                     w.pos_out, w.bag_of, err)
-    if (prb == 1) SEG(1);
-    else if (prb == 2) SEG(2);
-    else SEG(0);
-#undef SEG
+    hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(kSegThreads), 0,
+                       st, static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base,
+                       T, B, N, (uint32_t)sentinel, reinterpret_cast<uint32_t*>(w.keys_out),
+                       w.pos_out, w.bag_of, err);
     DLRM_LAUNCH_CHECK(name);
   } else if (tiled) {
     hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT, false>), dim3(keys_grid(T, B)),
@@ -1294,9 +1276,9 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   const int64_t maxv = dlrm::ceil_div(nchunks, lpb);
   DLRM_REQUIRE(maxv <= 8, DLRM_ERR_UNSUPPORTED, "%s: D=%lld too large", name, (long long)D);
   const int gpw = 64 / lpb;
-  const char* chenv = getenv("DLRM_TBE_CH");  // A/B override: 16 or 64
   int ch = N >= kLongChN ? kLongCH : CH;
-  if (chenv && (atoi(chenv) == CH || atoi(chenv) == kLongCH)) ch = atoi(chenv);
+  const int64_t tch = dlrm::tuning(DLRM_TUNE_TBE_BLOCK);  // (sweeps / coverage tests)
+  if (tch == CH || tch == kLongCH) ch = (int)tch;
   const int64_t nblocks = dlrm::ceil_div(N, (int64_t)ch);
   int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(nblocks, gpw), 4);
   if (blocks > 8192) blocks = 8192;
@@ -1563,6 +1545,30 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
 extern "C" int dlrm_mlp_chain_supported(const dlrm_mlp_chain* chain) {
   MlpChain mc{};
   return mlp_chain_prepare(chain, mc);
+}
+
+extern "C" int dlrm_mlp_chain_backward(const dlrm_mlp_chain* chain, const float* g_last,
+                                       int64_t ld_g_last, float* const* g, const int64_t* ld_g,
+                                       dlrm_stream_t stream) {
+  const char* name = "dlrm_mlp_chain_backward";
+  MlpChain mc{};
+  DLRM_ARG(mlp_chain_prepare(chain, mc), "%s: unsupported chain", name);
+  if (chain->rows == 0 || chain->layers < 2) return DLRM_OK;
+  DLRM_ARG(g_last && ld_g_last >= chain->out_width[chain->layers - 1], "%s: bad g_last", name);
+  DLRM_ARG(g && ld_g, "%s: null gradient arrays", name);
+  MlpGrad mg{};
+  mg.Glast = g_last;
+  mg.ldgl = ld_g_last;
+  for (int l = 0; l + 1 < chain->layers; ++l) {
+    DLRM_ARG(g[l] && ld_g[l] >= chain->out_width[l], "%s: bad gradient buffer %d", name, l);
+    DLRM_ARG(g[l] != g_last, "%s: gradient buffer %d aliases g_last", name, l);
+    mg.G[l] = g[l];
+    mg.ldg[l] = ld_g[l];
+  }
+  hipLaunchKernelGGL(mlp_chain_bwd_kernel, dim3((unsigned)dlrm::ceil_div(chain->rows, kMlpRows)),
+                     dim3(kMlpWaves * 64), 0, dlrm::as_stream(stream), mc, mg);
+  DLRM_LAUNCH_CHECK(name);
+  return DLRM_OK;
 }
 
 extern "C" int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream) {

@@ -33,10 +33,7 @@ class GemmProblem(ctypes.Structure):
                 ("B", c_void_p), ("ldb", c_int64), ("C", c_void_p), ("ldc", c_int64),
                 ("epilogue", c_int32), ("bias", c_void_p), ("aux", c_void_p),
                 ("ld_aux", c_int64), ("ones_col", c_int64), ("mode", c_int32),
-                ("splits", c_int32), ("partial", c_void_p),
-                ("a_planes", c_void_p), ("lda_planes", c_int64), ("a_plane_stride", c_int64),
-                ("b_planes", c_void_p), ("ldb_planes", c_int64), ("b_plane_stride", c_int64),
-                ("c_planes", c_void_p), ("ldc_planes", c_int64), ("c_plane_stride", c_int64)]
+                ("splits", c_int32), ("partial", c_void_p)]
 
 
 MLP_MAX_LAYERS = 4
@@ -55,6 +52,8 @@ P = c_void_p
 SIGNATURES = {
     "dlrm_abi_version": (c_int32, []),
     "dlrm_last_error": (ctypes.c_char_p, []),
+    "dlrm_set_tuning": (c_int32, [c_int32, c_int64]),
+    "dlrm_get_tuning": (c_int64, [c_int32]),
     "dlrm_tbe_forward": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32, P, P,
                                    c_int64, P, P]),
     "dlrm_tbe_backward_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
@@ -81,6 +80,7 @@ SIGNATURES = {
     "dlrm_tbe_forward_rows": (c_int32, [P, c_int32, c_int64, c_int64, P, c_int32, c_int32, P,
                                         c_int32, P, c_int32, P, P, c_int64, P, P]),
     "dlrm_mlp_chain_forward": (c_int32, [P, P]),
+    "dlrm_mlp_chain_backward": (c_int32, [P, P, c_int64, P, P, P]),
     "dlrm_tbe_expand_grad": (c_int32, [c_int64, c_int32, c_int32, P, c_int32, c_int64, P, P,
                                        c_int64, P, P]),
     "dlrm_qr_split_indices": (c_int32, [P, c_int32, c_int64, c_int64, P, P, P]),
@@ -108,7 +108,6 @@ SIGNATURES = {
     "dlrm_gemm_f32_group_workspace_size": (c_size_t, [c_int32, P]),
     "dlrm_gemm_f32_group": (c_int32, [c_int32, P, P, c_size_t, P]),
     "dlrm_gemm_f32_splits": (c_int32, [P]),
-    "dlrm_split_planes": (c_int32, [P, c_int64, c_int64, c_int64, P, c_int64, c_int64, P]),
     "dlrm_gemm_f32_partial_bytes": (c_size_t, [c_int64, c_int64, c_int32]),
     "dlrm_colsum_workspace_size": (c_size_t, [c_int64, c_int64]),
     "dlrm_colsum_f32": (c_int32, [c_int64, c_int64, P, c_int64, P, c_float, P, c_int32, P,

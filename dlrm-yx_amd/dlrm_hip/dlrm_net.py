@@ -360,6 +360,18 @@ class DLRM_Net(nn.Module):
         # cat returns [B, F*d] (the shape the top MLP consumes)
         return HF.interact(self.arch_interaction_op, x, ly, self.arch_interaction_itself)
 
+    def flush_index_errors(self) -> None:
+        """Raise ops.TBEIndexError if the LAST lookup of any embedding module hit an index
+        outside its table.  With the default strict_indices="deferred" a module raises at
+        its next forward (one call late, no host sync per lookup); call this after the
+        final training / evaluation step so the last call is checked too."""
+        if not isinstance(self.emb_l, nn.Module):
+            return
+        for m in self.emb_l.modules():  # (includes emb_l itself)
+            chk = getattr(m, "tbe_errors", None)
+            if chk is not None:
+                chk.flush()
+
     # ----------------------------------------------------------- forward --
     def forward(self, dense_x, lS_o, lS_i):
         if ext_dist.my_size > 1:

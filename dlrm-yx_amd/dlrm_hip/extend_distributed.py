@@ -98,6 +98,25 @@ class All2AllInfo(object):
     pass
 
 
+class _Done(object):
+    """A completed request (the host-staged gloo exchange below is synchronous)."""
+
+    def wait(self):
+        return None
+
+
+def _all_to_all_single(out, inp, out_splits, in_splits):
+    """all_to_all_single, async.  Device tensors under gloo (several ranks sharing one GPU
+    in the tests, or a CPU rendezvous) go through host memory synchronously; under nccl
+    (RCCL over xGMI, the MI355X path) the exchange stays on the device and async."""
+    if out.is_cuda and dist.get_backend() == "gloo":
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+        out.copy_(o)
+        return _Done()
+    return dist.all_to_all_single(out, inp, out_splits, in_splits, async_op=True)
+
+
 class Request(object):
     def __init__(self):
         self.req = None
@@ -129,7 +148,7 @@ class All2All_Req(Function):
             inp = torch.cat([x.reshape(x.shape[0], -1) for x in inputs], dim=1).view(-1)
             out = inp.new_empty([a2a_info.global_table_num * a2a_info.local_batch_num *
                                  a2a_info.emb_dim])
-            req = dist.all_to_all_single(out, inp, tsl, bsl, async_op=True)
+            req = _all_to_all_single(out, inp, tsl, bsl)
             a2a_info.batch_split_lengths = bsl
             a2a_info.table_split_lengths = tsl
             myreq.req = req
@@ -180,8 +199,8 @@ class All2All_Wait(Function):
             go = torch.cat([g.contiguous().view(-1) for g in grad_outputs])
             gi = go.new_empty([a2a_info.batch_size * a2a_info.local_table_num *
                                a2a_info.emb_dim])
-            req = dist.all_to_all_single(gi, go, a2a_info.batch_split_lengths,
-                                         a2a_info.table_split_lengths, async_op=True)
+            req = _all_to_all_single(gi, go, a2a_info.batch_split_lengths,
+                                     a2a_info.table_split_lengths)
             myreq.req = req
             myreq.tensor = gi
             return (go,)
@@ -217,13 +236,16 @@ class AllGather(Function):
         ctx.local_start = sum(global_lengths[:my_rank])
         ctx.local_length = global_lengths[my_rank]
         input = input.contiguous()
+        staged = input.is_cuda and dist.get_backend() == "gloo"
+        src = input.cpu() if staged else input
         parts = []
         for length in global_lengths:
             shp = list(input.size())
             shp[dim] = length
-            parts.append(input.new_empty(shp))
-        dist.all_gather(parts, input)
-        return torch.cat(parts, dim=dim)
+            parts.append(src.new_empty(shp))
+        dist.all_gather(parts, src)
+        out = torch.cat(parts, dim=dim)
+        return out.to(input.device) if staged else out
 
     @staticmethod
     def backward(ctx, grad_output):

@@ -55,6 +55,7 @@ class HipEmbeddingBagList(nn.ModuleList):
     def __init__(self, modules: Sequence[nn.Module], weight_flat: Optional[torch.Tensor],
                  row_ranges: Sequence[tuple], plain_index: Sequence[int], D: int):
         super().__init__(modules)
+        ops.check_tbe_rows(row_ranges[-1][1] if row_ranges else 0, "HipEmbeddingBagList")
         self.weight_flat = weight_flat
         self.row_ranges = list(row_ranges)      # per plain table: (start, end) rows
         self.plain_index = list(plain_index)    # table ids of the plain tables
@@ -131,6 +132,7 @@ class TableBatchedEmbeddingBags(nn.Module):
         super().__init__()
         Es = [int(e) for e in num_embeddings]
         assert num_tables == len(Es), "num_tables must match num_embeddings"
+        ops.check_tbe_rows(sum(Es), "TableBatchedEmbeddingBags")
         if stochastic_rounding:
             raise ValueError("stochastic rounding applies to fp16 tables only (fp32 here)")
         self.T = num_tables
@@ -210,6 +212,7 @@ class SplitTableBatchedEmbeddingBags(nn.Module):
         self.eps = float(eps)
         self.row_format = ops.ROWS_F16
         total = int(sum(Es))
+        ops.check_tbe_rows(total, "SplitTableBatchedEmbeddingBags")
         w = torch.empty(total, self.D)
         self.row_ranges = []
         o = 0

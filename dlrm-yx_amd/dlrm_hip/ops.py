@@ -77,6 +77,35 @@ class DeferredErrorCheck:
         self.poll()
 
 
+# dlrm_tune_key (include/dlrm_hip.h): plan overrides for sweeps and coverage tests
+TUNE_KEYS = {"gemm_tile": 1, "gemm_split": 2, "tbe_block": 3, "tbe_sort": 4}
+
+
+class tuning:
+    """Context manager over dlrm_set_tuning (thread-local plan overrides; results stay
+    exact, only the plan changes), e.g. ``with ops.tuning(gemm_tile=64064, gemm_split=4):``
+    or ``tuning(tbe_block=64)``; the previous values are restored on exit."""
+
+    def __init__(self, **kw):
+        for k in kw:
+            if k not in TUNE_KEYS:
+                raise KeyError(f"unknown tuning key {k!r} (one of {sorted(TUNE_KEYS)})")
+        self.kw = kw
+        self.prev = {}
+
+    def __enter__(self):
+        lib = _lib.load()
+        for k, v in self.kw.items():
+            self.prev[k] = int(lib.dlrm_get_tuning(TUNE_KEYS[k]))
+            _lib.call("dlrm_set_tuning", TUNE_KEYS[k], int(v))
+        return self
+
+    def __exit__(self, *a):
+        for k, v in self.prev.items():
+            _lib.call("dlrm_set_tuning", TUNE_KEYS[k], int(v))
+        return False
+
+
 LOSS_MSE, LOSS_BCE = 0, 1
 QR_OPS = {"mult": 0, "add": 1, "concat": 2}
 
@@ -175,6 +204,35 @@ def mlp_chain_forward(chain, device=None) -> None:
     dev = device if device is not None else torch.cuda.current_device()
     _lib.call("dlrm_mlp_chain_forward", ctypes.cast(ctypes.byref(chain), ctypes.c_void_p),
               _stream(dev))
+
+
+def mlp_chain_backward(chain, g_last: torch.Tensor, grads, device=None) -> None:
+    """dlrm_mlp_chain_backward: the chain's data gradients in one launch.  ``g_last``:
+    dLoss/d(pre-activation of the last layer) [rows, >= out_width[-1]]; ``grads``: L-1
+    output tensors [rows, >= out_width[l]] (g_0 .. g_{L-2})."""
+    _check_cuda(g_last, *grads)
+    L = int(chain.layers)
+    if len(grads) != L - 1:
+        raise ValueError(f"mlp_chain_backward: {L - 1} gradient buffers expected")
+    ptrs = (ctypes.c_void_p * max(L - 1, 1))(*[g.data_ptr() for g in grads])
+    lds = (ctypes.c_int64 * max(L - 1, 1))(*[g.stride(0) for g in grads])
+    dev = device if device is not None else g_last.device
+    _lib.call("dlrm_mlp_chain_backward", ctypes.cast(ctypes.byref(chain), ctypes.c_void_p),
+              _p(g_last), g_last.stride(0), ctypes.cast(ptrs, ctypes.c_void_p),
+              ctypes.cast(lds, ctypes.c_void_p), _stream(dev))
+
+
+# the TBE backward's sort keys are 32-bit global rows (ABI v4): a table set that one
+# backward call serves must hold fewer rows (checked where tables are built, so a forward
+# is never accepted for a configuration the backward would refuse)
+TBE_MAX_ROWS = 0xFFFFFFFF - 1
+
+
+def check_tbe_rows(total_rows: int, what: str) -> None:
+    if int(total_rows) > TBE_MAX_ROWS:
+        raise ValueError(f"{what}: {int(total_rows)} rows in one table-batched buffer; the "
+                         f"embedding backward supports < 2^32 - 1 rows per call (shard the "
+                         f"tables over more ranks or modules)")
 
 
 # lookups per table the in-launch per-table sort handles (tbe_bwd.hip kSegCap)
@@ -515,53 +573,16 @@ def gemm_workspace_size(M: int, N: int, K: int, trans_a: bool = False,
 GEMM_FULL, GEMM_PARTIAL, GEMM_REDUCE = 0, 1, 2  # dlrm_gemm_mode
 
 
-def planes_empty(rows: int, cols: int, device) -> torch.Tensor:
-    """Zeroed split-bf16 planes [3, rows, roundup(cols, 8)] for an fp32 [rows, cols] matrix
-    (the padding columns stay zero: the GEMM reads k-contiguous rows up to roundup(K, 8))."""
-    return torch.zeros((3, rows, (cols + 7) // 8 * 8), dtype=torch.bfloat16, device=device)
-
-
-def split_planes(X: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """X (2-D fp32, unit inner stride) -> planes [3, rows, >= cols] bf16 with
-    X = P[0] + P[1] + P[2] exactly (dlrm_split_planes)."""
-    _check_cuda(X, out)
-    if X.dim() != 2 or X.stride(1) != 1 or X.dtype != torch.float32:
-        raise ValueError("split_planes: X must be 2-D fp32 with unit inner stride")
-    rows, cols = X.shape
-    if out is None:
-        out = planes_empty(rows, cols, X.device)
-    if (out.dim() != 3 or out.shape[0] != 3 or out.shape[1] < rows or out.stride(2) != 1
-            or out.dtype != torch.bfloat16 or out.stride(1) < cols):
-        raise ValueError("split_planes: out must be bf16 [3, >= rows, >= cols]")
-    _lib.call("dlrm_split_planes", _p(X), rows, cols, X.stride(0), _p(out), out.stride(1),
-              out.stride(0), _stream(X.device))
-    return out
-
-
-def _plane_args(P: Optional[torch.Tensor]):
-    if P is None:
-        return None, 0, 0
-    if P.dim() != 3 or P.shape[0] != 3 or P.dtype != torch.bfloat16 or P.stride(2) != 1:
-        raise ValueError("planes must be bf16 [3, rows, ld] with unit inner stride")
-    return P.data_ptr(), P.stride(1), P.stride(0)
-
-
 def gemm_problem(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False,
                  trans_b: bool = False, C: Optional[torch.Tensor] = None, alpha: float = 1.0,
                  epilogue: int = EPI_STORE, bias: Optional[torch.Tensor] = None,
                  aux: Optional[torch.Tensor] = None, ones_col: int = -1,
-                 partial: Optional[torch.Tensor] = None, splits: int = 0,
-                 a_planes: Optional[torch.Tensor] = None,
-                 b_planes: Optional[torch.Tensor] = None,
-                 c_planes: Optional[torch.Tensor] = None):
+                 partial: Optional[torch.Tensor] = None, splits: int = 0):
     """One dlrm_gemm_problem: C = epilogue(alpha * op(A) @ op(B)) with row-major 2-D
     operands (unit inner stride); ones_col >= 0 also writes C[:, ones_col] =
     epilogue(alpha * op(A).sum(1)) (a Linear bias gradient).  With ``partial`` the problem
     is a PARTIAL one: K split ``splits`` ways, raw partials into ``partial``, C untouched
-    until reduce_problem(...) runs in a later launch.  ``a_planes`` / ``b_planes``: the
-    split-bf16 planes of the stored A / B (split_planes; both or neither) - the GEMM then
-    runs on the bf16 matrix core from them; ``c_planes``: also split every written C
-    element into these planes.  Returns (struct, C)."""
+    until reduce_problem(...) runs in a later launch.  Returns (struct, C)."""
     _check_cuda(A, B, C, bias, aux)
     if A.stride(1) != 1 or B.stride(1) != 1:
         raise ValueError("gemm operands need unit inner stride")
@@ -584,8 +605,7 @@ def gemm_problem(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False,
                           aux.data_ptr() if aux is not None else None,
                           aux.stride(0) if aux is not None else 0, int(ones_col),
                           GEMM_PARTIAL if partial is not None else GEMM_FULL, int(splits),
-                          partial.data_ptr() if partial is not None else None,
-                          *_plane_args(a_planes), *_plane_args(b_planes), *_plane_args(c_planes))
+                          partial.data_ptr() if partial is not None else None)
     return pr, C
 
 

@@ -24,12 +24,12 @@ optimizer update.  Layout decisions (MI355X-first):
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
+from torch.autograd.profiler import record_function
 
 from . import ops
 from .sharders import shard
@@ -155,6 +155,7 @@ class DLRMTrainer:
         self.row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64,
                                      device=self.dev)
         self.total_rows = int(sum(rows))
+        ops.check_tbe_rows(self.total_rows, "DLRMTrainer (this rank's tables)")
         self.weights = torch.empty((max(self.total_rows, 1), D), dtype=torch.float32,
                                    device=self.dev)
         self.momentum = None
@@ -201,40 +202,30 @@ class DLRMTrainer:
         self.bot = self.layers[:self.n_bot]
         self.top = self.layers[self.n_bot:]
         self._bufs = {}
-        # Split-bf16 planes of the top MLP (one GPU, SGD fused into the backward): every top
-        # GEMM reads its operands as exact (h, m, l) bf16 planes and runs on the bf16 matrix
-        # core (dlrm_gemm_problem.a/b_planes); each producer writes the planes of what it
-        # writes (c_planes: forward activations, data gradients, the SGD-updated weights),
-        # two producers outside the GEMMs split theirs in one launch each (the interaction
-        # output R, the head's input gradient).  Opt-in (DLRM_GEMM_PLANES=1): measured
-        # slower than the exact-f32 path in the C3 step (profiles/r03_planes_*.txt).
-        self.use_planes = (os.environ.get("DLRM_GEMM_PLANES", "0") == "1" and world_size == 1
-                           and self.grads is None and len(self.top) > 1)
-        self.Wp = ([ops.planes_empty(L.N, L.Kp, self.dev) for L in self.top[:-1]]
-                   if self.use_planes else None)
         # independent kernels of a step run on a side stream (see step())
         self.concurrent = True
-        # which overlaps to use: "fwd" (bottom MLP || lookup), "top" (wgrad || next dgrad),
+        # which overlaps to use (attribute, A/B only): "fwd" (bottom MLP || lookup),
         # "bot" (bottom-MLP backward || embedding backward).  Off by default: measured on
         # MI355X, each cross-queue dependency in a replayed hipGraph costs ~10 us, more than
         # the overlap recovers at C3 (profiles/r01_overlap_ab.txt).
-        self.overlaps = set(os.environ.get("DLRM_OVERLAPS", "").split(","))
+        self.overlaps = set()
         self._side = torch.cuda.Stream(device=self.dev)
         self._tbe_ws: Optional[torch.Tensor] = None
         # run the embedding backward's per-table sort inside the lookup launch
-        # (dlrm_tbe_forward_presort); DLRM_TBE_PRESORT=0 sorts in the backward instead
-        self.tbe_presort = os.environ.get("DLRM_TBE_PRESORT", "1") != "0"
+        # (dlrm_tbe_forward_presort); False: the backward sorts itself
+        self.tbe_presort = True
         # MLP backward: a layer's split wgrad (partials only) in the same launch as its dgrad
-        self.group_wgrad = os.environ.get("DLRM_GROUP_WGRAD", "1") != "0"
-        self.full_last_wgrad = os.environ.get("DLRM_FULL_LAST_WGRAD", "0") == "1"
-        # bottom-MLP backward schedule: "partial" (split wgrads reduced in the next launch)
-        # or "full" (in-launch split-K, n_bot launches; bottom_bwd_full)
-        self.bot_sched = os.environ.get("DLRM_BOT_SCHED", "partial")
+        self.group_wgrad = True
+        self.full_last_wgrad = False
+        # bottom-MLP backward schedule: "partial" (split wgrads reduced in the next launch),
+        # "full" (in-launch split-K, n_bot launches; bottom_bwd_full) or "chain" (the data
+        # gradients in one row-block launch, then every wgrad in one grouped launch)
+        self.bot_sched = "partial"
         # one GPU: the bottom MLP forward as a role of the lookup launch (mlp_rows.hpp)
-        self.fuse_bottom = os.environ.get("DLRM_FUSE_BOTTOM", "1") != "0"
+        self.fuse_bottom = True
         # one GPU, one-hot batches: the dot interaction gathers the embedding rows itself
         # (dlrm_interact_dot_forward_gather); the lookup launch keeps only its sort role
-        self.fuse_gather = os.environ.get("DLRM_FUSE_GATHER", "1") != "0"
+        self.fuse_gather = True
         self.gather_fused = False  # set by the last step
         self.bottom_fused = False  # set by the last step
         # device TBE error bits (ops.TBE_ERR_*): out-of-range indices are skipped by the
@@ -266,14 +257,6 @@ class DLRMTrainer:
                 L.W.zero_()
                 L.W[:, :L.K].normal_(0.0, math.sqrt(2.0 / (L.N + L.K)), generator=g)
                 L.b.normal_(0.0, math.sqrt(1.0 / L.N), generator=g)
-        self._split_weight_planes()
-
-    def _split_weight_planes(self):
-        """(Re)derive the top weights' planes from the fp32 weights (after any host-side
-        write of the weights; the step itself keeps them in step)."""
-        if self.use_planes:
-            for L, P in zip(self.top[:-1], self.Wp):
-                ops.split_planes(L.W, out=P)
 
     def load_dense(self, mlp_params: Sequence[tuple], tables: Optional[Sequence] = None):
         """Copy (W [N,K], b [N]) per layer (bottom then top) and optionally GLOBAL tables."""
@@ -290,7 +273,6 @@ class DLRMTrainer:
                     if self.phys_kind[p] != 0:
                         src = src[self.phys_kind[p] - 1]
                     self.weights[s:e].copy_(torch.as_tensor(src))
-        self._split_weight_planes()
 
     @classmethod
     def from_oracle(cls, cfg: TrainerConfig, ref, device="cuda:0", **kw):
@@ -315,6 +297,28 @@ class DLRMTrainer:
         views = [self.weights[int(self.row_base[p].item()):int(self.row_base[p + 1].item())]
                  for p, jj in enumerate(self.phys_src) if jj == j]
         return views[0] if len(views) == 1 else tuple(views)
+
+    def table_momentum(self, t: int):
+        """RWSAdagrad row-wise momentum of local table t (a (quotient, remainder) pair for a
+        QR table), the reference's optimizer state['momentum'] (optim/rwsadagrad.py:80-84)."""
+        if self.momentum is None:
+            raise ValueError("no row-wise momentum: optimizer is not rwsadagrad")
+        j = self.local_tables.index(t)
+        views = [self.momentum[int(self.row_base[p].item()):int(self.row_base[p + 1].item())]
+                 for p, jj in enumerate(self.phys_src) if jj == j]
+        return views[0] if len(views) == 1 else tuple(views)
+
+    def dense_adagrad_state(self):
+        """Per layer (sum of squared W gradients [N, K], of b [N]): the dense branch's
+        state['sum'] of RWSAdagrad (optim/rwsadagrad.py:116-119)."""
+        if self.adagrad_sum is None:
+            raise ValueError("no Adagrad state: optimizer is not rwsadagrad")
+        out, o = [], 0
+        for L in self.layers:
+            S = self.adagrad_sum[o:o + L.N * L.Kp].view(L.N, L.Kp)
+            out.append((S[:, :L.K].detach().clone(), S[:, L.K].detach().clone()))
+            o += L.N * L.Kp
+        return out
 
     # ------------------------------------------------------------- batches --
     @property
@@ -511,12 +515,6 @@ class DLRMTrainer:
         bufs["prob"] = torch.zeros(Bl, **f32)
         bufs["dz"] = torch.zeros(Bl, **f32)
         bufs["loss"] = torch.zeros(1, **f32)
-        if self.use_planes:  # planes of R, the top activations (1-columns: h = 1) and g
-            bufs["Rp"] = ops.planes_empty(Bl, self.ldR, dev)
-            bufs["top_actp"] = [ops.planes_empty(Bl, L.Np, dev) for L in self.top[:-1]]
-            for P, L in zip(bufs["top_actp"], self.top[:-1]):
-                P[0, :, L.N] = 1.0
-            bufs["gp"] = [ops.planes_empty(Bl, wmax, dev) for _ in range(3)]
         self._bufs[key] = bufs
         return bufs
 
@@ -591,8 +589,13 @@ class DLRMTrainer:
         def side_if(flag, s1):
             return torch.cuda.stream(s1) if flag else _NullCtx()
 
+        # the reference's profiler phase names (dlrm_s_pytorch.py:692-721, 171, 1923), so a
+        # torch.profiler trace of this step lines up with one of the reference's
+        emb_sizes = "-".join(str(int(cfg.ln_emb[t])) for t in self.local_tables)
+
         def lookup():  # embeddings (full batch, local tables)
-            with prof("tbe_fwd"):
+            with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
+                    prof("tbe_fwd"):
                 if self.T_local > 0:
                     idx, off = st["csr"] = self._phys_csr(batch, B)
                     out = bufs["P"] if self.qr_active else bufs["E"]
@@ -611,16 +614,18 @@ class DLRMTrainer:
 
         def bottom_fwd():
             h = batch.X
-            for L, out in zip(self.bot, bufs["bot_act"]):
-                self._gemm([self._fwd(L, h, out)], side=c_fwd)
-                h = out
+            with record_function("module::forward_pass::bottom_mlp"):
+                for L, out in zip(self.bot, bufs["bot_act"]):
+                    self._gemm([self._fwd(L, h, out)], side=c_fwd)
+                    h = out
 
         def fwd_single():  # one GPU: bottom MLP || lookup
             chain = self._bottom_chain(batch, bufs) if presort and not c_fwd else None
             self.bottom_fused = chain is not None
             if chain is not None:
                 # the bottom MLP forward runs as a role of the lookup launch
-                with prof("tbe_fwd"):
+                with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
+                        record_function("module::forward_pass::bottom_mlp"), prof("tbe_fwd"):
                     idx, off = st["csr"] = self._phys_csr(batch, B)
                     out = None if gather else bufs["P"] if self.qr_active else bufs["E"]
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
@@ -642,7 +647,7 @@ class DLRMTrainer:
 
         def middle():  # interaction, top MLP, head, top backward, interaction backward
             x, feats = self._features(bufs, Bl)
-            with prof("interaction_fwd"):
+            with record_function("module::forward_pass::interaction"), prof("interaction_fwd"):
                 if gather:  # one-hot lookup fused: rows read straight from the tables
                     ops.interact_forward_gather(x, self.weights, self.row_base, batch.indices,
                                                 cfg.arch_interaction_itself, out=bufs["R"],
@@ -650,24 +655,18 @@ class DLRMTrainer:
                 else:
                     ops.interact_forward(cfg.arch_interaction_op, x, feats,
                                          cfg.arch_interaction_itself, out=bufs["R"])
-                pl = self.use_planes
-                if pl:
-                    ops.split_planes(bufs["R"], out=bufs["Rp"])
             h = bufs["R"]
-            hp = bufs["Rp"] if pl else None
-            nt = len(self.top) - 1
-            for li, (L, out) in enumerate(zip(self.top[:-1], bufs["top_act"])):
-                # the last GEMM layer's output feeds only the head (fp32): no planes
-                op = bufs["top_actp"][li] if pl and li < nt - 1 else None
-                self._gemm([self._fwd(L, h, out, hp, self.Wp[li] if pl else None, op)])
-                h, hp = out, op
+            with record_function("module::forward_pass::top_mlp"):
+                for L, out in zip(self.top[:-1], bufs["top_act"]):
+                    self._gemm([self._fwd(L, h, out)])
+                    h = out
             last = self.top[-1]
             # head: last layer + sigmoid + loss + dz + input grad + [dw | db] (bias folded:
             # [h | 1] . [w | b]) in two launches; the update follows every read of w
             G = bufs["g"]
             gi = 0
             gview = G[gi][:, :last.Kp]
-            with prof("head"):
+            with record_function("## Loss Compute ##"), prof("head"):
                 ops.head_step(h[:, :last.Kp], last.W[0, :last.Kp], batch.target,
                               cfg.loss_function, cfg.loss_threshold, 1.0, prob=bufs["prob"],
                               dz=bufs["dz"], loss_out=bufs["loss"], dX=gview,
@@ -676,29 +675,26 @@ class DLRMTrainer:
                               lr=lr if fused_opt else 0.0,
                               workspace=self._ws_head_step(Bl, last.Kp))
             g = gview
-            GP = bufs["gp"] if pl else [None] * 3
-            if pl:  # the head's input gradient as planes for the top backward
-                with prof("head"):
-                    ops.split_planes(g[:, :self.top[-2].N], out=GP[gi])
             rq = []  # reduce jobs riding on the next launch; G rotates over three buffers
+            bwd = record_function("## Backward ##")
+            bwd.__enter__()
             for li in range(len(self.top) - 2, -1, -1):
                 L = self.top[li]
                 inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
-                inpp = (bufs["top_actp"][li - 1] if li > 0 else bufs["Rp"]) if pl else None
                 gn = (gi + 1) % 3
-                pk = dict(gp=GP[gi], wp=self.Wp[li], outp=GP[gn] if li > 0 else None) \
-                    if pl else {}
-                dg = self._dgrad(L, g, inp if li > 0 else None, G[gn], **pk)
-                wk = dict(planes=(GP[gi], inpp, self.Wp[li])) if pl else {}
-                w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li), **wk)
+                dg = self._dgrad(L, g, inp if li > 0 else None, G[gn])
+                w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li))
                 if r is not None and self.group_wgrad:
                     # the split wgrad only writes partials (its update rides on the next
                     # launch's reduce job), so it may run beside the dgrad reading W
                     self._gemm([dg, w] + rq)
+                    rq = [r]
                 else:
+                    # an unsplit wgrad updates W_l in its epilogue: it rides on the NEXT
+                    # launch (dgrad of layer l-1 reads W_{l-1}, not W_l; its g_l buffer
+                    # is not overwritten there: G rotates over three)
                     self._gemm([dg] + rq)
-                    self._gemm([w])
-                rq = [r] if r is not None else []
+                    rq = [w]
                 g, gi = G[gn], gn
             _, gfeats = self._features(bufs, Bl, grad=True)
             with prof("interaction_bwd"):  # + the backward of the bottom MLP's last ReLU
@@ -710,6 +706,7 @@ class DLRMTrainer:
                     ops.interact_backward(cfg.arch_interaction_op, x, feats, g[:, :self.num_int],
                                           cfg.arch_interaction_itself, grad_x=bufs["gx"],
                                           grad_ly=gfeats, relu_x=True)
+            bwd.__exit__(None, None, None)
             st["rq"] = rq
 
         def bottom_bwd_full():
@@ -732,7 +729,27 @@ class DLRMTrainer:
                 else:
                     self._gemm(pending + [w] + rq)
 
+        def bottom_bwd_chain(chain):
+            """Bottom-MLP backward in two launches: the data gradients of every layer in one
+            row-block launch (dlrm_mlp_chain_backward, gradients kept in LDS between layers),
+            then every layer's weight gradient (in-launch split-K, SGD fused on one GPU)
+            in one grouped GEMM launch together with the top MLP's pending reduce job."""
+            rq = st.pop("rq")
+            gs = [bufs["gb"][li][:, :self.bot[li].N] for li in range(self.n_bot - 1)]
+            ops.mlp_chain_backward(chain, bufs["gx"], gs)
+            probs = []
+            for li in range(self.n_bot):
+                g = gs[li] if li < self.n_bot - 1 else bufs["gx"]
+                inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
+                probs.append(self._wgrad(self.bot[li], g, inp, fused_opt, lr))
+            self._gemm(probs + rq)
+
         def bottom_bwd(s1=None):
+            if self.bot_sched == "chain" and not c_bot and len(self.bot) + len(st["rq"]) <= 6:
+                chain = self._bottom_chain(batch, bufs, backward=True)
+                if chain is not None and self.n_bot >= 2:
+                    with prof("gemm"):
+                        return bottom_bwd_chain(chain)
             if self.bot_sched == "full" and not c_bot and fused_opt:
                 return bottom_bwd_full()
             rq = st.pop("rq")
@@ -772,6 +789,7 @@ class DLRMTrainer:
                                      max_lookups_per_table=batch.max_per_table,
                                      error_flag=self.tbe_error_flag, presorted=presort)
 
+        @record_function("## Backward ##")
         def backward_single():  # one GPU: bottom backward || embedding backward
             s0, s1 = streams()
             if c_bot:
@@ -787,7 +805,7 @@ class DLRMTrainer:
                 s0.wait_stream(s1)
 
         def dense_update():
-            with prof("dense_update"):
+            with record_function("## Backward ##"), prof("dense_update"):
                 scale = 1.0 / self.world
                 if cfg.optimizer == "sgd":
                     ops.sgd_update(self.params, self.grads, lr * scale)
@@ -812,13 +830,13 @@ class DLRMTrainer:
             ("gpu", lookup),
             ("comm", lambda: st.__setitem__("a2a", self._alltoall_fwd(bufs, Bl))),
             ("gpu", bottom_fwd),
-            ("comm", lambda: st.pop("a2a").wait()),
+            ("comm", lambda: st.pop("a2a").wait()),  # All2All_Wait (extend_distributed.py:489)
             ("gpu", middle),
             ("comm", lambda: st.__setitem__("a2a", self._alltoall_bwd(bufs, Bl))),
-            ("gpu", bottom_bwd),
+            ("gpu", record_function("## Backward ##")(bottom_bwd)),
             ("comm", lambda: st.__setitem__("ar", self._allreduce_dense())),
             ("comm", lambda: st.pop("a2a").wait()),
-            ("gpu", emb_bwd),
+            ("gpu", record_function("## Backward ##")(emb_bwd)),
             ("comm", lambda: st.pop("ar").wait()),
             ("gpu", dense_update),
             ("comm", done),
@@ -902,65 +920,52 @@ class DLRMTrainer:
 
     # -------------------------------------------------------------- pieces --
     @staticmethod
-    def _fwd(L: _Layer, h, out, hp=None, wp=None, outp=None):
-        """[h | 1] . [W | b]^T with ReLU (bias folded into the last k-term); with planes
-        (hp, wp) on the bf16 matrix core, outp = the planes of out (or None)."""
-        return ops.gemm_problem(h[:, :L.Kp], L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU,
-                                a_planes=hp, b_planes=wp, c_planes=outp)[0]
+    def _fwd(L: _Layer, h, out):
+        """[h | 1] . [W | b]^T with ReLU (bias folded into the last k-term)."""
+        return ops.gemm_problem(h[:, :L.Kp], L.W, trans_b=True, C=out, epilogue=ops.EPI_RELU)[0]
 
     @staticmethod
-    def _dgrad(L: _Layer, g, inp, out, gp=None, wp=None, outp=None):
+    def _dgrad(L: _Layer, g, inp, out):
         """dX = g W (x ReLU'(inp) when inp is given).  Widths that are not a multiple of 4
-        run over Kp (the bias column's gradient lands in a column nobody reads).  Planes:
-        gp / wp of g / W, outp = the planes of dX (or None)."""
+        run over Kp (the bias column's gradient lands in a column nobody reads)."""
         n = L.K if L.K % 4 == 0 else L.Kp
-        pk = dict(a_planes=gp, b_planes=wp, c_planes=outp)
         if inp is not None:
             return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n], epilogue=ops.EPI_DRELU,
-                                    aux=inp, **pk)[0]
-        return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n], **pk)[0]
+                                    aux=inp)[0]
+        return ops.gemm_problem(g[:, :L.N], L.W[:, :n], C=out[:, :n])[0]
 
     @staticmethod
-    def _wgrad(L: _Layer, g, inp, fused_opt, lr, planes=None, **part):
+    def _wgrad(L: _Layer, g, inp, fused_opt, lr, **part):
         """[dW | db] = g^T [inp | 1]; fused SGD on one GPU.  With K % 4 == 0 the bias
         gradient is the row sum of g^T (ones_col) and the GEMM covers only the K weight
-        columns; otherwise the constant-1 column of inp is multiplied like a weight column.
-        planes = (planes of g, of inp, of W): read g / inp from them, keep W's in step."""
+        columns; otherwise the constant-1 column of inp is multiplied like a weight column."""
         C = L.W if fused_opt else L.gW
         kw = dict(alpha=lr, epilogue=ops.EPI_SGD) if fused_opt else {}
-        if planes is not None:
-            kw.update(a_planes=planes[0], b_planes=planes[1], c_planes=planes[2])
         if L.K % 4 == 0:
             return ops.gemm_problem(g[:, :L.N], inp[:, :L.K], trans_a=True, C=C, ones_col=L.K,
                                     **kw, **part)[0]
         return ops.gemm_problem(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=C, **kw, **part)[0]
 
-    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key, last=False, planes=None):
+    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key, last=False):
         """The wgrad of L as (problem, reduce job or None): split-K wgrads write partials
         into a per-layer buffer and their reduction (+ SGD) runs in the NEXT launch.  The
         last GEMM of the step (last=True) has no next launch to carry a reduce job: its
         K split, if any, is reduced inside its own launch (FULL mode)."""
         if last and self.full_last_wgrad:
-            return self._wgrad(L, g, inp, fused_opt, lr, planes), None
+            return self._wgrad(L, g, inp, fused_opt, lr), None
         bufs = self._cur
         sp = bufs.setdefault("splits", {})
         if key not in sp:
-            sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr, planes), partial=True)
-            # tuning override (A/B sweeps only): DLRM_WG_SPLITS="top1:4,bot0:2"
-            for item in os.environ.get("DLRM_WG_SPLITS", "").split(","):
-                name, _, val = item.partition(":")
-                if name == f"{key[0]}{key[1]}" and val.isdigit() and int(val) >= 1:
-                    sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr, planes),
-                                              partial=True, requested=int(val))
+            sp[key] = ops.gemm_splits(self._wgrad(L, g, inp, fused_opt, lr), partial=True)
         s = sp[key]
         if s <= 1:
-            return self._wgrad(L, g, inp, fused_opt, lr, planes), None
+            return self._wgrad(L, g, inp, fused_opt, lr), None
         parts = bufs.setdefault("partials", {})
         M, N = L.N, (L.K if L.K % 4 == 0 else L.Kp)
         need = ops.gemm_partial_bytes(M, N, s)
         if key not in parts or parts[key].numel() * 4 < need:
             parts[key] = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
-        pr = self._wgrad(L, g, inp, fused_opt, lr, planes, partial=parts[key], splits=s)
+        pr = self._wgrad(L, g, inp, fused_opt, lr, partial=parts[key], splits=s)
         return pr, ops.reduce_problem(pr)
 
     def _gemm(self, problems, side=False):
@@ -986,10 +991,10 @@ class DLRMTrainer:
             self._colsum(hin[:, :last.Kp], scale=dz, out=last.gW[0],
                          workspace=self._ws_colsum(Bl, last.Kp))
 
-    def _bottom_chain(self, batch: Batch, bufs):
-        """The bottom MLP forward as a dlrm_mlp_chain (None when disabled or unsupported,
-        or when there are no local tables to share a launch with)."""
-        if not self.fuse_bottom or self.T_local == 0:
+    def _bottom_chain(self, batch: Batch, bufs, backward: bool = False):
+        """The bottom MLP as a dlrm_mlp_chain (None when unsupported; for the forward also
+        when disabled or when there are no local tables to share the lookup launch with)."""
+        if not backward and (not self.fuse_bottom or self.T_local == 0):
             return None
         chain = ops.mlp_chain(batch.X, [(L.W, out, L.Kp)
                                         for L, out in zip(self.bot, bufs["bot_act"])])

@@ -95,9 +95,32 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  * 3: dlrm_qr_expand_csr takes phys_capacity + error_flag; a PARTIAL split count must be
  *    normalized (dlrm_gemm_f32_splits) (round 3).
  * 4: dlrm_gemm_problem carries split-bf16 planes; dlrm_split_planes; the TBE backward's
- *    rows per call must be < 2^32 - 1 (round 3). */
+ *    rows per call must be < 2^32 - 1 (round 3).
+ * 5: the split-bf16 planes and dlrm_split_planes are gone again (measured slower than the
+ *    exact-f32 MFMA path in the step, profiles/r03_planes_*.txt): dlrm_gemm_problem ends
+ *    at `partial`; dlrm_tbe_forward_presort's out = NULL (sort-only) mode is used by the
+ *    engine (round 4). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
+
+/* Plan overrides for autotuning sweeps and coverage tests (ABI v5; the library reads no
+ * environment).  THREAD-LOCAL: they apply to the calls the calling host thread makes;
+ * value 0 restores the planner's choice.  Results stay exact under any override (the
+ * tests compare every path with the reference), only speed changes.
+ *   DLRM_TUNE_GEMM_TILE  : BM * 1000 + BN of the pipelined GEMM's workgroup tile (64064,
+ *                          128064, 64128, 32064, 64032); the measured plan table is skipped
+ *   DLRM_TUNE_GEMM_SPLIT : K splits of every FULL problem (with DLRM_TUNE_GEMM_TILE)
+ *   DLRM_TUNE_TBE_BLOCK  : sorted lookups per TBE-backward block (16 or 64)
+ *   DLRM_TUNE_TBE_SORT   : 1 = the device-wide radix sort even where the tiled per-table
+ *                          sort applies */
+enum dlrm_tune_key {
+  DLRM_TUNE_GEMM_TILE = 1,
+  DLRM_TUNE_GEMM_SPLIT = 2,
+  DLRM_TUNE_TBE_BLOCK = 3,
+  DLRM_TUNE_TBE_SORT = 4
+};
+int dlrm_set_tuning(int32_t key, int64_t value);
+int64_t dlrm_get_tuning(int32_t key);
 
 /* ------------------------------------------------ table-batched embedding -- */
 /*
@@ -146,6 +169,18 @@ int dlrm_mlp_chain_supported(const dlrm_mlp_chain* chain);
 
 /* The chain on its own: 16 rows per workgroup, every layer in one launch. */
 int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream);
+
+/* The data gradients of the chain's backward (round 4; the autograd of apply_mlp's
+ * Linear+ReLU stack, dlrm_s_pytorch.py:518-524, without the weight gradients, which the
+ * caller runs as one grouped GEMM launch): given g_last = dLoss/d(pre-activation of the
+ * last layer) [rows][>= out_width[L-1]], for l = L-1 .. 1
+ *   g[l-1] = (g_l . W_l[:, :out_width[l-1]]) * (Y_{l-1} > 0)   (columns < out_width[l-1])
+ * with g_{L-1} = g_last; W_l and Y_{l-1} are the chain's (the forward's weights and
+ * outputs).  16 rows per workgroup, every layer in one launch, gradients kept in LDS
+ * between layers.  g / ld_g: L-1 buffers and row pitches, none aliasing g_last.  Same
+ * support rules as the forward (dlrm_mlp_chain_supported). */
+int dlrm_mlp_chain_backward(const dlrm_mlp_chain* chain, const float* g_last, int64_t ld_g_last,
+                            float* const* g, const int64_t* ld_g, dlrm_stream_t stream);
 
 /*
  * dlrm_tbe_forward + the per-table sort of the backward (which depends only on the
@@ -435,7 +470,7 @@ enum dlrm_gemm_mode {
 };
 
 /*
- * Grouped GEMM: up to 4 INDEPENDENT problems in one launch (e.g. the dgrad of layer l
+ * Grouped GEMM: up to 6 INDEPENDENT problems in one launch (4 before ABI v5) (e.g. the dgrad of layer l
  * beside the wgrad of layer l+1 of an MLP backward: both read dY_{l+1}, neither writes
  * what the other reads).  Each problem is dlrm_gemm_f32's contract, plus:
  *   ones_col >= 0:  C[m][ones_col] = epilogue(alpha * sum_k op(A)(m,k))   (ones_col in
@@ -471,31 +506,8 @@ typedef struct dlrm_gemm_problem {
   int32_t mode;     /* dlrm_gemm_mode */
   int32_t splits;   /* PARTIAL / REDUCE */
   float* partial;   /* PARTIAL / REDUCE */
-  /* Split-bf16 planes (ABI v4; all NULL = the exact-f32 MFMA path).  The planes of an
-   * fp32 matrix X stored [rows][ld] are three bf16 matrices h, m, l at
-   * planes + q * plane_stride (q = 0, 1, 2), row pitch ld_planes (a multiple of 8), with
-   * X = h + m + l exactly (dlrm_split_planes).  With a_planes AND b_planes set, the GEMM
-   * reads op(A), op(B) from the planes (A / B still describe the same matrices and must
-   * hold them) and computes on the bf16 matrix core: six products per k-step
-   * (hh, hm, mh, hl, lh, mm), fp32 accumulation, accuracy at or below the exact-f32 path
-   * (tests/test_gpu_kernels.py::test_gemm_planes_*).  Needs K and every mn-contiguous
-   * extent % 8 == 0 after padding: a k-contiguous operand's rows are read up to
-   * roundup(K, 8), so the plane columns [K, roundup(K, 8)) must be zero in A or in B.
-   * c_planes (optional, any mode that writes C): every C element the epilogue writes is
-   * also split into c_planes, so the next GEMM can read it as planes. */
-  const void* a_planes;
-  int64_t lda_planes, a_plane_stride;
-  const void* b_planes;
-  int64_t ldb_planes, b_plane_stride;
-  void* c_planes;
-  int64_t ldc_planes, c_plane_stride;
 } dlrm_gemm_problem;
 
-/* X [rows][cols] fp32 (row pitch ld) -> planes [3][rows][ld_planes] bf16 (plane stride
- * plane_stride): X = h + m + l exactly (round to nearest at each level), the layout the
- * GEMM's a_planes / b_planes / c_planes use.  ld_planes % 8 == 0, ld_planes >= cols. */
-int dlrm_split_planes(const float* X, int64_t rows, int64_t cols, int64_t ld, void* planes,
-                      int64_t ld_planes, int64_t plane_stride, dlrm_stream_t stream);
 size_t dlrm_gemm_f32_group_workspace_size(int32_t n, const dlrm_gemm_problem* problems);
 /* The planner's K split for one problem as if launched alone, in its mode (FULL: an
  * in-launch split; PARTIAL: the split a deferred REDUCE will finish).  PARTIAL with

@@ -350,14 +350,16 @@ class OracleDLRM(nn.Module):
 
 
 def distributed_step(model: OracleDLRM, W: int, device_indices: Sequence[int], X, lS_o, lS_i,
-                     T, lr: float):
+                     T, lr: float, optimizer=None):
     """distributed_forward semantics (dlrm_s_pytorch.py:686-730, extend_distributed.py:
     405-508, DDP :1626-1633) simulated in one process for W ranks:
       * the all-to-all delivers features in RANK-MAJOR table order;
       * rank s's loss is the mean over its batch slice; embedding gradients are the SUM of
         the per-rank gradients (a2a backward, no averaging -> W x the global-mean grad);
       * dense (MLP) gradients are averaged over ranks (DDP).
-    Returns the list of per-rank Z and losses; updates the model in place (SGD)."""
+    Returns the list of per-rank Z and losses; updates the model in place: SGD at ``lr``, or
+    ``optimizer`` (e.g. RWSAdagradOracle over model.parameters(), the driver's C4 run
+    :1636-1666) stepped on those gradients (its own lr; ``lr`` unused)."""
     B = X.shape[0]
     order = [t for r in range(W) for t in range(len(model.emb_l)) if device_indices[t] == r]
     ly = [model.emb_l[t](lS_i[t], lS_o[t]) for t in range(len(model.emb_l))]
@@ -380,7 +382,12 @@ def distributed_step(model: OracleDLRM, W: int, device_indices: Sequence[int], X
             if p.grad is None:
                 continue
             g = p.grad if name.startswith("emb_l") else p.grad / W
-            p.add_(g, alpha=-lr)
+            if optimizer is None:
+                p.add_(g, alpha=-lr)
+            else:
+                p.grad = g
+        if optimizer is not None:
+            optimizer.step()
     return Zs, Es
 
 

@@ -45,3 +45,28 @@ def init_mlp(g):
 
 def rank_key(W, sharder, r, name):
     return f"W{W}_{sharder}_r{r}_{name}"
+
+
+# tests/golden/dist_qr.npz: the reference's gloo runs of the C4 model (QR tables above
+# qr_threshold rows + RWSAdagrad over the driver's parameter groups); keys
+# W{W}_{sharder}_{op}_r{r}_*, QR tables as init_emb{t}_q / _r
+QR_CASES = [(2, "greedy", "mult"), (2, "naive", "add"), (4, "greedy", "mult")]
+
+
+def load_qr():
+    return np.load(os.path.join(GOLDEN, "dist_qr.npz"), allow_pickle=False)
+
+
+def qr_rank_key(W, sharder, op, r, name):
+    return f"W{W}_{sharder}_{op}_r{r}_{name}"
+
+
+def init_tables_qr(g):
+    """Per table: [rows, D] (plain) or (weight_q, weight_r) (QR)."""
+    out = []
+    for t in range(len(g["ln_emb"])):
+        if f"init_emb{t}_q" in g:
+            out.append((g[f"init_emb{t}_q"], g[f"init_emb{t}_r"]))
+        else:
+            out.append(g[f"init_emb{t}"])
+    return out

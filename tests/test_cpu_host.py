@@ -26,7 +26,7 @@ def test_abi_library_exports_every_header_symbol():
         assert hasattr(lib, n), f"{n} declared in include/dlrm_hip.h but not exported"
         assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
     assert set(_lib.SIGNATURES) == set(names)
-    assert lib.dlrm_abi_version() == 4
+    assert lib.dlrm_abi_version() == 5
 
 
 def test_abi_rejects_bad_arguments_without_gpu():
@@ -39,9 +39,9 @@ def test_abi_rejects_bad_arguments_without_gpu():
         _lib.call("dlrm_tbe_forward", None, 4, None, 1, 1, None, 16, None, 32, None, None, 4,
                   None, None)
     assert e.value.code == 1
-    # split-bf16 planes: the pitch must hold whole 16-B chunks (checked before any launch)
+    # tuning overrides: known keys only, thread-local, 0 restores the planner
     with pytest.raises(_lib.DLRMHipError) as e:
-        _lib.call("dlrm_split_planes", None, 4, 7, 7, None, 7, 28, None)
+        _lib.call("dlrm_set_tuning", 99, 1)
     assert e.value.code == 1
     # workspace queries are pure host arithmetic
     assert _lib.query("dlrm_tbe_backward_workspace_size", 53248, 54063992, 128) > 53248 * 20
@@ -141,17 +141,35 @@ def test_gemm_partial_split_counts_are_normalized_or_rejected():
     assert e.value.code == 1 and "normalized" in str(e.value)
 
 
-def test_planes_host_api_checks_without_gpu():
-    """ops.split_planes / gemm_problem plane arguments are validated on the host: device
-    tensors only, bf16 [3, rows, ld] planes with unit inner stride."""
-    import torch
+def test_tuning_overrides_are_thread_local_and_restored():
+    """ops.tuning sets dlrm_set_tuning keys for the calling thread only and restores the
+    previous values on exit (no environment is read by the library)."""
+    import threading
+    from dlrm_hip import _lib, ops
+    lib = _lib.load()
+    assert lib.dlrm_get_tuning(ops.TUNE_KEYS["gemm_tile"]) == 0
+    seen = []
+    with ops.tuning(gemm_tile=64064, tbe_block=64):
+        assert lib.dlrm_get_tuning(ops.TUNE_KEYS["gemm_tile"]) == 64064
+        assert lib.dlrm_get_tuning(ops.TUNE_KEYS["tbe_block"]) == 64
+        t = threading.Thread(target=lambda: seen.append(
+            lib.dlrm_get_tuning(ops.TUNE_KEYS["gemm_tile"])))
+        t.start()
+        t.join()
+    assert seen == [0]
+    assert lib.dlrm_get_tuning(ops.TUNE_KEYS["gemm_tile"]) == 0
+    assert lib.dlrm_get_tuning(ops.TUNE_KEYS["tbe_block"]) == 0
+    with pytest.raises(KeyError):
+        ops.tuning(nope=1)
+
+
+def test_oversize_table_sets_are_refused_at_construction():
+    """The TBE backward keys on 32-bit global rows: a table set of >= 2^32 - 1 rows is
+    refused where it is built (module / trainer), not at the first backward."""
     from dlrm_hip import ops
-    with pytest.raises(ValueError, match="device tensors"):
-        ops.split_planes(torch.zeros(4, 8))
-    P = torch.zeros(3, 4, 8, dtype=torch.bfloat16)
-    assert ops._plane_args(None) == (None, 0, 0)
-    assert ops._plane_args(P) == (P.data_ptr(), 8, 32)
-    with pytest.raises(ValueError, match="bf16"):
-        ops._plane_args(torch.zeros(3, 4, 8))
-    with pytest.raises(ValueError, match="bf16"):
-        ops._plane_args(P[:2])
+    ops.check_tbe_rows(54063992, "C3")
+    with pytest.raises(ValueError, match="2\\^32"):
+        ops.check_tbe_rows(1 << 32, "test")
+    from dlrm_hip.modules import TableBatchedEmbeddingBags
+    with pytest.raises(ValueError, match="2\\^32"):
+        TableBatchedEmbeddingBags(2, [1 << 31, 1 << 31], 4, tables=[None, None])

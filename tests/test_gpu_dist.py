@@ -284,3 +284,202 @@ def test_c3_table_list_greedy_ranks_match_oracle(W):
             assert ok, (r, "W", i, msg)
             ok, msg = fp32_close_relu_flips(b, lin[i].bias.detach().numpy())
             assert ok, (r, "b", i, msg)
+
+
+def _qr_worker(rank, W, port, sharder, op, q, graph=False):
+    """One rank of the fused trainer on the C4 model (QR tables + RWSAdagrad) from the
+    reference's initial weights in dist_qr.npz."""
+    try:
+        sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd"), HERE]
+        import torch.distributed as dist
+        import dist_fixture as DF
+        from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=W)
+        g = DF.load_qr()
+        cfg = TrainerConfig(**DF.config(g), loss_function="bce",
+                            learning_rate=float(g["lr"][0]), optimizer="rwsadagrad",
+                            sharder=sharder, qr_flag=True,
+                            qr_collisions=int(g["qr_collisions"][0]), qr_operation=op,
+                            qr_threshold=int(g["qr_threshold"][0]))
+        tr = DLRMTrainer(cfg, device="cuda:0", rank=rank, world_size=W,
+                         process_group=dist.group.WORLD, init=False)
+        tr.load_dense(DF.init_mlp(g), DF.init_tables_qr(g))
+        data = [(X.numpy(), lS_o.numpy(), [i.numpy() for i in lS_i], T.numpy())
+                for X, lS_o, lS_i, T in DF.batches(g)]
+        batches = [tr.make_batch(*d) for d in data]
+        res = {"Z": [], "E": [], "local": tr.local_tables}
+        runs = [lambda b=b: tr.step(b) for b in batches]
+        if graph:
+            tr.step(batches[0])
+            torch.cuda.synchronize()
+            runs = [None] + [tr.capture(b) for b in batches[1:]]
+        for i, b in enumerate(batches):
+            if runs[i] is not None:
+                runs[i]()
+            bufs = tr._bufs[(b.X.shape[0], b.X.shape[0] * W)]
+            res["Z"].append(bufs["prob"].cpu().numpy())
+            res["E"].append(float(bufs["loss"].cpu()))
+        torch.cuda.synchronize()
+        tr.check_errors()
+        cpu = lambda v: tuple(x.cpu().numpy() for x in v) if isinstance(v, tuple) \
+            else v.cpu().numpy()  # noqa: E731
+        res["tables"] = {t: cpu(tr.table(t)) for t in tr.local_tables}
+        res["mom"] = {t: cpu(tr.table_momentum(t)) for t in tr.local_tables}
+        res["dense"] = [(w.cpu().numpy(), b.cpu().numpy()) for w, b in tr.dense_state()]
+        res["sum"] = [(w.cpu().numpy(), b.cpu().numpy()) for w, b in tr.dense_adagrad_state()]
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("W,sharder,op,graph", [(2, "greedy", "mult", False),
+                                                (2, "naive", "add", False),
+                                                (4, "greedy", "mult", False),
+                                                (4, "greedy", "mult", True)])
+def test_c4_qr_rwsadagrad_ranks_match_reference_gloo_run(W, sharder, op, graph):
+    """BASELINE configs[4]'s model sharded across ranks (QR tables split into quotient and
+    remainder tables on their owner rank, fused RWSAdagrad on the embedding rows, the
+    DDP-averaged dense gradient into Adagrad) against the REFERENCE's own gloo run
+    (dist_qr.npz, make_golden_dist.py --qr): per-rank Z and loss of 3 steps, every rank's
+    final quotient / remainder / plain tables and their row-wise momentum, and the final
+    dense weights and Adagrad sums, all within the 1e-5 fp32 bound."""
+    import dist_fixture as DF
+    from conftest import fp32_close
+    g = DF.load_qr()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_qr_worker, args=(r, W, port, sharder, op, q, graph))
+          for r in range(W)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(W))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(W):
+        assert isinstance(res[r], dict), res[r]
+    key = lambda r, name: DF.qr_rank_key(W, sharder, op, r, name)  # noqa: E731
+    names = [("bot", 2 * i) for i in range(len(g["ln_bot"]) - 1)] + \
+            [("top", 2 * i) for i in range(len(g["ln_top"]) - 1)]
+    for r in range(W):
+        assert res[r]["local"] == g[key(r, "local")].tolist()
+        for s in range(int(g["steps"][0])):
+            ok, msg = fp32_close(res[r]["Z"][s], g[key(r, f"s{s}_Z")].ravel())
+            assert ok, (s, r, msg)
+            ok, msg = fp32_close(np.array([res[r]["E"][s]]), g[key(r, f"s{s}_loss")])
+            assert ok, (s, r, msg)
+        for t in res[r]["local"]:
+            w, m = res[r]["tables"][t], res[r]["mom"][t]
+            parts = [("_q", w[0], m[0]), ("_r", w[1], m[1])] if isinstance(w, tuple) else \
+                [("", w, m)]
+            assert (len(parts) == 2) == (f"init_emb{t}_q" in g)
+            for suf, wv, mv in parts:
+                ok, msg = fp32_close(wv, g[key(r, f"final_emb{t}{suf}")])
+                assert ok, (r, t, suf, msg)
+                ok, msg = fp32_close(mv, g[key(r, f"final_mom{t}{suf}")])
+                assert ok, ("momentum", r, t, suf, msg)
+        for (w, b), (sw, sb), (pre, i) in zip(res[r]["dense"], res[r]["sum"], names):
+            for got, nm in ((w, "weight"), (b, "bias")):
+                ok, msg = fp32_close(got, g[key(r, f"final_{pre}.{i}.{nm}")])
+                assert ok, (r, pre, i, nm, msg)
+            for got, nm in ((sw, "weight"), (sb, "bias")):
+                ok, msg = fp32_close(got, g[key(r, f"final_sum_{pre}.{i}.{nm}")])
+                assert ok, ("adagrad sum", r, pre, i, nm, msg)
+
+
+def _module_worker(rank, W, port, sharder, q):
+    """One rank of the reference's own driver loop (make_golden_dist.py's worker) with the
+    drop-in dlrm_hip.dlrm_net.DLRM_Net: ext_dist.init_distributed (gloo), the distributed
+    constructor (sharders + local tables), the MLPs in DDP, torch.optim.SGD, forward =
+    distributed_forward (HIP lookup -> ext_dist.alltoall -> HIP bottom MLP -> wait -> HIP
+    interaction -> HIP top MLP), loss_fn, backward through the all-to-all, step."""
+    try:
+        sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd"), HERE]
+        import dist_fixture as DF
+        from dlrm_hip import extend_distributed as ed
+        from dlrm_hip.dlrm_net import DLRM_Net
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(W), LOCAL_RANK=str(rank))
+        ed.init_distributed(rank=rank, local_rank=rank, size=W, use_gpu=False, backend="gloo")
+        g = DF.load()
+        c = DF.config(g)
+        dev = torch.device("cuda", 0)
+        net = DLRM_Net(c["m_spa"], np.array(c["ln_emb"]), np.array(c["ln_bot"]),
+                       np.array(c["ln_top"]), arch_interaction_op="dot",
+                       sigmoid_top=len(c["ln_top"]) - 2, loss_function="bce",
+                       sharder=sharder).to(dev)
+        local = list(net.local_emb_indices)
+        with torch.no_grad():
+            for k, t in enumerate(local):
+                net.emb_l[k].weight.copy_(torch.tensor(g[f"init_emb{t}"]))
+            for pre, seq in (("bot", net.bot_l), ("top", net.top_l)):
+                for name, p in seq.named_parameters():
+                    p.copy_(torch.tensor(g[f"init_{pre}.{name}"]))
+        net.bot_l = ed.DDP(net.bot_l)
+        net.top_l = ed.DDP(net.top_l)
+        opt = torch.optim.SGD(net.parameters(), lr=float(g["lr"][0]))
+        sl = ed.get_my_slice(int(g["B"][0]))
+        res = {"Z": [], "E": [], "local": local, "n_emb_per_rank": list(net.n_emb_per_rank)}
+        for s, (X, lS_o, lS_i, T) in enumerate(DF.batches(g)):
+            Z = net(X[sl].to(dev), [lS_o[t].to(dev) for t in local],
+                    [lS_i[t].to(dev) for t in local])
+            E = net.loss_fn(Z, T[sl].to(dev))
+            opt.zero_grad()
+            E.backward()
+            opt.step()
+            res["Z"].append(Z.detach().cpu().numpy())
+            res["E"].append(float(E.detach().cpu()))
+        torch.cuda.synchronize()
+        res["tables"] = {t: net.emb_l[k].weight.detach().cpu().numpy()
+                         for k, t in enumerate(local)}
+        res["dense"] = {f"{pre}.{name}": p.detach().cpu().numpy()
+                        for pre, seq in (("bot", net.bot_l.module), ("top", net.top_l.module))
+                        for name, p in seq.named_parameters()}
+        ed.barrier()
+        torch.distributed.destroy_process_group()
+        q.put((rank, res))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("W,sharder", [(2, "greedy"), (2, "naive_chunk"), (4, "greedy")])
+def test_module_distributed_forward_matches_reference_gloo_run(W, sharder):
+    """The drop-in module's multi-rank path (DLRM_Net.distributed_forward ->
+    ext_dist.alltoall -> All2All_Req / All2All_Wait, extend_distributed.py:405-508, 601-639,
+    DDP :1626-1633) under the reference's driver loop, W ranks sharing one GPU (gloo:
+    the exchange host-staged), against the REFERENCE's own gloo run (dist.npz): per-rank Z
+    and loss of 3 SGD steps, final local tables and dense parameters."""
+    import dist_fixture as DF
+    from conftest import fp32_close
+    g = DF.load()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_module_worker, args=(r, W, port, sharder, q)) for r in range(W)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(W))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(W):
+        assert isinstance(res[r], dict), res[r]
+    for r in range(W):
+        assert res[r]["local"] == g[DF.rank_key(W, sharder, r, "local")].tolist()
+        assert res[r]["n_emb_per_rank"] == g[DF.rank_key(W, sharder, r, "n_emb_per_rank")].tolist()
+        for s in range(int(g["steps"][0])):
+            ok, msg = fp32_close(res[r]["Z"][s], g[DF.rank_key(W, sharder, r, f"s{s}_Z")])
+            assert ok, (s, r, msg)
+            ok, msg = fp32_close(np.array([res[r]["E"][s]]),
+                                 g[DF.rank_key(W, sharder, r, f"s{s}_loss")])
+            assert ok, (s, r, msg)
+        for t, w in res[r]["tables"].items():
+            ok, msg = fp32_close(w, g[DF.rank_key(W, sharder, r, f"final_emb{t}")])
+            assert ok, (r, t, msg)
+        for name, w in res[r]["dense"].items():
+            ok, msg = fp32_close(w, g[DF.rank_key(W, sharder, r, f"final_{name}")])
+            assert ok, (r, name, msg)

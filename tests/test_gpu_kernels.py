@@ -370,12 +370,10 @@ GEMM_SHAPES = [(2048, 1024, 479), (64, 64, 64), (100, 37, 13), (2, 4, 10), (1000
                (256, 512, 2048), (33, 129, 67)]
 
 
-@pytest.mark.parametrize("math", ["f32", "x6"])
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
-def test_gemm_vs_fp64(ops, M, N, K, ta, tb, math, monkeypatch):
-    """Both GEMM maths (exact-f32 MFMA, split-bf16 x6) within the fp32 dot-product bound."""
-    monkeypatch.setenv("DLRM_GEMM_MATH", math)
+def test_gemm_vs_fp64(ops, M, N, K, ta, tb):
+    """The exact-f32 MFMA GEMM within the fp32 dot-product bound of an fp64 product."""
     torch.manual_seed(M + N + K)
     A = torch.randn(K, M) if ta else torch.randn(M, K)
     Bm = torch.randn(N, K) if tb else torch.randn(K, N)
@@ -387,35 +385,32 @@ def test_gemm_vs_fp64(ops, M, N, K, ta, tb, math, monkeypatch):
     assert ok, msg
 
 
-GEMM_CFGS = [("f32", "64x64"), ("f32", "128x64"), ("f32", "64x128"), ("f32", "64x32"),
-             ("f32", "32x64"), ("x6", "64x64"), ("x6", "64x32"), ("x6", "32x64")]
+# workgroup tiles the planner can pick (dlrm_set_tuning DLRM_TUNE_GEMM_TILE = BM*1000 + BN)
+GEMM_CFGS = [64064, 128064, 64128, 64032, 32064]
 
 
-@pytest.mark.parametrize("math,cfg", GEMM_CFGS)
-def test_gemm_every_kernel_config(ops, math, cfg, monkeypatch):
-    """Every tile/BK/k-group/MFMA-shape instantiation the planner can pick, forced via the
-    tuning override, on ragged shapes in all four operand layouts, with and without split-K."""
-    monkeypatch.setenv("DLRM_GEMM_MATH", math)
-    monkeypatch.setenv("DLRM_GEMM_CFG", cfg)
+@pytest.mark.parametrize("cfg", GEMM_CFGS)
+def test_gemm_every_kernel_config(ops, cfg):
+    """Every tile instantiation the planner can pick, forced via the tuning override
+    (ops.tuning / dlrm_set_tuning), on ragged shapes in all four operand layouts, with and
+    without split-K."""
     ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)  # split-K tickets start at 0
     for (M, N, K) in [(130, 70, 300), (64, 128, 256), (3, 5, 1030)]:
         for ta, tb in [(0, 1), (0, 0), (1, 0), (1, 1)]:
-            for split in ("1", "3", "7"):
-                monkeypatch.setenv("DLRM_GEMM_SPLIT", split)
+            for split in (1, 3, 7):
                 torch.manual_seed(M * 7 + N + K + ta * 3 + tb)
                 A = torch.randn(K, M) if ta else torch.randn(M, K)
                 Bm = torch.randn(N, K) if tb else torch.randn(K, N)
                 opA = A.double().t() if ta else A.double()
                 opB = Bm.double().t() if tb else Bm.double()
-                C = ops.gemm(A.to(dev), Bm.to(dev), bool(ta), bool(tb), workspace=ws).cpu()
+                with ops.tuning(gemm_tile=cfg, gemm_split=split):
+                    C = ops.gemm(A.to(dev), Bm.to(dev), bool(ta), bool(tb), workspace=ws).cpu()
                 ok, msg = gemm_close(C.numpy(), (opA @ opB).numpy(),
                                      (opA.abs() @ opB.abs()).numpy(), K)
                 assert ok, (cfg, M, N, K, ta, tb, split, msg)
 
 
-@pytest.mark.parametrize("math", ["f32", "x6"])
-def test_gemm_epilogues(ops, math, monkeypatch):
-    monkeypatch.setenv("DLRM_GEMM_MATH", math)
+def test_gemm_epilogues(ops):
     torch.manual_seed(3)
     M, N, K = 300, 200, 130
     X, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
@@ -658,7 +653,7 @@ def test_module_lookup_raises_index_error(ops):
         m(bad, off)
 
 
-def test_gemm_splitk_in_launch_fixup_is_deterministic_and_resets(ops, monkeypatch):
+def test_gemm_splitk_in_launch_fixup_is_deterministic_and_resets(ops):
     """In-launch split-K: the last workgroup of a tile sums the partials in split order.
     Repeated calls on one workspace (tickets reset by the kernel) are bitwise identical,
     equal the unsplit sum within fp32 tolerance, and the tickets end at zero."""
@@ -675,26 +670,27 @@ def test_gemm_splitk_in_launch_fixup_is_deterministic_and_resets(ops, monkeypatc
     assert ok, msg
     tiles = 16384  # the fixed ticket region
     assert int(ws[:4 * tiles].view(torch.int32).abs().sum()) == 0
-    for split in ("2", "5", "9"):  # forced splits, fused SGD epilogue
-        monkeypatch.setenv("DLRM_GEMM_SPLIT", split)
-        monkeypatch.setenv("DLRM_GEMM_CFG", "64x64")
+    for split in (2, 5, 9):  # forced splits, fused SGD epilogue
         C0 = torch.randn(M, N, device=dev)
         C = C0.clone()
-        ops.gemm(A, Bm, True, False, C=C, alpha=0.5, epilogue=ops.EPI_SGD, workspace=ws)
+        with ops.tuning(gemm_tile=64064, gemm_split=split):
+            ops.gemm(A, Bm, True, False, C=C, alpha=0.5, epilogue=ops.EPI_SGD, workspace=ws)
         ok, msg = gemm_close((C0 - C).cpu().numpy() / 0.5, ref.numpy(),
                              (A.double().abs().t() @ Bm.double().abs()).cpu().numpy(), K + 4)
         assert ok, (split, msg)
         assert int(ws[:4 * tiles].view(torch.int32).abs().sum()) == 0
 
 
-@pytest.mark.parametrize("math,cfg", GEMM_CFGS)
-@pytest.mark.parametrize("split", ["1", "4"])
-def test_gemm_ones_col_bias_gradient(ops, math, cfg, split, monkeypatch):
+@pytest.mark.parametrize("cfg", GEMM_CFGS)
+@pytest.mark.parametrize("split", [1, 4])
+def test_gemm_ones_col_bias_gradient(ops, cfg, split):
     """ones_col: C[:, ones_col] = epi(alpha * rowsum(op(A))) beside the GEMM - the bias
     gradient of a Linear layer whose bias is the weight column ones_col (fused SGD)."""
-    monkeypatch.setenv("DLRM_GEMM_MATH", math)
-    monkeypatch.setenv("DLRM_GEMM_CFG", cfg)
-    monkeypatch.setenv("DLRM_GEMM_SPLIT", split)
+    with ops.tuning(gemm_tile=cfg, gemm_split=split):
+        _ones_col_cases(ops)
+
+
+def _ones_col_cases(ops):
     ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
     for (Bt, Nout, K) in [(2048, 256, 512), (300, 130, 64), (64, 16, 8)]:
         torch.manual_seed(Bt + Nout + K)
@@ -716,11 +712,9 @@ def test_gemm_ones_col_bias_gradient(ops, math, cfg, split, monkeypatch):
         assert torch.equal(W[:, K + 1:], W0[:, K + 1:])  # untouched pad columns
 
 
-@pytest.mark.parametrize("math", ["f32", "x6"])
-def test_gemm_group_matches_separate_launches(ops, math, monkeypatch):
+def test_gemm_group_matches_separate_launches(ops):
     """A grouped launch (dgrad of layer l || wgrad+SGD of layer l+1, plus two more problems
     of other layouts) gives bitwise the results of the same problems launched one by one."""
-    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     torch.manual_seed(5)
     Bt = 1024
     g1 = torch.randn(Bt, 512, device=dev)
@@ -765,13 +759,11 @@ def test_gemm_group_matches_separate_launches(ops, math, monkeypatch):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("math", ["f32", "x6"])
 @pytest.mark.parametrize("ones", [False, True])
-def test_gemm_partial_then_reduce_equals_full(ops, ones, math, monkeypatch):
+def test_gemm_partial_then_reduce_equals_full(ops, ones):
     """A PARTIAL problem (split-K partials to a buffer) finished by a REDUCE job in a later
     launch gives bitwise the in-launch split-K result (same splits, same sum order), with
     the fused SGD epilogue and the ones_col bias row sums."""
-    monkeypatch.setenv("DLRM_GEMM_MATH", math)
     torch.manual_seed(11)
     Bt, Nout, K = 2048, 256, 512
     g = torch.randn(Bt, Nout, device=dev)
@@ -795,14 +787,13 @@ def test_gemm_partial_then_reduce_equals_full(ops, ones, math, monkeypatch):
     assert torch.equal(W1, W2)
 
 
-@pytest.mark.parametrize("path", ["", "DLRM_INTERACT_V2", "DLRM_INTERACT_V1"])
+@pytest.mark.parametrize("path", ["staged", "runtime_d"])
 @pytest.mark.parametrize("D", [16, 128])
-def test_interact_backward_relu_x_and_paths(ops, monkeypatch, path, D):
+def test_interact_backward_relu_x_and_paths(ops, path, D):
     """relu_x fuses ReLU'(x) into feature 0's gradient, on the LDS-staged kernel and on the
-    fallback paths (separate mask pass); all paths agree with autograd on a torch fp32
-    reference (bmm + tril gather), within the fp32 tolerance."""
-    if path:
-        monkeypatch.setenv(path, "1")
+    fallback path (features not 16-B aligned: the runtime-D MFMA kernel + a separate mask
+    pass); both agree with autograd on a torch fp32 reference (bmm + tril gather), within
+    the fp32 tolerance."""
     torch.manual_seed(D)
     B, F = 70, 27
     x = torch.randn(B, D)          # mixed signs: the mask matters
@@ -815,13 +806,20 @@ def test_interact_backward_relu_x_and_paths(ops, monkeypatch, path, D):
     li, lj = torch.tril_indices(F, F, -1)
     R = torch.cat([xr, Z[:, li, lj]], 1)
     (R * gR).sum().backward()
-    gx, gly = ops.interact_backward("dot", x.to(dev), ly.to(dev), gR.to(dev), relu_x=True)
+    def dev_(t):  # runtime_d: a 1-float offset breaks the 16-B alignment of every row
+        if path == "staged":
+            return t.to(dev)
+        buf = torch.empty(t.numel() + 1, device=dev)
+        v = buf[1:].view(t.shape)
+        v.copy_(t)
+        return v
+    gx, gly = ops.interact_backward("dot", dev_(x), dev_(ly), gR.to(dev), relu_x=True)
     ok, msg = fp32_close(gx.cpu().numpy(), (xr.grad * (x > 0)).numpy())
     assert ok, msg
     ok, msg = fp32_close(gly.cpu().numpy(), lr_.grad.numpy())
     assert ok, msg
-    # forward on every path vs the same reference
-    out = ops.interact_forward("dot", x.to(dev), ly.to(dev))
+    # forward on both paths vs the same reference
+    out = ops.interact_forward("dot", dev_(x), dev_(ly))
     ok, msg = fp32_close(out.cpu().numpy(), R.detach().numpy())
     assert ok, msg
 
@@ -875,6 +873,36 @@ def test_mlp_chain_forward_matches_reference(ops, rows, dims):
         scale = max(1.0, r.abs().max().item())
         assert err <= 1e-5 * scale, err
         assert torch.all(Y[:, n:] == -7.0)  # padding / bias column untouched
+
+
+@pytest.mark.parametrize("rows,dims", [(2048, [13, 512, 256, 128]), (37, [13, 512, 256, 128]),
+                                       (128, [13, 512, 256, 64, 16]), (48, [200, 120, 500, 33, 7])])
+def test_mlp_chain_backward_matches_reference(ops, rows, dims):
+    """dlrm_mlp_chain_backward (the row-block dgrad chain of the bottom MLP backward) vs fp64
+    autograd-by-hand: g_{l-1} = (g_l W_l[:, :n_{l-1}]) * (Y_{l-1} > 0) for every layer but
+    the first; ragged batch, 4 layers, widths off the 16-grid; columns >= n untouched."""
+    X, layers = _mlp_setup(rows, dims)
+    ops.mlp_chain_forward(ops.mlp_chain(X, layers))
+    chain = ops.mlp_chain(X, layers)
+    L = len(layers)
+    g = torch.Generator(device=dev).manual_seed(9)
+    n_last = layers[-1][0].shape[0]
+    g_last = torch.randn(rows, n_last + 3, generator=g, device=dev)
+    grads = [torch.full((rows, layers[l][0].shape[0] + 5), -7.0, device=dev) for l in range(L - 1)]
+    ops.mlp_chain_backward(chain, g_last, grads)
+    torch.cuda.synchronize()
+    gl = g_last[:, :n_last].double()
+    for l in range(L - 1, 0, -1):
+        W, _, _ = layers[l]
+        n_prev = layers[l - 1][0].shape[0]
+        Yp = layers[l - 1][1][:, :n_prev].double()
+        ref = (gl @ W[:, :n_prev].double()) * (Yp > 0)
+        got = grads[l - 1][:, :n_prev].double()
+        scale = (gl.abs() @ W[:, :n_prev].double().abs()).max().item()
+        err = (got - ref).abs().max().item()
+        assert err <= 1e-5 * max(1.0, scale), (l, err, scale)
+        assert torch.all(grads[l - 1][:, n_prev:] == -7.0)
+        gl = got
 
 
 def test_mlp_chain_unsupported_is_refused(ops):
@@ -936,7 +964,7 @@ def _tbe_bwd_case(rows, B, L, D, seed, invalid=False, idx_dtype=torch.int32):
 @pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad", "dense"])
 @pytest.mark.parametrize("invalid", [False, True])
 @pytest.mark.parametrize("idx_dtype", [torch.int32, torch.int64])
-def test_tbe_backward_tiled_sort(ops, mode, invalid, idx_dtype, monkeypatch):
+def test_tbe_backward_tiled_sort(ops, mode, invalid, idx_dtype):
     """Tables with more than 4096 lookups (L = 100 pooling): the tiled per-table radix sort
     gives bitwise the updates of the device-wide sort when every index is valid (same
     (row, position) order), and matches the fp64 coalesced reference either way; skewed
@@ -946,13 +974,13 @@ def test_tbe_backward_tiled_sort(ops, mode, invalid, idx_dtype, monkeypatch):
     W0 = torch.randn(sum(rows), D, device=dev) * 0.1
     mom0 = torch.rand(sum(rows), device=dev)
     res = []
-    for tiled in ("1", "0"):
-        monkeypatch.setenv("DLRM_TBE_TILED_SORT", tiled)
+    for tiled in (True, False):  # False: the device-wide sort forced (DLRM_TUNE_TBE_SORT)
         W = W0.clone() if mode != "dense" else torch.zeros_like(W0)
         mom = mom0.clone()
         flag = torch.zeros(1, dtype=torch.int32, device=dev)
-        ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8, momentum=mom,
-                         max_lookups_per_table=B * L, error_flag=flag)
+        with ops.tuning(tbe_sort=0 if tiled else 1):
+            ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8,
+                             momentum=mom, max_lookups_per_table=B * L, error_flag=flag)
         torch.cuda.synchronize()
         assert (int(flag.item()) != 0) == invalid
         res.append((W.cpu(), mom.cpu()))
@@ -1015,11 +1043,12 @@ def _c1_case(dist: str, seed: int):
 
 
 @pytest.mark.parametrize("dist", ["uniform", "zipf"])
-def test_tbe_c1_full_shape_forward_and_backward_vs_oracle(ops, monkeypatch, dist):
+def test_tbe_c1_full_shape_forward_and_backward_vs_oracle(ops, dist):
     """The C1-shape lookup and its backward + exact SGD at FULL size against the oracle:
     forward vs nn.EmbeddingBag (fp32, lookup order), backward vs the fp64 coalesced update
-    W0 - lr * sum(g), with the block length forced to 16 and to 64 (DLRM_TBE_CH) and left
-    to the planner (64 at this size; the planner's choice is bitwise the forced 64)."""
+    W0 - lr * sum(g), with the block length forced to 16 and to 64 and left
+    to the planner (64 at this size; the planner's choice is bitwise the forced 64).  The
+    forced lengths go through ops.tuning (dlrm_set_tuning DLRM_TUNE_TBE_BLOCK)."""
     T, R, D, B, L, idx, off, W0, G, row_base = _c1_case(dist, 17 if dist == "uniform" else 18)
     lr = 0.25
     out = ops.tbe_forward(W0.to(dev), row_base.to(dev), T, B, idx.to(dev), off.to(dev)).cpu()
@@ -1036,14 +1065,11 @@ def test_tbe_c1_full_shape_forward_and_backward_vs_oracle(ops, monkeypatch, dist
     ref = (W0.double() - lr * gsum).numpy()
     res = {}
     for ch in ("16", "64", ""):
-        if ch:
-            monkeypatch.setenv("DLRM_TBE_CH", ch)
-        else:
-            monkeypatch.delenv("DLRM_TBE_CH", raising=False)
         W = W0.to(dev)
         flag = torch.zeros(1, dtype=torch.int32, device=dev)
-        ops.tbe_backward("sgd", W, row_base.to(dev), T, B, idx.to(dev), off.to(dev), G.to(dev),
-                         lr=lr, max_lookups_per_table=B * L, error_flag=flag)
+        with ops.tuning(tbe_block=int(ch or 0)):
+            ops.tbe_backward("sgd", W, row_base.to(dev), T, B, idx.to(dev), off.to(dev),
+                             G.to(dev), lr=lr, max_lookups_per_table=B * L, error_flag=flag)
         torch.cuda.synchronize()
         assert int(flag.item()) == 0
         res[ch] = W.cpu()
@@ -1089,237 +1115,3 @@ def test_interact_gather_matches_lookup_then_interact(ops, D, F, self_int):
     torch.cuda.synchronize()
     assert int(err.item()) & ops.TBE_ERR_INDEX
     assert torch.equal(R2, ops.interact_forward("dot", x, E2, self_int))
-
-
-@pytest.mark.parametrize("split", ["1", "3"])
-def test_gemm_x6l_body(ops, split, monkeypatch):
-    """The 128x128 split-bf16 body (DLRM_GEMM_MATH=x6l, pipe_body6L, 32x32x16 MFMA, 2x4
-    waves): ragged shapes in all four operand layouts within the fp32 dot-product bound;
-    epilogues (bias+ReLU, ReLU', SGD with the ones_col bias row sums); a PARTIAL problem
-    + REDUCE bitwise equal to the in-launch split."""
-    monkeypatch.setenv("DLRM_GEMM_MATH", "x6l")
-    monkeypatch.setenv("DLRM_GEMM_SPLIT", split)
-    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
-    for (M, N, K) in [(1000, 300, 130), (2048, 256, 480), (515, 520, 36)]:
-        for ta, tb in [(0, 1), (0, 0), (1, 0), (1, 1)]:
-            torch.manual_seed(M + N + K + ta * 3 + tb)
-            A = torch.randn(K, M) if ta else torch.randn(M, K)
-            Bm = torch.randn(N, K) if tb else torch.randn(K, N)
-            opA = A.double().t() if ta else A.double()
-            opB = Bm.double().t() if tb else Bm.double()
-            C = ops.gemm(A.to(dev), Bm.to(dev), bool(ta), bool(tb), workspace=ws).cpu()
-            ok, msg = gemm_close(C.numpy(), (opA @ opB).numpy(),
-                                 (opA.abs() @ opB.abs()).numpy(), K)
-            assert ok, (M, N, K, ta, tb, msg)
-    torch.manual_seed(3)
-    M, N, K = 1024, 300, 130
-    X, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
-    Y = ops.gemm(X.to(dev), W.to(dev), False, True, epilogue=ops.EPI_BIAS_RELU, bias=b.to(dev),
-                 workspace=ws).cpu()
-    ref = X.double() @ W.double().t() + b.double()
-    ok, msg = gemm_close(Y.numpy(), torch.relu(ref).numpy(),
-                         (X.double().abs() @ W.double().abs().t() + b.double().abs()).numpy(), K)
-    assert ok, msg
-    G, aux = torch.randn(M, N), torch.randn(M, K)
-    dX = ops.gemm(G.to(dev), W.to(dev), epilogue=ops.EPI_DRELU, aux=aux.to(dev),
-                  workspace=ws).cpu()
-    ref = (G.double() @ W.double()) * (aux > 0)
-    ok, msg = gemm_close(dX.numpy(), ref.numpy(), (G.double().abs() @ W.double().abs()).numpy(), N)
-    assert ok, msg
-    # wgrad + fused SGD + bias row sums: FULL in-launch vs PARTIAL + REDUCE (bitwise)
-    Bt, Nout, Kw = 2048, 1024, 512  # >= 2^18 outputs: the x6l planner takes it
-    g = torch.randn(Bt, Nout, device=dev)
-    Xw = torch.randn(Bt, Kw + 4, device=dev)
-    W0 = torch.randn(Nout, Kw + 4, device=dev)
-    kw = dict(trans_a=True, alpha=0.5, epilogue=ops.EPI_SGD, ones_col=Kw)
-    W1 = W0.clone()
-    pr, _ = ops.gemm_problem(g, Xw[:, :Kw], C=W1, **kw)
-    ops.gemm_group([pr], ws)
-    s = ops.gemm_splits(pr)  # the FULL plan's split, repeated by the PARTIAL problem
-    W2 = W0.clone()
-    part = torch.empty(ops.gemm_partial_bytes(Nout, Kw, s) // 4, device=dev)
-    pp, _ = ops.gemm_problem(g, Xw[:, :Kw], C=W2, partial=part, splits=s, **kw)
-    ops.gemm_group([pp], ws)
-    ops.gemm_group([ops.reduce_problem(pp)], ws)
-    torch.cuda.synchronize()
-    assert torch.equal(W1, W2)
-    gd, Xd = g.double().cpu(), Xw[:, :Kw].double().cpu()
-    got = (W0 - W1).double().cpu() / 0.5
-    ok, msg = gemm_close(got[:, :Kw].numpy(), (gd.t() @ Xd).numpy(),
-                         (gd.abs().t() @ Xd.abs()).numpy(), Bt + 8)
-    assert ok, msg
-    ok, msg = gemm_close(got[:, Kw].numpy(), gd.sum(0).numpy(), gd.abs().sum(0).numpy(), Bt + 8)
-    assert ok, msg
-
-
-# ------------------------------------------------------ pre-split planes (x6d body) --
-def _planes(ops, X):
-    return ops.split_planes(X.contiguous())
-
-
-@pytest.mark.gpu
-def test_split_planes_exact(ops):
-    """dlrm_split_planes: x = h + m + l exactly (fp64 sum), each plane bf16 round-to-nearest,
-    padding columns untouched (zero)."""
-    torch.manual_seed(0)
-    X = (torch.randn(300, 77) * torch.logspace(-20, 20, 77)).to(dev)
-    X[0, :5] = torch.tensor([0.0, -0.0, 1.0, 1e38, -1e-30])
-    P = ops.split_planes(X)
-    assert P.shape == (3, 300, 80)
-    Pd = P.double()
-    Xp = torch.zeros(300, 80, dtype=torch.float64, device=dev)
-    Xp[:, :77] = X.double()
-    assert torch.equal(Pd[0] + Pd[1] + Pd[2], Xp)
-    assert torch.equal(P[0][:, :77], X.to(torch.bfloat16))
-    assert int(P[:, :, 77:].abs().sum()) == 0
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(1000, 296, 136), (2048, 1024, 1024), (2048, 1024, 1028),
-                                   (520, 64, 2048)])
-@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
-def test_gemm_planes_layouts(ops, M, N, K, ta, tb):
-    """The pre-split body: every operand layout within the fp32 dot-product bound of the
-    fp64 product (as accurate as the exact-f32 MFMA path), tile shapes 128x64 / 64x64,
-    ragged edges, K % 8 == 4 on k-contiguous operands (zero plane padding)."""
-    if K % 8 and (ta or not tb):
-        pytest.skip("an mn-contiguous operand needs K % 8 == 0")
-    torch.manual_seed(M + N + K + 3 * ta + tb)
-    A = (torch.randn(K, M) if ta else torch.randn(M, K)).to(dev)
-    Bm = (torch.randn(N, K) if tb else torch.randn(K, N)).to(dev)
-    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
-    pr, C = ops.gemm_problem(A, Bm, bool(ta), bool(tb), a_planes=_planes(ops, A),
-                             b_planes=_planes(ops, Bm))
-    ops.gemm_group([pr], ws)
-    opA = A.double().t() if ta else A.double()
-    opB = Bm.double().t() if tb else Bm.double()
-    ok, msg = gemm_close(C.cpu().numpy(), (opA @ opB).cpu().numpy(),
-                         (opA.abs() @ opB.abs()).cpu().numpy(), K)
-    assert ok, (M, N, K, ta, tb, msg)
-    Cf = ops.gemm(A, Bm, bool(ta), bool(tb), workspace=ws)  # the f32 path, for reference
-    assert not torch.equal(C, Cf) or K < 32  # (a different math actually ran)
-
-
-@pytest.mark.gpu
-def test_gemm_planes_epilogues_and_c_planes(ops):
-    """Forward (ReLU) and dgrad (ReLU') from planes write c_planes bitwise equal to
-    split_planes of the C they write; a wgrad with fused SGD and bias row sums (ones_col)
-    runs FULL and as PARTIAL + REDUCE (bitwise equal), both keeping the weight planes in
-    step with the weights; DLRM_GEMM_PLANES=0 runs the f32 body on the same problem."""
-    torch.manual_seed(5)
-    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
-    Bt, K, Nout = 2048, 1024, 512
-    X = torch.randn(Bt, K + 4, device=dev)
-    X[:, K] = 1.0
-    X[:, K + 1:] = 0.0
-    W = torch.randn(Nout, K + 4, device=dev) * 0.05
-    W[:, K + 1:] = 0.0
-    XP, WP = _planes(ops, X), _planes(ops, W)
-    Y = torch.zeros(Bt, Nout, device=dev)
-    YP = ops.planes_empty(Bt, Nout, dev)
-    pr, _ = ops.gemm_problem(X, W, trans_b=True, C=Y, epilogue=ops.EPI_RELU, a_planes=XP,
-                             b_planes=WP, c_planes=YP)
-    ops.gemm_group([pr], ws)
-    ref = torch.relu(X.double() @ W.double().t())
-    ok, msg = gemm_close(Y.cpu().numpy(), ref.cpu().numpy(),
-                         (X.double().abs() @ W.double().abs().t()).cpu().numpy(), K + 4)
-    assert ok, msg
-    assert torch.equal(YP, _planes(ops, Y))
-    # dgrad with ReLU' of X
-    G = torch.randn(Bt, Nout, device=dev)
-    GP = _planes(ops, G)
-    dX = torch.zeros(Bt, K, device=dev)
-    dXP = ops.planes_empty(Bt, K, dev)
-    pd, _ = ops.gemm_problem(G, W[:, :K], C=dX, epilogue=ops.EPI_DRELU, aux=X, a_planes=GP,
-                             b_planes=WP, c_planes=dXP)
-    ops.gemm_group([pd], ws)
-    ref = (G.double() @ W[:, :K].double()) * (X[:, :K] > 0)
-    ok, msg = gemm_close(dX.cpu().numpy(), ref.cpu().numpy(),
-                         (G.double().abs() @ W[:, :K].double().abs()).cpu().numpy(), Nout)
-    assert ok, msg
-    assert torch.equal(dXP, _planes(ops, dX))
-    # wgrad + SGD + bias row sums: FULL vs PARTIAL + REDUCE, weight planes kept in step
-    kw = dict(trans_a=True, alpha=0.5, epilogue=ops.EPI_SGD, ones_col=K, a_planes=GP,
-              b_planes=XP)
-    W1, W1P = W.clone(), WP.clone()
-    pw, _ = ops.gemm_problem(G, X[:, :K], C=W1, c_planes=W1P, **kw)
-    ops.gemm_group([pw], ws)
-    s = max(2, ops.gemm_splits(pw, partial=True))
-    W2, W2P = W.clone(), WP.clone()
-    part = torch.empty(ops.gemm_partial_bytes(Nout, K, s) // 4, device=dev)
-    pp, _ = ops.gemm_problem(G, X[:, :K], C=W2, c_planes=W2P, partial=part,
-                             splits=ops.gemm_splits(pw, partial=True, requested=s), **kw)
-    ops.gemm_group([pp], ws)
-    ops.gemm_group([ops.reduce_problem(pp)], ws)
-    torch.cuda.synchronize()
-    assert torch.equal(W1P, _planes(ops, W1)) and torch.equal(W2P, _planes(ops, W2))
-    gd, Xd = G.double().cpu(), X[:, :K].double().cpu()
-    for Wn in (W1, W2):
-        got = (W - Wn).double().cpu() / 0.5
-        ok, msg = gemm_close(got[:, :K].numpy(), (gd.t() @ Xd).numpy(),
-                             (gd.abs().t() @ Xd.abs()).numpy(), Bt + 8)
-        assert ok, msg
-        ok, msg = gemm_close(got[:, K].numpy(), gd.sum(0).numpy(), gd.abs().sum(0).numpy(),
-                             Bt + 8)
-        assert ok, msg
-
-
-@pytest.mark.gpu
-def test_gemm_planes_group_and_env_off(ops, monkeypatch):
-    """A grouped launch of pre-split problems (dgrad + PARTIAL wgrad + an earlier layer's
-    REDUCE) equals the same problems launched alone, bitwise; DLRM_GEMM_PLANES=0 gives the
-    exact-f32 result bitwise."""
-    torch.manual_seed(7)
-    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
-    Bt, K, N = 2048, 512, 1024
-    G = torch.randn(Bt, N, device=dev)
-    X = torch.relu(torch.randn(Bt, K + 4, device=dev))
-    W = torch.randn(N, K + 4, device=dev) * 0.05
-    GP, XP, WP = _planes(ops, G), _planes(ops, X), _planes(ops, W)
-
-    def problems(dX, W_, WP_, part):
-        pd, _ = ops.gemm_problem(G, W[:, :K], C=dX, epilogue=ops.EPI_DRELU, aux=X,
-                                 a_planes=GP, b_planes=WP)
-        pw0, _ = ops.gemm_problem(G, X[:, :K], trans_a=True, C=W_, alpha=0.1,
-                                  epilogue=ops.EPI_SGD, ones_col=K, a_planes=GP, b_planes=XP,
-                                  c_planes=WP_)
-        s = max(2, ops.gemm_splits(pw0, partial=True))
-        pw, _ = ops.gemm_problem(G, X[:, :K], trans_a=True, C=W_, alpha=0.1,
-                                 epilogue=ops.EPI_SGD, ones_col=K, a_planes=GP, b_planes=XP,
-                                 c_planes=WP_, partial=part, splits=s)
-        return pd, pw
-    part = torch.empty(ops.gemm_partial_bytes(N, K, 32) // 4, device=dev)
-    dX1, W1, W1P = torch.zeros(Bt, K, device=dev), W.clone(), WP.clone()
-    pd, pw = problems(dX1, W1, W1P, part)
-    ops.gemm_group([pd, pw], ws)
-    ops.gemm_group([ops.reduce_problem(pw)], ws)
-    dX2, W2, W2P = torch.zeros(Bt, K, device=dev), W.clone(), WP.clone()
-    pd, pw = problems(dX2, W2, W2P, part)
-    ops.gemm_group([pd], ws)
-    ops.gemm_group([pw], ws)
-    ops.gemm_group([ops.reduce_problem(pw)], ws)
-    torch.cuda.synchronize()
-    assert torch.equal(dX1, dX2) and torch.equal(W1, W2) and torch.equal(W1P, W2P)
-    monkeypatch.setenv("DLRM_GEMM_PLANES", "0")
-    dX3 = torch.zeros(Bt, K, device=dev)
-    pd, _ = ops.gemm_problem(G, W[:, :K], C=dX3, epilogue=ops.EPI_DRELU, aux=X, a_planes=GP,
-                             b_planes=WP)
-    ops.gemm_group([pd], ws)
-    dX4 = ops.gemm(G, W[:, :K], epilogue=ops.EPI_DRELU, aux=X, workspace=ws)
-    torch.cuda.synchronize()
-    assert torch.equal(dX3, dX4)
-
-
-@pytest.mark.gpu
-def test_gemm_c_planes_on_the_generic_path(ops):
-    """Unaligned operands (the generic kernel, and its row-sum kernel for ones_col) keep
-    c_planes in step with C too: a weight updated there must not leave stale planes."""
-    torch.manual_seed(11)
-    G, X = torch.randn(6, 3, device=dev), torch.randn(6, 7, device=dev)
-    W = torch.randn(3, 8, device=dev)
-    WP = _planes(ops, W)
-    pw, _ = ops.gemm_problem(G, X, trans_a=True, C=W, alpha=0.1, epilogue=ops.EPI_SGD,
-                             ones_col=7, c_planes=WP)
-    ops.gemm_group([pw])
-    torch.cuda.synchronize()
-    assert torch.equal(WP, _planes(ops, W))

@@ -95,11 +95,8 @@ def _rand_batch(rng, rows, B, L, m_den, loss, dist="uniform"):
 
 
 @pytest.mark.parametrize("name", list(CASES))
-@pytest.mark.parametrize("planes", ["0", "1"])
-def test_step_vs_oracle(name, planes, monkeypatch):
-    """Two steps vs the oracle, on the exact-f32 GEMMs and with the top MLP on split-bf16
-    planes (DLRM_GEMM_PLANES=1: pre-split x6d body, c_planes kept by every producer)."""
-    monkeypatch.setenv("DLRM_GEMM_PLANES", planes)
+def test_step_vs_oracle(name):
+    """Two steps vs the oracle."""
     DLRMTrainer, TrainerConfig = _trainer()
     c = CASES[name]
     D, rows = c["D"], c["rows"]
@@ -109,7 +106,6 @@ def test_step_vs_oracle(name, planes, monkeypatch):
     cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"], ln_top=ln_top,
                         loss_function=c["loss"], learning_rate=c["lr"])
     tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
-    assert tr.use_planes == (planes == "1")
     rng = np.random.RandomState(3)
     for s in range(2):
         X, lS_o, lS_i, T = _rand_batch(rng, rows, c["B"], c["L"], c["bot"][0], c["loss"])
@@ -505,19 +501,26 @@ def test_gather_fused_step_matches_pooled_path(graph):
         assert torch.equal(a, b)
 
 
-def test_c4_terabyte_widths_trajectory_vs_oracle():
+@pytest.mark.parametrize("lr", [1e-4, 1e-3])
+def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     """C4 (QR mult, 4 collisions, threshold 200 + RWSAdagrad) at the Terabyte widths (D = 128,
     bot 13-512-256-128, top 479-1024-1024-512-256-1) with the 26 tables capped at 20k rows,
-    B = 256, lr 1e-3: 10 steps on 10 batches against the oracle's QREmbeddingBag +
-    RWSAdagrad.  The reference's own trajectory at this lr swings (saturated sigmoid after
-    step 1, recovery by step ~10: tools/c4_lr_probe.py); the engine must follow it."""
+    B = 256: 10 steps on 10 batches against the oracle's QREmbeddingBag + RWSAdagrad.
+    Every step: Z and the loss within the 1e-5 bound (the loss only on steps whose sigmoid
+    is not saturated: a clamped log(0) turns a 1-ulp difference of p into O(10) of loss).
+    After the last step: every quotient / remainder / plain table and its row-wise momentum
+    within 1e-5, the dense weights and their Adagrad sums within 1e-5 up to rare ReLU
+    boundary flips.  lr 1e-4 is the bench's C4 lr (no saturation); at 1e-3 the reference's
+    own trajectory swings through saturation (tools/c4_lr_probe.py) and the engine must
+    follow it."""
     import bench
+    from conftest import fp32_close_relu_flips
     DLRMTrainer, TrainerConfig = _trainer()
     c = bench.CONFIGS["terabyte_qr_rwsadagrad"]
     rows = [min(r, 20000) for r in c["rows"]]
     D, bot = c["D"], c["bot"]
     ln_top = [_num_int(len(rows), D)] + c["top"]
-    B, lr, thr = 256, 1e-3, c["qr"]["threshold"]
+    B, thr = 256, c["qr"]["threshold"]
     np.random.seed(0)
     torch.manual_seed(0)
     ref = O.OracleDLRM(D, rows, bot, ln_top, loss_function="bce")
@@ -531,6 +534,7 @@ def test_c4_terabyte_widths_trajectory_vs_oracle():
     opt = O.RWSAdagradOracle(ref.parameters(), lr=lr)
     rng = np.random.RandomState(1)
     losses = []
+    n_loss_checked = 0
     for s in range(10):
         X, lS_o, lS_i, T = _rand_batch(rng, rows, B, 1, bot[0], "bce")
         Xt, ot, it, Tt = (torch.tensor(X), torch.tensor(lS_o), [torch.tensor(i) for i in lS_i],
@@ -541,10 +545,36 @@ def test_c4_terabyte_widths_trajectory_vs_oracle():
         Er.backward()
         opt.step()
         Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
-        losses.append((round(E.item(), 4), round(Er.item(), 4)))
-        ok, msg = fp32_close(E.cpu().numpy(), [Er.item()], atol=1e-4)
-        assert ok, (s, losses, msg)
+        losses.append((round(E.item(), 5), round(Er.item(), 5)))
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.detach().numpy().ravel())
+        assert ok, (s, "Z", losses, msg)
+        zr = Zr.detach().double()
+        if bool(((zr > 1e-6) & (zr < 1 - 1e-6)).all()):  # no sample saturated
+            n_loss_checked += 1
+            ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
+            assert ok, (s, "loss", losses, msg)
     print("C4 losses (engine, oracle):", losses)
+    if lr <= 1e-4:
+        assert n_loss_checked == 10
+    torch.cuda.synchronize()
+    tr.check_errors()
+    for t, e in enumerate(ref.emb_l):
+        got_w, got_m = tr.table(t), tr.table_momentum(t)
+        parts = [(e.weight_q, got_w[0], got_m[0]), (e.weight_r, got_w[1], got_m[1])] \
+            if hasattr(e, "weight_q") else [(e.weight, got_w, got_m)]
+        for p, gw, gm in parts:
+            ok, msg = fp32_close(gw.cpu().numpy(), p.detach().numpy())
+            assert ok, ("table", t, msg)
+            ok, msg = fp32_close(gm.cpu().numpy(), opt.state[id(p)]["momentum"].numpy())
+            assert ok, ("momentum", t, msg)
+    lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
+    for L, (W, b), (sW, sb) in zip(lin, tr.dense_state(), tr.dense_adagrad_state()):
+        for got, p in ((W, L.weight), (b, L.bias)):
+            ok, msg = fp32_close_relu_flips(got.cpu().numpy(), p.detach().numpy())
+            assert ok, ("dense", msg)
+        for got, p in ((sW, L.weight), (sb, L.bias)):
+            ok, msg = fp32_close_relu_flips(got.cpu().numpy(), opt.state[id(p)]["sum"].numpy())
+            assert ok, ("adagrad sum", msg)
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -579,5 +609,38 @@ def test_c3_zipf_hot_rows_vs_oracle(graph):
         ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
         assert ok, (s, msg)
         ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
+        assert ok, (s, msg)
+    _compare_state(tr, ref)
+
+
+@pytest.mark.parametrize("name", ["c3_small", "c2_small"])
+@pytest.mark.parametrize("graph", [False, True])
+def test_bottom_backward_chain_schedule_vs_oracle(name, graph):
+    """bot_sched="chain": the bottom MLP's data gradients in one row-block launch
+    (dlrm_mlp_chain_backward) and every bottom wgrad (in-launch split-K, SGD fused) plus the
+    top MLP's pending reduce job in one grouped launch; C3 (3 bottom layers) and C2 (4
+    layers: 5 problems in the group) widths, 2 steps vs the oracle, eager and replayed."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    ln_top = [_num_int(len(rows), D)] + c["top"]
+    np.random.seed(7)
+    ref = O.OracleDLRM(D, rows, c["bot"], ln_top, loss_function=c["loss"])
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"], ln_top=ln_top,
+                        loss_function=c["loss"], learning_rate=c["lr"])
+    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
+    tr.bot_sched = "chain"
+    rng = np.random.RandomState(3)
+    for s in range(2):
+        X, lS_o, lS_i, T = _rand_batch(rng, rows, c["B"], c["L"], c["bot"][0], c["loss"])
+        Zr, Er = ref.train_step(torch.tensor(X), torch.tensor(lS_o),
+                                [torch.tensor(i) for i in lS_i], torch.tensor(T), c["lr"])
+        b = tr.make_batch(X, lS_o, lS_i, T)
+        if graph and s > 0:
+            tr.capture(b)()
+            Z = tr._cur["prob"]
+        else:
+            Z, _ = tr.step(b)
+        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
         assert ok, (s, msg)
     _compare_state(tr, ref)

@@ -1,5 +1,5 @@
 """Time each trainer GEMM shape (tools/gemm_sweep.py's problems) under a list of tile
-configs (DLRM_GEMM_CFG values, with the plan table's split), graph-timed.
+configs (ops.tuning gemm_tile overrides, with the plan table's split), graph-timed.
 
     python tools/gemm_cfg_ab.py [--batches 2048] [--cfgs 64x32,64x32x2x1,...]
 """
@@ -43,21 +43,16 @@ def main():
             for name, mk in cases:
                 res = []
                 for c in ["plan"] + cfgs:
-                    os.environ.pop("DLRM_GEMM_CFG", None)
-                    os.environ.pop("DLRM_GEMM_SPLIT", None)
                     pr0 = mk()
                     s = ops.gemm_splits(pr0)
-                    if c != "plan":
-                        os.environ["DLRM_GEMM_CFG"] = c
-                        os.environ["DLRM_GEMM_SPLIT"] = str(s)
+                    tile = 0 if c == "plan" else int(c.split("x")[0]) * 1000 + int(c.split("x")[1])
                     pr = mk()
-                    t = timeit(lambda: ops.gemm_group([pr], ws))
+                    with ops.tuning(gemm_tile=tile, gemm_split=s if tile else 0):
+                        t = timeit(lambda: ops.gemm_group([pr], ws))
                     tot[c] += t
                     res.append(f"{c}:{t * 1e6:.1f}")
                 fl = 2 * B * N * K
                 print(f"B{B} L{li} {name:5s} {fl / 1e9:.2f} GF  " + "  ".join(res), flush=True)
-    os.environ.pop("DLRM_GEMM_CFG", None)
-    os.environ.pop("DLRM_GEMM_SPLIT", None)
     print("TOTAL " + "  ".join(f"{c}:{t * 1e6:.1f}" for c, t in tot.items()))
 
 

@@ -29,10 +29,9 @@ def main():
     ap.add_argument("--cfg", default="")
     ap.add_argument("--split", default="")
     args = ap.parse_args()
-    if args.cfg:
-        os.environ["DLRM_GEMM_CFG"] = args.cfg
-    if args.split:
-        os.environ["DLRM_GEMM_SPLIT"] = args.split
+    if args.cfg:  # plan override (dlrm_set_tuning, this thread)
+        bm, bn = (int(v) for v in args.cfg.split("x")[:2])
+        ops.tuning(gemm_tile=bm * 1000 + bn, gemm_split=int(args.split or 0)).__enter__()
     dev = "cuda"
     B, K, N = args.B, args.K, args.N
     Kp = pad4(K + 1)

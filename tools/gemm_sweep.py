@@ -19,6 +19,8 @@ CFGS = ["64x64", "32x64", "64x32", "128x64", "64x128"]
 LAYERS = {  # (K, N) of the C3 (terabyte) layers
     "terabyte": [(13, 512), (512, 256), (256, 128), (479, 1024), (1024, 1024), (1024, 512),
                  (512, 256)],
+    # C2 (Criteo Kaggle): bot 13-512-256-64-16, top 367-512-256 (the 256 -> 1 head is not a GEMM)
+    "kaggle": [(13, 512), (512, 256), (256, 64), (64, 16), (367, 512), (512, 256)],
 }
 
 
@@ -50,6 +52,7 @@ def main():
     ap.add_argument("--batches", default="2048")
     ap.add_argument("--layers", default="terabyte")
     ap.add_argument("--out", default="")
+    ap.add_argument("--fwd-splits", action="store_true", help="also sweep K splits of fwd/dgrad")
     args = ap.parse_args()
     dev = "cuda"
     ws = torch.zeros(256 << 20, dtype=torch.uint8, device=dev)
@@ -81,21 +84,19 @@ def main():
                                                 epilogue=ops.EPI_SGD, partial=part, splits=s)[0]
                 nw = Kp
             cases.append(("wgrad", 2, N, nw, B, [1, 2, 3, 4, 6, 8, 12, 16], wg))
+            if args.fwd_splits:  # latency-bound small batches: split the K of fwd / dgrad too
+                cases = [(n_, l_, m_, nn_, kk_, sp_ if n_ == "wgrad" else [1, 2, 4, 8, 16], f_)
+                         for n_, l_, m_, nn_, kk_, sp_, f_ in cases]
             for name, layout, M, Nn, KK, splits, mk in cases:
-                for k in ("DLRM_GEMM_CFG", "DLRM_GEMM_SPLIT"):
-                    os.environ.pop(k, None)
                 t_def = timeit(lambda: ops.gemm_group([mk(0)], ws))
                 res = []
                 for cfg in CFGS:
-                    os.environ["DLRM_GEMM_CFG"] = cfg
+                    bm_, bn_ = (int(v) for v in cfg.split("x"))
                     for s in splits:
-                        os.environ["DLRM_GEMM_SPLIT"] = str(s)
-                        if name == "wgrad":
-                            pr = mk(s)
-                        else:
-                            pr = mk(0)
+                        pr = mk(s) if name == "wgrad" else mk(0)
                         try:
-                            t = timeit(lambda: ops.gemm_group([pr], ws))
+                            with ops.tuning(gemm_tile=bm_ * 1000 + bn_, gemm_split=s):
+                                t = timeit(lambda: ops.gemm_group([pr], ws))
                         except Exception as e:  # noqa: BLE001
                             print("skip", name, cfg, s, e, flush=True)
                             continue
@@ -111,8 +112,6 @@ def main():
                       + " ".join(f"{c}s{sp}:{tt * 1e6:.1f}" for tt, c, sp in res[:6]), flush=True)
                 plans.append(dict(M=M, N=Nn, K=KK, layout=layout, bm=bm, bn=bn, split=s,
                                   us=round(t * 1e6, 1)))
-    for k in ("DLRM_GEMM_CFG", "DLRM_GEMM_SPLIT"):
-        os.environ.pop(k, None)
     print(f"TOTAL default {tot_def * 1e6:.1f} us, best {tot_best * 1e6:.1f} us")
     if args.out:
         json.dump(plans, open(args.out, "w"), indent=1)

@@ -28,12 +28,6 @@ for rows in (TB, TB[:1], [3]):
         t = timeit(lambda: ops.tbe_backward("sgd", W, rb, T, B, idx, off, G, lr=1e-6,
                                             workspace=ws, max_lookups_per_table=mx))
         res.append(f"hint={mx}: {t * 1e6:.1f} us")
-    for prb in ("1", "2"):  # sort timing probes: ranking only / ranking + scan
-        os.environ["DLRM_SEGSORT_PROBE"] = prb
-        t = timeit(lambda: ops.tbe_backward("sgd", W, rb, T, B, idx, off, G, lr=1e-6,
-                                            workspace=ws, max_lookups_per_table=B))
-        res.append(f"probe{prb}: {t * 1e6:.1f} us")
-    os.environ.pop("DLRM_SEGSORT_PROBE")
     ops.tbe_forward_presort(W, rb, T, B, idx, off, ws, B)
     t = timeit(lambda: ops.tbe_backward("sgd", W, rb, T, B, idx, off, G, lr=1e-6, workspace=ws,
                                         max_lookups_per_table=B, presorted=True))
