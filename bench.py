@@ -597,6 +597,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
     ap.add_argument("--bot-sched", default="", help="A/B: bottom-MLP backward schedule "
                     "(partial | full | chain; default: the trainer's)")
+    ap.add_argument("--tune", default="", help="A/B: library plan overrides, e.g. "
+                    "gemm_sched=1 (dlrm_set_tuning keys, ops.TUNE_KEYS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -624,6 +626,11 @@ def main():
         pg = dist.group.WORLD
 
     from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+    tune = None
+    if args.tune:
+        from dlrm_hip import ops
+        tune = ops.tuning(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
+        tune.__enter__()  # this (launching) thread, for the whole run
 
     c = dict(CONFIGS[args.config])
     if args.lr > 0:
@@ -832,7 +839,8 @@ def main():
                        "lookups_per_bag": c["L"], "bot": c["bot"], "top": ln_top,
                        "optimizer": c["optimizer"], "qr": c.get("qr"),
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
-                       "hip_graph": use_graph, "bot_sched": tr.bot_sched},
+                       "hip_graph": use_graph, "bot_sched": tr.bot_sched,
+                       "tune": args.tune or None},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,
             "comm": comm,
             "loss_before_timed": loss_first, "loss_last": loss, "lr": c["lr"],

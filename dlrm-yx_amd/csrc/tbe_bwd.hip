@@ -899,8 +899,9 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
 
 // One workgroup per table: exclusive scan of its NB * J counts in (digit, tile) order.
 // hist is [t][j][d]: thread d walks the tiles of digit d (coalesced across the threads,
-// eight loads in flight), the digit totals are scanned across the workgroup, then each
-// thread rewrites its digit's column with base + running count.
+// 32 loads in flight: the C1 shape's J = 50 tiles in two round trips), the digit totals
+// are scanned across the workgroup, then each thread rewrites its digit's column with
+// base + running count.
 template <int DB>
 __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const TiledPass a,
                                                                       const void* off_v,
@@ -925,7 +926,7 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const Tile
   }
   uint32_t* h = a.hist + (int64_t)t * a.J * NB;
   const int J = a.J;
-  constexpr int U = 8;
+  constexpr int U = 32 / DPT;
   // digits d0 .. d0+DPT-1 of this thread (NB < threads: the first NB threads only)
   const int d0 = tid * DPT;
   const bool active = d0 < NB;
