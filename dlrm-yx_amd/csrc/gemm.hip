@@ -450,13 +450,8 @@ __device__ __forceinline__ void finish_tile(const GemmParams& p, const f32x4 (&a
 
 // One output tile (and K split) of problem p: the software-pipelined 16x16x4 body.  The
 // workgroup is WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile.
-// SCHED (A/B, dlrm_set_tuning DLRM_TUNE_GEMM_SCHED): 0 = the schedule above; 1 = early
-// barrier (the K-tile's barrier right after the last staging store, tile t+1's fragments
-// read under the REST of tile t's k-steps); 2 = two staging register sets, so a K-tile's
-// global loads are issued two K-tiles before their LDS store instead of one.
-template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS, int SCHED = 0>
+template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS>
 __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* smem) {
-  constexpr bool EB = SCHED == 1, PD2 = SCHED == 2;
   constexpr int NT = WGM * WGN * 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -494,8 +489,8 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   for (int i = 0; i < FM; ++i) rs[i] = 0.f;
 
   const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
-  SA sa, sa2;  // (sa2, sb2: the second staging set of SCHED 2)
-  SB sb, sb2;
+  SA sa;
+  SB sb;
   // buffer descriptors over exactly the addressed extent (host guarantees < 2 GiB)
   const int64_t a_ext = A_KC ? (p.M - 1) * p.lda + p.K : (p.K - 1) * p.lda + p.M;
   const int64_t b_ext = B_KC ? (p.N - 1) * p.ldb + p.K : (p.K - 1) * p.ldb + p.N;
@@ -510,20 +505,18 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   const int a_step = A_KC ? kBK * 4 : (int)(kBK * p.lda * 4);
   const int b_step = B_KC ? kBK * 4 : (int)(kBK * p.ldb * 4);
   const int kb32 = (int)kbeg, K32 = (int)p.K;
-  auto fetch_in = [&](SA& xa, SB& xb, int c, int t) {  // staged float4 c of K-tile t
+  auto fetch_one = [&](int c, int t) {  // staged float4 c of K-tile t (unused past nk)
     if (c < SA::NV)
-      xa.fetch4(c, fa, ra, a_step, t, kb32 + t * kBK, K32);
+      sa.fetch4(c, fa, ra, a_step, t, kb32 + t * kBK, K32);
     else
-      xb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * kBK, K32);
+      sb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * kBK, K32);
   };
-  auto put_from = [&](const SA& xa, const SB& xb, int c, float* buf) {
+  auto put_one = [&](int c, float* buf) {
     if (c < SA::NV)
-      xa.store_one(c, buf, tid);
+      sa.store_one(c, buf, tid);
     else
-      xb.store_one(c - SA::NV, buf + SA::SIZE, tid);
+      sb.store_one(c - SA::NV, buf + SA::SIZE, tid);
   };
-  auto fetch_one = [&](int c, int t) { fetch_in(sa, sb, c, t); };  // (unused past nk)
-  auto put_one = [&](int c, float* buf) { put_from(sa, sb, c, buf); };
   auto read_frags = [&](const float* buf, float (&a)[FM][KL], float (&b)[FN][KL]) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) sa.template frag<KL>(buf, wm0 + i * 16, l16, kq * KL, a[i]);
@@ -541,10 +534,6 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   for (int c = 0; c < NS; ++c) put_one(c, smem);
 #pragma unroll
   for (int c = 0; c < NS; ++c) fetch_one(c, 1);
-  if constexpr (PD2) {
-#pragma unroll
-    for (int c = 0; c < NS; ++c) fetch_in(sa2, sb2, c, 2);
-  }
   __syncthreads();
   read_frags(smem, a, b);
 
@@ -552,68 +541,8 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   // barrier, then tile t+1's fragments into (na, nb) under the last k-step.  The loop is
   // unrolled by two so the fragment sets ping-pong without register copies.
   auto iteration = [&](int kt, float (&ca)[FM][KL], float (&cb)[FN][KL], float (&na)[FM][KL],
-                       float (&nb)[FN][KL], SA& xa, SB& xb) {
+                       float (&nb)[FN][KL]) {
     float* nbuf = smem + ((kt + 1) & 1) * (SA::SIZE + SB::SIZE);
-    if constexpr (PD2) {
-      // set (xa, xb) holds tile t+1 (fetched two K-tiles ago): store it, refill with t+3
-#pragma unroll
-      for (int s = 0; s < KL - 1; ++s) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][s], cb[j][s], acc[i][j], 0, 0, 0);
-        if constexpr (RS) {
-#pragma unroll
-          for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][s]);
-        }
-        if (s < NS) {
-          put_from(xa, xb, s, nbuf);
-          fetch_in(xa, xb, s, kt + 3);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      __syncthreads();
-      read_frags(nbuf, na, nb);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][KL - 1], cb[j][KL - 1], acc[i][j],
-                                                           0, 0, 0);
-      if constexpr (RS) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][KL - 1]);
-      }
-      return;
-    }
-    if constexpr (EB) {
-      // stores of tile t+1 under k-steps 0..NS-1, barrier, its fragments read under the
-      // remaining k-steps (both fragment sets are live there: the ping-pong pair)
-#pragma unroll
-      for (int s = 0; s < KL; ++s) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][s], cb[j][s], acc[i][j], 0, 0, 0);
-        if constexpr (RS) {
-#pragma unroll
-          for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][s]);
-        }
-        if (s < NS) {
-          put_one(s, nbuf);
-          fetch_one(s, kt + 2);
-        }
-        if (s == NS - 1) {
-          __syncthreads();  // tile t+1 complete in LDS; every read of buffer t is done
-          read_frags(nbuf, na, nb);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      return;
-    }
 #pragma unroll
     for (int s = 0; s < KL - 1; ++s) {
 #pragma unroll
@@ -647,9 +576,9 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   };
   float a1[FM][KL], b1[FN][KL];
   for (int kt = 0; kt < nk; kt += 2) {
-    iteration(kt, a, b, a1, b1, sa, sb);
+    iteration(kt, a, b, a1, b1);
     if (kt + 1 >= nk) break;
-    iteration(kt + 1, a1, b1, a, b, sa2, sb2);
+    iteration(kt + 1, a1, b1, a, b);
   }
 
   // Row sums: lanes l16, l16+16, l16+32, l16+48 hold the four k-quarters of row l16
@@ -715,7 +644,7 @@ __host__ __device__ constexpr int kind_bit(int layout, bool rs) { return 1 << (r
 // Up to kMaxGroup independent problems; block -> (problem, tile, split) after the XCD remap.
 // KINDS is the set of body kinds compiled in (a launch uses the smallest instantiation that
 // covers its problems: fewer bodies, fewer registers).
-template <int BM, int BN, int WGM, int WGN, int KINDS, int SCHED = 0>
+template <int BM, int BN, int WGM, int WGN, int KINDS>
 __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
     const GemmGroup g) {
   __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
@@ -733,15 +662,15 @@ __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
   if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
   const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
   if constexpr ((KINDS & 1) != 0)
-    if (kind == 0) return pipe_body<BM, BN, WGM, WGN, true, true, false, SCHED>(p, lb, smem);
+    if (kind == 0) return pipe_body<BM, BN, WGM, WGN, true, true, false>(p, lb, smem);
   if constexpr ((KINDS & 2) != 0)
-    if (kind == 1) return pipe_body<BM, BN, WGM, WGN, true, false, false, SCHED>(p, lb, smem);
+    if (kind == 1) return pipe_body<BM, BN, WGM, WGN, true, false, false>(p, lb, smem);
   if constexpr ((KINDS & 4) != 0)
-    if (kind == 2) return pipe_body<BM, BN, WGM, WGN, false, false, false, SCHED>(p, lb, smem);
+    if (kind == 2) return pipe_body<BM, BN, WGM, WGN, false, false, false>(p, lb, smem);
   if constexpr ((KINDS & 8) != 0)
-    if (kind == 3) return pipe_body<BM, BN, WGM, WGN, false, true, false, SCHED>(p, lb, smem);
+    if (kind == 3) return pipe_body<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
   if constexpr ((KINDS & 16) != 0)
-    if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true, SCHED>(p, lb, smem);
+    if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
 }
 
 // Fallback for operands the pipelined body cannot take (unaligned rows, ragged float4
@@ -1035,22 +964,16 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
   // row sums, two wgrads), else all kinds
-  const int64_t sched = dlrm::tuning(DLRM_TUNE_GEMM_SCHED);
-#define K_(M_)                                                                                \
-  case M_:                                                                                   \
-    if (sched == 1)                                                                          \
-      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_, 1>), grid, block, 0, st, g); \
-    else if (sched == 2)                                                                     \
-      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_, 2>), grid, block, 0, st, g); \
-    else                                                                                     \
-      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g);   \
+  switch (kinds) {
+#define K_(M_)                                                                          \
+  case M_:                                                                             \
+    hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g); \
     break;
-  switch (kinds) {  // (any other mix runs on the all-kinds instantiation)
     K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
-    default:
-      switch (31) { K_(31) }
-  }
 #undef K_
+    default:
+      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
+  }
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32");
   return DLRM_OK;
 }

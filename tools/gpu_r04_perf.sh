@@ -25,16 +25,6 @@ ab)
     python -c "import json;d=json.load(open('$OUT/ab_b256_$s.json'));print('b256 $s',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
   done
   ;;
-eb)
-  for t in 0 1 2; do
-    $B --tune gemm_sched=$t --steps 300 --warmup 30 > "$OUT/eb_$t.json" 2> "$OUT/eb_$t.err" || exit $?
-    python -c "import json;d=json.load(open('$OUT/eb_$t.json'));print('eb $t',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
-  done
-  for t in 0 2 1 0 2 1; do
-    $B --tune gemm_sched=$t --steps 300 --warmup 30 > "$OUT/eb2_$t.json" 2>> "$OUT/eb_$t.err" || exit $?
-    python -c "import json;d=json.load(open('$OUT/eb2_$t.json'));print('eb $t',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
-  done
-  ;;
 trace)
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c3 ${BOT:+--bot-sched $BOT} || exit $?
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c2 --config kaggle ${BOT:+--bot-sched $BOT} || exit $?
