@@ -596,9 +596,14 @@ def main():
                          "steps, so the clocks have left their idle state (tools/ramp_probe.py)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
     ap.add_argument("--bot-sched", default="", help="A/B: bottom-MLP backward schedule "
-                    "(partial | full | chain; default: the trainer's)")
+                    "(partial | full | chain | auto; default: the trainer's)")
+    ap.add_argument("--tbe-role", type=int, default=-1, help="A/B: 1 = the embedding update's "
+                    "passes ride on the bottom-backward GEMM launches, 0 = own launches "
+                    "(default: the trainer's)")
+    ap.add_argument("--tbe-role-at", default="", help="A/B: bottom-backward launches "
+                    "carrying the update's two passes, e.g. 0,2")
     ap.add_argument("--tune", default="", help="A/B: library plan overrides, e.g. "
-                    "gemm_sched=1 (dlrm_set_tuning keys, ops.TUNE_KEYS)")
+                    "gemm_tile=64032 (dlrm_set_tuning keys, ops.TUNE_KEYS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -648,6 +653,10 @@ def main():
     tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, process_group=pg, seed=1)
     if args.bot_sched:
         tr.bot_sched = args.bot_sched
+    if args.tbe_role >= 0:
+        tr.tbe_role = bool(args.tbe_role)
+    if args.tbe_role_at:
+        tr.tbe_role_at = tuple(int(v) for v in args.tbe_role_at.split(","))
     nb = 10  # the reference cycles 10 pre-generated batches (dlrm_data_pytorch.py:631)
     batches = [tr.synthetic_batch(B, c["L"], seed=100 + i) for i in range(nb)]
     torch.cuda.synchronize()
@@ -839,7 +848,8 @@ def main():
                        "lookups_per_bag": c["L"], "bot": c["bot"], "top": ln_top,
                        "optimizer": c["optimizer"], "qr": c.get("qr"),
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
-                       "hip_graph": use_graph, "bot_sched": tr.bot_sched,
+                       "hip_graph": use_graph, "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
+                       "tbe_role_at": list(tr.tbe_role_at),
                        "tune": args.tune or None},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,
             "comm": comm,

@@ -39,6 +39,7 @@
 #include <type_traits>
 
 #include "common.hpp"
+#include "tbe_bwd_roles.hpp"
 
 namespace {
 
@@ -645,13 +646,10 @@ __host__ __device__ constexpr int kind_bit(int layout, bool rs) { return 1 << (r
 // KINDS is the set of body kinds compiled in (a launch uses the smallest instantiation that
 // covers its problems: fewer bodies, fewer registers).
 template <int BM, int BN, int WGM, int WGN, int KINDS>
-__global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
-    const GemmGroup g) {
-  __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
+__device__ __forceinline__ void group_body(const GemmGroup& g, int b, float* smem) {
   // Problems own consecutive PHYSICAL block ranges, so each one is dealt round-robin over
   // all eight XCDs (a remap across the whole launch would give each problem a few XCDs);
   // inside its range the XCD remap gives each XCD a contiguous run of that problem's tiles.
-  const int b = blockIdx.x;
   int q = 0;
 #pragma unroll
   for (int i = 1; i < kMaxGroup; ++i)
@@ -671,6 +669,27 @@ __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
     if (kind == 3) return pipe_body<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
   if constexpr ((KINDS & 16) != 0)
     if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
+}
+
+template <int BM, int BN, int WGM, int WGN, int KINDS>
+__global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
+    const GemmGroup g) {
+  __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
+  group_body<BM, BN, WGM, WGN, KINDS>(g, blockIdx.x, smem);
+}
+
+// The group plus one pass of a deferred embedding update (tbe_bwd_roles.hpp) in the same
+// launch: workgroups [0, r.blocks) run the pass (dispatched first: its HBM-latency-bound
+// waves start before the GEMM tiles fill the CUs), the rest the GEMM problems.  Tiles
+// 64x32 / 32x64 only, at >= 4 waves per SIMD (<= 128 VGPRs: the pass alone would take
+// twice that, and the GEMM tiles would run at half their occupancy).
+template <int BM, int BN, int WGM, int WGN, int PHASE>
+__global__ __launch_bounds__(WGM * WGN * 64, 4) void gemm_role_kernel(const GemmGroup g,
+                                                                      const TbeBwdRole r) {
+  __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
+  const int b = blockIdx.x;
+  if (b < r.blocks) return tbe_role_run<PHASE>(r, b);
+  group_body<BM, BN, WGM, WGN, 31>(g, b - r.blocks, smem);
 }
 
 // Fallback for operands the pipelined body cannot take (unaligned rows, ragged float4
@@ -919,7 +938,8 @@ size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
 }
 
 template <int BM, int BN, int WGM = 2, int WGN = 2>
-int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes, hipStream_t st) {
+int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes,
+                 const TbeBwdRole* role, int phase, hipStream_t st) {
   constexpr int NT = WGM * WGN * 64;
   GemmGroup g{};
   g.n = n;
@@ -961,6 +981,22 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   for (int i = 0; i < n; ++i)
     if (g.p[i].mode != DLRM_GEMM_REDUCE)
       kinds |= kind_bit(g.p[i].layout, g.p[i].layout == 2 && g.p[i].ones_col >= 0);
+  if constexpr ((BM == 64 && BN == 32) || (BM == 32 && BN == 64)) {
+    if (role) {  // + a deferred embedding-update pass (every body kind compiled in)
+      static_assert(NT == 256, "the update passes run 256-thread workgroups");
+      DLRM_REQUIRE((int64_t)role->blocks + blocks < INT32_MAX, DLRM_ERR_UNSUPPORTED,
+                   "dlrm_gemm_f32_group_role: too many workgroups");
+      const dim3 grid(role->blocks + g.total), block(NT);
+      if (phase == 1)
+        hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 1>), grid, block, 0, st, g, *role);
+      else
+        hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 2>), grid, block, 0, st, g, *role);
+      DLRM_LAUNCH_CHECK("dlrm_gemm_f32_group_role");
+      return DLRM_OK;
+    }
+  } else {
+    DLRM_REQUIRE(!role, DLRM_ERR_UNSUPPORTED, "dlrm_gemm_f32_group_role: tile %dx%d", BM, BN);
+  }
   const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
   // row sums, two wgrads), else all kinds
@@ -1053,11 +1089,15 @@ size_t ws_for(int n, const Desc* d) {
   Tile t;
   Plan pl[kMaxGroup];
   plan_launch(m, q, t, pl);
-  return group_ws_bytes(m, q, t, pl);
+  const size_t a = group_ws_bytes(m, q, t, pl);
+  const size_t b = group_ws_bytes(m, q, Tile{64, 32, 2, 2}, pl);  // as a role launch
+  return a > b ? a : b;
 }
 
-int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
-  DLRM_ARG(n >= 1 && n <= kMaxGroup, "dlrm_gemm_f32_group: 1..%d problems", kMaxGroup);
+int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st,
+        const TbeBwdRole* role = nullptr, int phase = 0) {
+  DLRM_ARG(n >= (role ? 0 : 1) && n <= kMaxGroup, "dlrm_gemm_f32_group: 1..%d problems",
+           kMaxGroup);
   Desc q[kMaxGroup];
   int m = 0;
   for (int i = 0; i < n; ++i) {
@@ -1075,21 +1115,24 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st) {
     }
     q[m++] = d[i];
   }
-  if (m == 0) return DLRM_OK;
+  if (m == 0 && !role) return DLRM_OK;
   Tile t;
   Plan pl[kMaxGroup];
   plan_launch(m, q, t, pl);
+  // a launch carrying an update pass runs 64x32 or 32x64 tiles (gemm_role_kernel; the tile
+  // shape does not change any result, ws_for sizes the workspace for 64x32 too)
+  if (role && !(t == Tile{64, 32, 2, 2}) && !(t == Tile{32, 64, 2, 2})) t = Tile{64, 32, 2, 2};
   const size_t need = group_ws_bytes(m, q, t, pl);
   if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: in-launch splits off
     // (PARTIAL / REDUCE plans pair with each other across launches: kept)
     for (int i = 0; i < m; ++i)
       if (q[i].mode == DLRM_GEMM_FULL) pl[i] = make_plan(1, q[i].K);
   }
-  if (t.bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, st);
-  if (t.bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, st);
-  if (t.bm == 32) return launch_group<32, 64>(m, q, pl, ws, ws_bytes, st);
-  if (t.bn == 32) return launch_group<64, 32>(m, q, pl, ws, ws_bytes, st);
-  return launch_group<64, 64>(m, q, pl, ws, ws_bytes, st);
+  if (t.bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, role, phase, st);
+  if (t.bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, role, phase, st);
+  if (t.bm == 32) return launch_group<32, 64>(m, q, pl, ws, ws_bytes, role, phase, st);
+  if (t.bn == 32) return launch_group<64, 32>(m, q, pl, ws, ws_bytes, role, phase, st);
+  return launch_group<64, 64>(m, q, pl, ws, ws_bytes, role, phase, st);
 }
 
 Desc desc_of(const dlrm_gemm_problem& g) {
@@ -1142,6 +1185,24 @@ extern "C" int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* probs, vo
   Desc d[kMaxGroup];
   for (int i = 0; i < n; ++i) d[i] = desc_of(probs[i]);
   return run(n, d, workspace, workspace_bytes, dlrm::as_stream(stream));
+}
+
+extern "C" int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* probs,
+                                        void* workspace, size_t workspace_bytes,
+                                        const dlrm_tbe_bwd_role* role, int32_t phase,
+                                        dlrm_stream_t stream) {
+  const char* name = "dlrm_gemm_f32_group_role";
+  const auto* r = reinterpret_cast<const TbeBwdRole*>(role);
+  DLRM_ARG(!r || r->magic == kRoleMagic, "%s: role not filled by dlrm_tbe_backward_defer", name);
+  if (!r || r->blocks == 0) {
+    if (n == 0) return DLRM_OK;
+    return dlrm_gemm_f32_group(n, probs, workspace, workspace_bytes, stream);
+  }
+  DLRM_ARG(phase == 1 || phase == 2, "%s: phase must be 1 or 2", name);
+  DLRM_ARG(n >= 0 && n <= kMaxGroup && (n == 0 || probs), "%s: 0..%d problems", name, kMaxGroup);
+  Desc d[kMaxGroup];
+  for (int i = 0; i < n; ++i) d[i] = desc_of(probs[i]);
+  return run(n, d, workspace, workspace_bytes, dlrm::as_stream(stream), r, phase);
 }
 
 extern "C" int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem) {

@@ -27,16 +27,11 @@
 #include <utility>
 
 #include "mlp_rows.hpp"
+#include "tbe_bwd_roles.hpp"
 #include "tbe_common.hpp"
 
 namespace {
 
-constexpr int CH = 16;  // sorted lookups per block (all gradient rows of a block in flight)
-// Large batches of lookups (>= kLongChN) use longer blocks (kLongCH): fewer runs cross a
-// block edge, so fewer partial rows and less combine work; still 16 gradient rows in
-// flight per lane group.  The partial buffer is sized for CH.
-constexpr int kLongCH = 64;
-constexpr int64_t kLongChN = 1 << 18;
 
 // ---------------------------------------------------------------- backward --
 // Per-lookup key: global row (row_base[t] + idx) or sentinel (out of range / outside bags),
@@ -344,436 +339,6 @@ __global__ __launch_bounds__(kMlpWaves * 64) void mlp_chain_bwd_kernel(const Mlp
   mlp_rows_bwd_body(mc, mg, blockIdx.x, lds);
 }
 
-// MODE_SGD_F16: exact SGD on fp16 weights (the fbgemm TBE's FP16 tables): the row is read
-// as fp16, updated in fp32 and stored back rounded to nearest even.
-enum { MODE_SGD = 0, MODE_ADAGRAD = 1, MODE_DENSE = 2, MODE_SGD_F16 = 3 };
-
-// Weight-row element access by mode: fp32 rows, or fp16 rows (W then points at halves).
-template <int MODE, int VW>
-__device__ __forceinline__ typename VecT<VW>::T wload(const float* __restrict__ W, int64_t row,
-                                                      int64_t D, int chunk) {
-  if constexpr (MODE == MODE_SGD_F16) {
-    const _Float16* h = reinterpret_cast<const _Float16*>(W) + row * D + (int64_t)chunk * VW;
-    if constexpr (VW == 4) {
-      const uint2 u = *reinterpret_cast<const uint2*>(h);
-      return make_float4((float)__builtin_bit_cast(_Float16, (unsigned short)(u.x & 0xffff)),
-                         (float)__builtin_bit_cast(_Float16, (unsigned short)(u.x >> 16)),
-                         (float)__builtin_bit_cast(_Float16, (unsigned short)(u.y & 0xffff)),
-                         (float)__builtin_bit_cast(_Float16, (unsigned short)(u.y >> 16)));
-    } else {
-      return (float)h[0];
-    }
-  } else {
-    return reinterpret_cast<const typename VecT<VW>::T*>(W + row * D)[chunk];
-  }
-}
-
-template <int MODE, int VW>
-__device__ __forceinline__ void wstore(float* __restrict__ W, int64_t row, int64_t D, int chunk,
-                                       const typename VecT<VW>::T& v) {
-  if constexpr (MODE == MODE_SGD_F16) {
-    _Float16* h = reinterpret_cast<_Float16*>(W) + row * D + (int64_t)chunk * VW;
-    if constexpr (VW == 4) {
-      auto bits = [](float f) { return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)f); };
-      uint2 u;
-      u.x = bits(v.x) | (bits(v.y) << 16);
-      u.y = bits(v.z) | (bits(v.w) << 16);
-      *reinterpret_cast<uint2*>(h) = u;
-    } else {
-      h[0] = (_Float16)v;
-    }
-  } else {
-    reinterpret_cast<typename VecT<VW>::T*>(W + row * D)[chunk] = v;
-  }
-}
-
-// Apply the coalesced gradient g of one row (group-uniform control flow).
-template <int LPB, int VW, int MAXV, int MODE>
-__device__ __forceinline__ void finalize_row(float* __restrict__ W, float* __restrict__ mom,
-                                             int64_t D, int64_t row,
-                                             typename VecT<VW>::T (&g)[MAXV], int gl,
-                                             int nchunks, float lr, float eps) {
-  using V = typename VecT<VW>::T;
-  V* wrow = reinterpret_cast<V*>(W + row * D);
-  if (MODE == MODE_SGD || MODE == MODE_SGD_F16) {
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int chunk = gl + c * LPB;
-      if (chunk < nchunks) {
-        V w = wload<MODE, VW>(W, row, D, chunk);
-        vfma(w, -lr, g[c]);
-        wstore<MODE, VW>(W, row, D, chunk, w);
-      }
-    }
-  } else if (MODE == MODE_DENSE) {
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int chunk = gl + c * LPB;
-      if (chunk < nchunks) {
-        V w = wrow[chunk];
-        vadd(w, g[c]);
-        wrow[chunk] = w;
-      }
-    }
-  } else {  // RWSAdagrad: momentum += mean(g^2); w -= lr * g / (sqrt(momentum) + eps)
-    float sq = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c)
-      if (gl + c * LPB < nchunks) sq += vdot(g[c]);
-#pragma unroll
-    for (int m = LPB / 2; m >= 1; m >>= 1) sq += __shfl_xor(sq, m, kWave);
-    const float mnew = mom[row] + sq / (float)D;
-    if (gl == 0) mom[row] = mnew;
-    const float denom = sqrtf(mnew) + eps;
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int chunk = gl + c * LPB;
-      if (chunk < nchunks) {
-        V w = wrow[chunk];
-        V u = g[c];
-        if constexpr (VW == 4) {
-          u.x /= denom;
-          u.y /= denom;
-          u.z /= denom;
-          u.w /= denom;
-        } else {
-          u /= denom;
-        }
-        vfma(w, -lr, u);
-        wrow[chunk] = w;
-      }
-    }
-  }
-}
-
-// finalize_row with the row's weights (and momentum) already in registers: the load was
-// issued with the gradient rows, so the read-modify-write costs no extra HBM round trip.
-template <int LPB, int VW, int MAXV, int MODE>
-__device__ __forceinline__ void finalize_row_pf(float* __restrict__ W, float* __restrict__ mom,
-                                                int64_t D, int64_t row,
-                                                typename VecT<VW>::T (&g)[MAXV],
-                                                typename VecT<VW>::T (&w)[MAXV], float m0,
-                                                int gl, int nchunks, float lr, float eps) {
-  using V = typename VecT<VW>::T;
-  V* wrow = reinterpret_cast<V*>(W + row * D);
-  if (MODE == MODE_SGD || MODE == MODE_SGD_F16) {
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int chunk = gl + c * LPB;
-      if (chunk < nchunks) {
-        V x = w[c];
-        vfma(x, -lr, g[c]);
-        wstore<MODE, VW>(W, row, D, chunk, x);
-      }
-    }
-  } else if (MODE == MODE_DENSE) {
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int chunk = gl + c * LPB;
-      if (chunk < nchunks) {
-        V x = w[c];
-        vadd(x, g[c]);
-        wrow[chunk] = x;
-      }
-    }
-  } else {
-    float sq = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c)
-      if (gl + c * LPB < nchunks) sq += vdot(g[c]);
-#pragma unroll
-    for (int m = LPB / 2; m >= 1; m >>= 1) sq += __shfl_xor(sq, m, kWave);
-    const float mnew = m0 + sq / (float)D;
-    if (gl == 0) mom[row] = mnew;
-    const float denom = sqrtf(mnew) + eps;
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      const int chunk = gl + c * LPB;
-      if (chunk < nchunks) {
-        V x = w[c];
-        V u = g[c];
-        if constexpr (VW == 4) {
-          u.x /= denom;
-          u.y /= denom;
-          u.z /= denom;
-          u.w /= denom;
-        } else {
-          u /= denom;
-        }
-        vfma(x, -lr, u);
-        wrow[chunk] = x;
-      }
-    }
-  }
-}
-
-// SB: bag_of is indexed by sorted position (per-table sort) instead of by lookup position
-template <int LPB, int VW, int MAXV, typename KeyT, int MODE, bool SB>
-__global__ __launch_bounds__(256) void tbe_bwd_block_kernel(
-    float* __restrict__ W, float* __restrict__ mom, int64_t D, int B,
-    const KeyT* __restrict__ keys, const int32_t* __restrict__ pos,
-    const int32_t* __restrict__ bag_of, const float* __restrict__ psw,
-    const float* __restrict__ gout, int64_t gbs, int64_t N, float lr, float eps,
-    KeyT sentinel, float* __restrict__ partial, int ch) {
-  using V = typename VecT<VW>::T;
-  constexpr int GPW = kWave / LPB;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane / LPB;
-  const int gl = lane - g * LPB;
-  const int nchunks = (int)(D / VW);
-  const int64_t nblocks = (N + ch - 1) / ch;
-  const int64_t wave_id = (int64_t)xcd_contiguous(blockIdx.x, gridDim.x) * (blockDim.x / kWave) +
-                          threadIdx.x / kWave;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
-
-  for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {
-    const int64_t k = k0 + g;
-    if (k >= nblocks) continue;
-    const int64_t i0 = k * ch;
-    const int64_t i1 = (i0 + ch < N) ? i0 + ch : N;
-    const bool has_prev = i0 > 0;
-    const bool has_next = i1 < N;
-    const KeyT prev_key = has_prev ? keys[i0 - 1] : sentinel;
-    const KeyT next_key = has_next ? keys[i1] : sentinel;
-
-    V acc[MAXV], comp[MAXV];  // run sum, Kahan-compensated (hot rows: long runs)
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) vzero(acc[c]), vzero(comp[c]);
-    KeyT cur = sentinel;
-    int64_t seg_a = i0;
-    bool have = false;
-
-    // PF: the weight row (and momentum) of every run start in a chunk is loaded together
-    // with the chunk's gradient rows (MAXV == 1 keeps that within the register budget)
-    constexpr bool PF = MAXV == 1;
-    V wcur[MAXV];
-    float mcur = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) vzero(wcur[c]);
-
-    auto flush = [&](int64_t b_end) {
-      if (cur == sentinel) return;
-#pragma unroll
-      for (int c = 0; c < MAXV; ++c) vsub(acc[c], comp[c]);  // fold the compensation in
-      const bool starts = (seg_a > i0) || !has_prev || (prev_key != cur);
-      const bool ends = (b_end < i1) || !has_next || (next_key != cur);
-      if (starts && ends) {
-        if constexpr (PF)
-          finalize_row_pf<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)cur, acc, wcur, mcur, gl,
-                                               nchunks, lr, eps);
-        else
-          finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)cur, acc, gl, nchunks, lr, eps);
-      } else {
-        V* dst = reinterpret_cast<V*>(partial + (2 * k + (seg_a == i0 ? 0 : 1)) * D);
-#pragma unroll
-        for (int c = 0; c < MAXV; ++c)
-          if (gl + c * LPB < nchunks) dst[gl + c * LPB] = acc[c];
-      }
-    };
-
-    // a sub-batch is SUB lookups (>= 16: narrow rows keep 16 gradient rows in flight), each
-    // lane of the group holding R = SUB / LPB of them
-    constexpr int SUB = LPB >= 16 ? LPB : 16;
-    constexpr int R = SUB / LPB;
-    for (int64_t base = i0; base < i1; base += SUB) {
-      const int n = (int)((i1 - base) < SUB ? (i1 - base) : SUB);
-      KeyT my_key[R];
-      int64_t my_off[R];
-      float my_w[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        my_key[r] = sentinel;
-        my_off[r] = -1;
-        my_w[r] = 1.f;
-        const int li = r * LPB + gl;
-        if (li < n) {
-          my_key[r] = keys[base + li];
-          int32_t bag;
-          if constexpr (SB) {
-            bag = bag_of[base + li];
-            if (psw) my_w[r] = psw[pos[base + li]];
-          } else {
-            const int32_t p = pos[base + li];
-            bag = p >= 0 ? bag_of[p] : -1;
-            if (psw && p >= 0) my_w[r] = psw[p];
-          }
-          if (bag >= 0) {
-            const int t = bag / B;
-            const int b = bag - t * B;
-            my_off[r] = (int64_t)b * gbs + (int64_t)t * D;
-          }
-        }
-      }
-      constexpr int U = SUB < CH ? SUB : CH;  // gradient rows in flight per group (ch >= CH)
-      for (int j = 0; j < n; j += U) {
-        KeyT ku[U];
-        int64_t ou[U];
-        float wu[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          // lookup li of the sub-batch: lane li % LPB of the group, its register li / LPB
-          // (R > 1 only for LPB < 16, where U == SUB and j == 0: li is a constant)
-          static_assert(R == 1 || U == SUB, "narrow rows: one pass per sub-batch");
-          const int li = R == 1 ? ((j + u) < LPB ? (j + u) : 0) : u;
-          const int src = g * LPB + (R == 1 ? li : li % LPB);
-          const int rr = R == 1 ? 0 : li / LPB;
-          if constexpr (sizeof(KeyT) == 8)
-            ku[u] = (KeyT)__shfl((long long)my_key[rr], src, kWave);
-          else
-            ku[u] = (KeyT)__shfl((int)my_key[rr], src, kWave);
-          ou[u] = __shfl(my_off[rr], src, kWave);
-          wu[u] = __shfl(my_w[rr], src, kWave);
-          if (j + u >= n) ou[u] = -1;
-        }
-        V gv[U][MAXV];
-        V wv[PF ? U : 1][MAXV];
-        float mv[PF ? U : 1];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-#pragma unroll
-          for (int c = 0; c < MAXV; ++c) {
-            const int chunk = gl + c * LPB;
-            if (ou[u] >= 0 && chunk < nchunks) {
-              gv[u][c] = reinterpret_cast<const V*>(gout + ou[u])[chunk];
-              if (psw) vscale(gv[u][c], wu[u]);
-            } else {
-              vzero(gv[u][c]);
-            }
-          }
-          if constexpr (PF) {
-            // rows starting a run inside the chunk (repeats of one row load it once)
-            const bool lead = (j + u < n) && ku[u] != sentinel && (u == 0 || ku[u] != ku[u - 1]);
-#pragma unroll
-            for (int c = 0; c < MAXV; ++c) {
-              const int chunk = gl + c * LPB;
-              if (lead && chunk < nchunks)
-                wv[u][c] = wload<MODE, VW>(W, (int64_t)ku[u], D, chunk);
-              else
-                vzero(wv[u][c]);
-            }
-            mv[u] = (MODE == MODE_ADAGRAD && lead) ? mom[ku[u]] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (j + u < n) {
-            if (!have || ku[u] != cur) {
-              if (have) flush(base + j + u);
-              have = true;
-              cur = ku[u];
-              seg_a = base + j + u;
-#pragma unroll
-              for (int c = 0; c < MAXV; ++c) vzero(acc[c]), vzero(comp[c]);
-              if constexpr (PF) {
-#pragma unroll
-                for (int c = 0; c < MAXV; ++c) wcur[c] = wv[u][c];
-                mcur = mv[u];
-              }
-            }
-#pragma unroll
-            for (int c = 0; c < MAXV; ++c) vkahan(acc[c], comp[c], gv[u][c]);
-          }
-        }
-      }
-    }
-    if (have) flush(i1);
-  }
-}
-
-template <int LPB, int VW, int MAXV, typename KeyT, int MODE>
-__global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
-    float* __restrict__ W, float* __restrict__ mom, int64_t D, const KeyT* __restrict__ keys,
-    int64_t N, float lr, float eps, KeyT sentinel, const float* __restrict__ partial, int ch) {
-  using V = typename VecT<VW>::T;
-  constexpr int GPW = kWave / LPB;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane / LPB;
-  const int gl = lane - g * LPB;
-  const int nchunks = (int)(D / VW);
-  const int64_t nblocks = (N + ch - 1) / ch;
-  const int64_t wave_id = (int64_t)xcd_contiguous(blockIdx.x, gridDim.x) * (blockDim.x / kWave) +
-                          threadIdx.x / kWave;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
-
-  for (int64_t k0 = wave_id * GPW; k0 < nblocks; k0 += nwaves * GPW) {
-    const int64_t k = k0 + g;
-    if (k >= nblocks) continue;
-    const int64_t i0 = k * ch;
-    const int64_t i1 = (i0 + ch < N) ? i0 + ch : N;
-    if (i1 >= N) continue;
-    const KeyT last = keys[i1 - 1];
-    if (last == sentinel || keys[i1] != last) continue;  // run ends inside this block
-    // start of the last segment: first index of the block holding `last` (keys sorted)
-    int64_t a = i1;
-    for (int64_t i = i0 + gl; i < i1; i += LPB)
-      if (keys[i] == last && i < a) a = i;
-#pragma unroll
-    for (int m = LPB / 2; m >= 1; m >>= 1) {
-      const int64_t o = __shfl_xor(a, m, kWave);
-      a = o < a ? o : a;
-    }
-    const bool starts = (a > i0) || (i0 == 0) || (keys[i0 - 1] != last);
-    if (!starts) continue;  // the block where the run starts combines it
-    // Last block of the run: the run is contiguous, so "block kk continues it" (its first
-    // key equals `last`) holds for kk = k+1 .. kend and fails after.  The group's lanes
-    // probe LPB blocks per round in parallel instead of walking them one by one.
-    int64_t kend = k + 1;  // blocks k+1 .. kend-1 ... resolved below (kend = last one)
-    {
-      int64_t base = k + 1;
-      while (true) {
-        const int64_t kk = base + gl;
-        const bool cont = kk < nblocks && keys[kk * ch] == last;
-        // groups are LPB-aligned lane ranges: find the first lane (in order) that fails
-        uint64_t fail = __ballot(!cont);
-        if constexpr (LPB < 64) fail = (fail >> ((lane / LPB) * LPB)) & ((1ull << LPB) - 1);
-        if (fail) {
-          kend = base + __builtin_ctzll(fail) - 1;
-          break;
-        }
-        base += LPB;
-      }
-    }
-    V acc[MAXV];
-    const V* src = reinterpret_cast<const V*>(partial + (2 * k + (a == i0 ? 0 : 1)) * D);
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) {
-      if (gl + c * LPB < nchunks)
-        acc[c] = src[gl + c * LPB];
-      else
-        vzero(acc[c]);
-    }
-    // partials of blocks k+1 .. kend in block order, NF loads in flight, Kahan-compensated
-    // (a hot row's run crosses hundreds of blocks)
-    V comp[MAXV];
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) vzero(comp[c]);
-    constexpr int NF = MAXV <= 2 ? 16 : 8;
-    for (int64_t kk0 = k + 1; kk0 <= kend; kk0 += NF) {
-      V pv[NF][MAXV];
-#pragma unroll
-      for (int u = 0; u < NF; ++u) {
-        const int64_t kk = kk0 + u;
-        const V* s2 = reinterpret_cast<const V*>(partial + (2 * kk) * D);
-#pragma unroll
-        for (int c = 0; c < MAXV; ++c) {
-          if (kk <= kend && gl + c * LPB < nchunks)
-            pv[u][c] = s2[gl + c * LPB];
-          else
-            vzero(pv[u][c]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < NF; ++u)
-        if (kk0 + u <= kend) {
-#pragma unroll
-          for (int c = 0; c < MAXV; ++c) vkahan(acc[c], comp[c], pv[u][c]);
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < MAXV; ++c) vsub(acc[c], comp[c]);  // fold the compensation back in
-    finalize_row<LPB, VW, MAXV, MODE>(W, mom, D, (int64_t)last, acc, gl, nchunks, lr, eps);
-  }
-}
 
 // The per-table LDS sort applies (and dlrm_tbe_forward_presort can run it early).
 inline bool presort_applies(size_t key_bytes, int64_t max_seg, int64_t N) {
@@ -1195,7 +760,12 @@ template <typename KeyT, typename IdxT, typename OffT>
 int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
                const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
                const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
-               int64_t max_seg, int32_t* err, int presorted, hipStream_t st, const char* name) {
+               int64_t max_seg, int32_t* err, int presorted, TbeBwdRole* defer, hipStream_t st,
+               const char* name) {
+  if (defer) {  // until proven fusable: nothing deferred
+    *defer = TbeBwdRole{};
+    defer->magic = kRoleMagic;
+  }
   if (N == 0) return DLRM_OK;
   const KeyT sentinel = (KeyT)total_rows;
   const int end_bit = bit_width_u64((uint64_t)total_rows);
@@ -1284,6 +854,20 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(nblocks, gpw), 4);
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
+  if (defer && sizeof(KeyT) == 4 && vec4 && maxv == 1 && (per_table || bags) &&
+      tbe_role_fusable(mode, lpb, psw, (int64_t)B * gbs)) {
+    TbeBwdRole& r = *defer;
+    r.W = W, r.mom = mom, r.psw = psw, r.gout = gout, r.partial = w.partial;
+    r.keys = reinterpret_cast<const uint32_t*>(w.keys_out);
+    r.pos = w.pos_out;
+    r.bag_of = per_table ? w.bag_of : w.pos_out;
+    r.D = D, r.gbs = gbs, r.N = N, r.lr = lr, r.eps = eps;
+    r.sentinel = (uint32_t)sentinel;
+    r.B = B, r.ch = ch, r.mode = mode, r.lpb = lpb;
+    // a multiple of 8 workgroups keeps the co-launched GEMM tiles' XCD remap aligned
+    r.blocks = (int32_t)(dlrm::ceil_div(blocks, (int64_t)8) * 8);
+    return DLRM_OK;
+  }
 #define LAUNCH2(LPB, VW, MV, MODE)                                                             \
   do {                                                                                         \
     if (per_table || bags)                                                                     \
@@ -1339,7 +923,7 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
                  int B, const void* idx, int ib, const void* off, int ob, int64_t N,
                  int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
                  float eps, void* ws, size_t ws_bytes, int64_t max_seg, int32_t* err,
-                 int presorted, dlrm_stream_t stream, const char* name) {
+                 int presorted, TbeBwdRole* defer, dlrm_stream_t stream, const char* name) {
   DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
@@ -1355,7 +939,8 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
                "%s: %lld rows in one call (at most 2^32 - 2)", name, (long long)total_rows);
 #define BWD(K, I, O)                                                                     \
   return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
-                             gout, gbs, lr, eps, ws, ws_bytes, max_seg, err, presorted, st, name)
+                             gout, gbs, lr, eps, ws, ws_bytes, max_seg, err, presorted, defer, \
+                             st, name)
   if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
   if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
   if (ib == 64 && ob == 32) BWD(uint32_t, int64_t, int32_t);
@@ -1385,7 +970,7 @@ extern "C" int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* r
   return bwd_dispatch(MODE_SGD, weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, lr, 0.f, workspace, workspace_bytes,
-                      max_lookups_per_table, error_flag, presorted, stream,
+                      max_lookups_per_table, error_flag, presorted, nullptr, stream,
                       "dlrm_tbe_backward_sgd");
 }
 
@@ -1402,7 +987,7 @@ extern "C" int dlrm_tbe_backward_sgd_f16(void* weights, int64_t D, const int64_t
   return bwd_dispatch(MODE_SGD_F16, static_cast<float*>(weights), nullptr, D, row_base, T, B,
                       indices, index_bits, offsets, offset_bits, num_lookups, total_rows,
                       per_sample_weights, grad_out, grad_batch_stride, lr, 0.f, workspace,
-                      workspace_bytes, max_lookups_per_table, error_flag, presorted, stream,
+                      workspace_bytes, max_lookups_per_table, error_flag, presorted, nullptr, stream,
                       "dlrm_tbe_backward_sgd_f16");
 }
 
@@ -1417,7 +1002,7 @@ extern "C" int dlrm_tbe_backward_rowwise_adagrad(
   return bwd_dispatch(MODE_ADAGRAD, weights, momentum, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, lr, eps, workspace, workspace_bytes,
-                      max_lookups_per_table, error_flag, presorted, stream,
+                      max_lookups_per_table, error_flag, presorted, nullptr, stream,
                       "dlrm_tbe_backward_rowwise_adagrad");
 }
 
@@ -1433,8 +1018,36 @@ extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int
   return bwd_dispatch(MODE_DENSE, grad_weights, nullptr, D, row_base, T, B, indices, index_bits,
                       offsets, offset_bits, num_lookups, total_rows, per_sample_weights,
                       grad_out, grad_batch_stride, 0.f, 0.f, workspace, workspace_bytes,
-                      max_lookups_per_table, error_flag, presorted, stream,
+                      max_lookups_per_table, error_flag, presorted, nullptr, stream,
                       "dlrm_tbe_backward_dense");
+}
+
+static_assert(sizeof(TbeBwdRole) <= sizeof(dlrm_tbe_bwd_role), "dlrm_tbe_bwd_role too small");
+
+extern "C" int dlrm_tbe_backward_defer(
+    int32_t mode, float* weights, float* momentum, int64_t D, const int64_t* row_base,
+    int32_t T, int32_t B, const void* indices, int32_t index_bits, const void* offsets,
+    int32_t offset_bits, int64_t num_lookups, int64_t total_rows,
+    const float* per_sample_weights, const float* grad_out, int64_t grad_batch_stride, float lr,
+    float eps, int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes,
+    int32_t* error_flag, int32_t presorted, dlrm_tbe_bwd_role* role, dlrm_stream_t stream) {
+  const char* name = "dlrm_tbe_backward_defer";
+  DLRM_ARG(role, "%s: null role", name);
+  DLRM_ARG(mode == 0 || mode == 1, "%s: mode must be 0 (sgd) or 1 (rowwise adagrad)", name);
+  DLRM_ARG(mode == 0 || momentum, "%s: rowwise adagrad needs momentum", name);
+  auto* r = reinterpret_cast<TbeBwdRole*>(role);
+  *r = TbeBwdRole{};
+  r->magic = kRoleMagic;
+  return bwd_dispatch(mode == 0 ? MODE_SGD : MODE_ADAGRAD, weights, mode == 0 ? nullptr : momentum,
+                      D, row_base, T, B, indices, index_bits, offsets, offset_bits, num_lookups,
+                      total_rows, per_sample_weights, grad_out, grad_batch_stride, lr, eps,
+                      workspace, workspace_bytes, max_lookups_per_table, error_flag, presorted, r,
+                      stream, name);
+}
+
+extern "C" int32_t dlrm_tbe_bwd_role_blocks(const dlrm_tbe_bwd_role* role) {
+  const auto* r = reinterpret_cast<const TbeBwdRole*>(role);
+  return r && r->magic == kRoleMagic ? r->blocks : 0;
 }
 
 namespace {

@@ -58,8 +58,10 @@ __device__ __forceinline__ void vscale(float4& a, float w) {
   a.w *= w;
 }
 __device__ __forceinline__ void vscale(float& a, float w) { a *= w; }
+// explicit fmas: the contraction of a.x*a.x + ... would otherwise be the compiler's choice
+// per translation unit (the update passes run from two of them and must agree bitwise)
 __device__ __forceinline__ float vdot(const float4& a) {
-  return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+  return fmaf(a.w, a.w, fmaf(a.z, a.z, fmaf(a.y, a.y, a.x * a.x)));
 }
 __device__ __forceinline__ float vdot(const float& a) { return a * a; }
 

@@ -48,6 +48,11 @@ class MlpChain(ctypes.Structure):
 
 
 # name -> (restype, argtypes); mirrors include/dlrm_hip.h exactly.
+class TbeBwdRole(ctypes.Structure):
+    """struct dlrm_tbe_bwd_role (include/dlrm_hip.h): a deferred embedding update."""
+    _fields_ = [("opaque", ctypes.c_uint64 * 20)]
+
+
 P = c_void_p
 SIGNATURES = {
     "dlrm_abi_version": (c_int32, []),
@@ -107,6 +112,12 @@ SIGNATURES = {
                                 P, c_int64, P, c_int64, c_int32, P, P, c_int64, P, c_size_t, P]),
     "dlrm_gemm_f32_group_workspace_size": (c_size_t, [c_int32, P]),
     "dlrm_gemm_f32_group": (c_int32, [c_int32, P, P, c_size_t, P]),
+    "dlrm_gemm_f32_group_role": (c_int32, [c_int32, P, P, c_size_t, P, c_int32, P]),
+    "dlrm_tbe_backward_defer": (c_int32, [c_int32, P, P, c_int64, P, c_int32, c_int32, P,
+                                          c_int32, P, c_int32, c_int64, c_int64, P, P,
+                                          c_int64, c_float, c_float, c_int64, P, c_size_t, P,
+                                          c_int32, P, P]),
+    "dlrm_tbe_bwd_role_blocks": (c_int32, [P]),
     "dlrm_gemm_f32_splits": (c_int32, [P]),
     "dlrm_gemm_f32_partial_bytes": (c_size_t, [c_int64, c_int64, c_int32]),
     "dlrm_colsum_workspace_size": (c_size_t, [c_int64, c_int64]),

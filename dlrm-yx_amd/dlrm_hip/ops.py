@@ -369,6 +369,45 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
         raise ValueError(mode)
 
 
+def tbe_backward_defer(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
+                       indices: torch.Tensor, offsets: torch.Tensor, grad_out: torch.Tensor,
+                       lr: float = 0.0, eps: float = 0.0,
+                       momentum: Optional[torch.Tensor] = None,
+                       per_sample_weights: Optional[torch.Tensor] = None,
+                       grad_batch_stride: Optional[int] = None,
+                       workspace: Optional[torch.Tensor] = None,
+                       max_lookups_per_table: int = 0,
+                       error_flag: Optional[torch.Tensor] = None, presorted: bool = False):
+    """tbe_backward ('sgd' on fp32 weights or 'rowwise_adagrad') with its two update passes
+    deferred (dlrm_tbe_backward_defer): returns the role to hand to gemm_group(...,
+    role=, phase=1) and then phase=2 - or None when the update already ran in full (shape
+    the fused passes do not cover).  The workspace, weights, momentum and grad_out must stay
+    untouched until phase 2 has run."""
+    _check_cuda(weights, row_base, indices, offsets, grad_out, momentum, per_sample_weights)
+    if weights.dtype != torch.float32 or mode not in ("sgd", "rowwise_adagrad"):
+        raise ValueError("tbe_backward_defer: fp32 'sgd' or 'rowwise_adagrad' only")
+    D = weights.shape[1]
+    N = indices.numel()
+    total_rows = weights.shape[0]
+    if grad_batch_stride is None:
+        grad_batch_stride = T * D
+    need = tbe_backward_workspace_size(N, total_rows, D)
+    if workspace is None:
+        workspace = _ws("tbe_bwd", need, weights.device)
+    role = _lib.TbeBwdRole()
+    _lib.call("dlrm_tbe_backward_defer", 0 if mode == "sgd" else 1, _p(weights), _p(momentum),
+              D, _p(row_base), T, B, _p(indices), _bits(indices), _p(offsets), _bits(offsets), N,
+              total_rows, _p(per_sample_weights), _p(grad_out), grad_batch_stride, lr, eps,
+              int(max_lookups_per_table), _p(workspace), workspace.numel(), _p(error_flag),
+              int(presorted), ctypes.byref(role), _stream(weights.device))
+    return role if tbe_role_blocks(role) > 0 else None
+
+
+def tbe_role_blocks(role) -> int:
+    """Workgroups a deferred update pass adds to the launch carrying it (0: none)."""
+    return 0 if role is None else _lib.query("dlrm_tbe_bwd_role_blocks", ctypes.byref(role))
+
+
 def tbe_expand_grad(D: int, T: int, B: int, offsets: torch.Tensor, num_lookups: int,
                     grad_out: torch.Tensor, per_sample_weights: Optional[torch.Tensor] = None,
                     grad_batch_stride: Optional[int] = None) -> torch.Tensor:
@@ -641,13 +680,16 @@ def gemm_group_workspace_size(problems) -> int:
                       ctypes.cast(_problems(problems), ctypes.c_void_p))
 
 
-def gemm_group(problems, workspace: Optional[torch.Tensor] = None, device=None) -> None:
-    """Launch up to 4 independent GEMM problems (gemm_problem structs) in ONE kernel.
+def gemm_group(problems, workspace: Optional[torch.Tensor] = None, device=None, role=None,
+               phase: int = 0) -> None:
+    """Launch up to 6 independent GEMM problems (gemm_problem structs) in ONE kernel.
     ``workspace``: zero-initialised uint8 buffer (split-K tickets + partials); a cached one
-    is used when None."""
+    is used when None.  ``role`` (tbe_backward_defer) + ``phase`` (1, then 2): that pass of
+    the deferred embedding update runs as extra workgroups of the same launch (problems
+    may then be empty)."""
     arr = _problems(problems)
     need = _lib.query("dlrm_gemm_f32_group_workspace_size", len(problems),
-                      ctypes.cast(arr, ctypes.c_void_p))
+                      ctypes.cast(arr, ctypes.c_void_p)) if problems else 0
     dev = device if device is not None else torch.cuda.current_device()
     if need and workspace is None:
         workspace = _ws("gemm", need, dev)
@@ -655,6 +697,11 @@ def gemm_group(problems, workspace: Optional[torch.Tensor] = None, device=None) 
         # never fall back to a shared buffer behind the caller's back: two streams could
         # then write split-K partials into the same scratch
         raise ValueError(f"gemm workspace too small: {workspace.numel()} < {need} bytes")
+    if role is not None:
+        _lib.call("dlrm_gemm_f32_group_role", len(problems), ctypes.cast(arr, ctypes.c_void_p),
+                  _p(workspace) if need else None, workspace.numel() if need else 0,
+                  ctypes.byref(role), int(phase), _stream(dev))
+        return
     _lib.call("dlrm_gemm_f32_group", len(problems), ctypes.cast(arr, ctypes.c_void_p),
               _p(workspace) if need else None, workspace.numel() if need else 0,
               _stream(dev))

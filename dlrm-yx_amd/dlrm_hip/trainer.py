@@ -218,14 +218,23 @@ class DLRMTrainer:
         self.group_wgrad = True
         self.full_last_wgrad = False
         # bottom-MLP backward schedule: "partial" (split wgrads reduced in the next launch),
-        # "full" (in-launch split-K, n_bot launches; bottom_bwd_full) or "chain" (the data
-        # gradients in one row-block launch, then every wgrad in one grouped launch)
-        self.bot_sched = "partial"
+        # "full" (in-launch split-K, n_bot launches; bottom_bwd_full), "chain" (the data
+        # gradients in one row-block launch, then every wgrad in one grouped launch) or
+        # "auto": full at <= 128 rows per GPU, else partial (measured, one MI355X: full
+        # 0.976 vs partial 0.857 M samples/s at the Kaggle shape, B = 128; partial ahead at
+        # C3 B = 2048, 4.67 vs 4.54 M, and at B = 256, 1.21 vs 1.19 M;
+        # profiles/r04_bot_sched_ab.txt)
+        self.bot_sched = "auto"
         # one GPU: the bottom MLP forward as a role of the lookup launch (mlp_rows.hpp)
         self.fuse_bottom = True
         # one GPU, one-hot batches: the dot interaction gathers the embedding rows itself
         # (dlrm_interact_dot_forward_gather); the lookup launch keeps only its sort role
         self.fuse_gather = True
+        # one GPU: the embedding update's passes as extra workgroups of the bottom-MLP
+        # backward's GEMM launches (dlrm_gemm_f32_group_role); False: launches of their own
+        self.tbe_role = True
+        self.tbe_role_at = (0, 1)  # bottom-backward launches carrying pass 1 and pass 2
+        self._roles = []  # pending (role, phase) passes for the next _gemm launches
         self.gather_fused = False  # set by the last step
         self.bottom_fused = False  # set by the last step
         # device TBE error bits (ops.TBE_ERR_*): out-of-range indices are skipped by the
@@ -750,7 +759,10 @@ class DLRMTrainer:
                 if chain is not None and self.n_bot >= 2:
                     with prof("gemm"):
                         return bottom_bwd_chain(chain)
-            if self.bot_sched == "full" and not c_bot and fused_opt:
+            sched = self.bot_sched
+            if sched == "auto":
+                sched = "full" if Bl <= 128 else "partial"
+            if sched == "full" and not c_bot and fused_opt:
                 return bottom_bwd_full()
             rq = st.pop("rq")
             g = bufs["gx"]  # dLoss/d(pre-ReLU bottom output), from the interaction backward
@@ -772,7 +784,9 @@ class DLRMTrainer:
             if rq:
                 self._gemm(rq, side=c_bot)
 
-        def emb_bwd():  # embedding backward + fused update
+        def emb_bwd(defer=False):  # embedding backward + fused update
+            """defer=True: the update's two passes are returned as a role for the next two
+            GEMM launches (None: it ran in full here)."""
             with prof("tbe_bwd"):
                 if self.T_local > 0:
                     mode = "rowwise_adagrad" if cfg.optimizer == "rwsadagrad" else "sgd"
@@ -783,11 +797,12 @@ class DLRMTrainer:
                                                      self._qr_pq, self._qr_pr, bufs["P"],
                                                      bufs["dE"], bufs["dP"])
                         grad = bufs["dP"]
-                    ops.tbe_backward(mode, self.weights, self.row_base, self.T_phys, B, idx, off,
-                                     grad, lr=elr, eps=cfg.adagrad_eps, momentum=self.momentum,
-                                     workspace=self._ws_tbe(idx.numel()),
-                                     max_lookups_per_table=batch.max_per_table,
-                                     error_flag=self.tbe_error_flag, presorted=presort)
+                    fn = ops.tbe_backward_defer if defer else ops.tbe_backward
+                    return fn(mode, self.weights, self.row_base, self.T_phys, B, idx, off,
+                              grad, lr=elr, eps=cfg.adagrad_eps, momentum=self.momentum,
+                              workspace=self._ws_tbe(idx.numel()),
+                              max_lookups_per_table=batch.max_per_table,
+                              error_flag=self.tbe_error_flag, presorted=presort)
 
         @record_function("## Backward ##")
         def backward_single():  # one GPU: bottom backward || embedding backward
@@ -798,9 +813,26 @@ class DLRMTrainer:
                     self._gemm(rq)
                 st["rq"] = []
                 s1.wait_stream(s0)
+            # the embedding update's two HBM-bound passes ride as extra workgroups on the
+            # first two (MFMA-bound) bottom-backward launches: overlap with no cross-queue
+            # dependency (dlrm_tbe_backward_defer / dlrm_gemm_f32_group_role)
+            deferred = (self.tbe_role and not c_bot and self.T_local > 0
+                        and self.weights.dtype == torch.float32)
+            if deferred:
+                role = emb_bwd(defer=True)
+                if role is not None:  # pass p rides on bottom-backward launch tbe_role_at[p-1]
+                    a, b = self.tbe_role_at
+                    self._roles = [None] * (b + 1)
+                    self._roles[a], self._roles[b] = (role, 1), (role, 2)
             with side_if(c_bot, s1):
                 bottom_bwd()
-            emb_bwd()
+            while self._roles:  # a pass the bottom backward had no launch left for
+                if self._roles[0] is None:
+                    self._roles.pop(0)
+                else:
+                    self._gemm([])
+            if not deferred:
+                emb_bwd()
             if c_bot:
                 s0.wait_stream(s1)
 
@@ -969,13 +1001,17 @@ class DLRMTrainer:
         return pr, ops.reduce_problem(pr)
 
     def _gemm(self, problems, side=False):
+        """One grouped launch; it also carries the next pending pass of a deferred
+        embedding update (self._roles, set by the single-GPU backward)."""
         with self._prof("gemm"):
             ws = self._cur["gemm_ws_side" if side else "gemm_ws"]
-            need = ops.gemm_group_workspace_size(problems)
+            need = ops.gemm_group_workspace_size(problems) if problems else 0
             if need > ws.numel():  # first use of a new group shape: grow (not in capture)
                 ws = torch.zeros(need, dtype=torch.uint8, device=self.dev)
                 self._cur["gemm_ws_side" if side else "gemm_ws"] = ws
-            ops.gemm_group(problems, ws, self.dev)
+            nxt = self._roles.pop(0) if self._roles and not side else None
+            role, phase = nxt if nxt is not None else (None, 0)
+            ops.gemm_group(problems, ws, self.dev, role=role, phase=phase)
 
     def _colsum(self, *args, **kw):
         with self._prof("colsum"):

@@ -99,7 +99,9 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  * 5: the split-bf16 planes and dlrm_split_planes are gone again (measured slower than the
  *    exact-f32 MFMA path in the step, profiles/r03_planes_*.txt): dlrm_gemm_problem ends
  *    at `partial`; dlrm_tbe_forward_presort's out = NULL (sort-only) mode is used by the
- *    engine (round 4). */
+ *    engine (round 4).
+ * 6: dlrm_tbe_backward_defer + dlrm_gemm_f32_group_role: the embedding backward's update
+ *    passes as extra workgroups of grouped GEMM launches (round 4). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 
@@ -325,6 +327,36 @@ int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_b
                             dlrm_stream_t stream);
 
 /*
+ * Deferred update (ABI v6): dlrm_tbe_backward_sgd (mode 0) or
+ * dlrm_tbe_backward_rowwise_adagrad (mode 1, momentum required) with the same arguments,
+ * except that the two update passes - the block pass over the sorted lookups and the
+ * combine pass over runs that cross blocks - are not launched: *role receives them, to
+ * run as extra workgroups of two later launches, phase 1 then phase 2, via
+ * dlrm_gemm_f32_group_role (typically the bottom-MLP backward's GEMM launches, which touch
+ * none of the TBE's buffers: the HBM-bound update overlaps the MFMA-bound GEMMs with no
+ * cross-stream dependency).  Everything before the passes (the sort, unless presorted)
+ * is launched here.  The result is bitwise the non-deferred call's.  role->blocks == 0
+ * after the call (not covered: D != 4*LPB for LPB in 4..32, unaligned rows, per-sample
+ * weights, B * grad_batch_stride >= 2^31, N == 0): the update ran in full here and the
+ * role passes are no-ops.  Until both phases have run, the workspace,
+ * weights, momentum and grad_out must stay as they are.
+ */
+typedef struct dlrm_tbe_bwd_role {
+  uint64_t opaque[20];
+} dlrm_tbe_bwd_role;
+int dlrm_tbe_backward_defer(int32_t mode, float* weights, float* momentum, int64_t D,
+                            const int64_t* row_base, int32_t T, int32_t B,
+                            const void* indices, int32_t index_bits, const void* offsets,
+                            int32_t offset_bits, int64_t num_lookups, int64_t total_rows,
+                            const float* per_sample_weights, const float* grad_out,
+                            int64_t grad_batch_stride, float lr, float eps,
+                            int64_t max_lookups_per_table, void* workspace,
+                            size_t workspace_bytes, int32_t* error_flag, int32_t presorted,
+                            dlrm_tbe_bwd_role* role, dlrm_stream_t stream);
+/* Workgroups a deferred pass adds to the launch that carries it (0: nothing deferred). */
+int32_t dlrm_tbe_bwd_role_blocks(const dlrm_tbe_bwd_role* role);
+
+/*
  * Sparse-gradient values of an EmbeddingBag(sparse=True) backward
  * (torch _embedding_bag_sparse_backward as reached from dlrm_s_pytorch.py:1929):
  *   values[l][:] = w_l * grad_out[b*grad_batch_stride + t*D + :] for lookup l of bag (t,b)
@@ -517,6 +549,13 @@ int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem);
 size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits);
 int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
                         size_t workspace_bytes, dlrm_stream_t stream);
+/* dlrm_gemm_f32_group plus pass `phase` (1 or 2) of a deferred embedding update
+ * (dlrm_tbe_backward_defer) as extra workgroups of the same launch; n may be 0 (the pass
+ * alone).  role == NULL, or a role with nothing deferred: dlrm_gemm_f32_group.  The
+ * problems must not touch the update's buffers (weights, momentum, grad_out, workspace). */
+int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
+                             size_t workspace_bytes, const dlrm_tbe_bwd_role* role,
+                             int32_t phase, dlrm_stream_t stream);
 
 /* Workspace for dlrm_colsum_f32 (deterministic two-pass column reduction). */
 size_t dlrm_colsum_workspace_size(int64_t M, int64_t N);

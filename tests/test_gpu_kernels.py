@@ -1007,6 +1007,82 @@ def test_tbe_backward_tiled_sort(ops, mode, invalid, idx_dtype):
         assert ok, msg
 
 
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
+@pytest.mark.parametrize("D", [16, 32, 64, 128, 6, 256])
+@pytest.mark.parametrize("sort", ["presorted", "per_table", "tiled", "global"])
+def test_tbe_backward_deferred_into_gemm_launches(ops, mode, D, sort):
+    """dlrm_tbe_backward_defer + the two passes as extra workgroups of grouped GEMM launches
+    (phase 1 beside a dgrad + wgrad pair, phase 2 alone or beside a FULL split-K problem):
+    the embedding update is bitwise the standalone dlrm_tbe_backward's and the GEMM results
+    bitwise the plain group launch's.  D = 6 (no float4 rows) and 256 (two chunks per lane)
+    are outside the fused variants: the role comes back None, the update already done."""
+    L = 40 if sort in ("tiled", "global") else 1
+    rows, B = [3, 5000, 700, 90000], 256
+    T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 21, invalid=True)
+    W0 = torch.randn(sum(rows), D, device=dev) * 0.1
+    mom0 = torch.rand(sum(rows), device=dev)
+    mx = B * L
+    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), sum(rows), D),
+                     dtype=torch.uint8, device=dev)
+    torch.manual_seed(3)
+    A1, B1 = torch.randn(300, 260, device=dev), torch.randn(260, 512, device=dev)
+    A2, B2 = torch.randn(512, 300, device=dev), torch.randn(512, 260, device=dev)
+    A3, B3 = torch.randn(64, 4096, device=dev), torch.randn(4096, 96, device=dev)
+
+    def probs():
+        p1, c1 = ops.gemm_problem(A1, B1)
+        p2, c2 = ops.gemm_problem(A2, B2, trans_a=True)
+        p3, c3 = ops.gemm_problem(A3, B3)  # FULL, split in-launch (K = 4096, 2 tiles)
+        return [p1, p2], [p3], (c1, c2, c3)
+
+    res = []
+    for defer in (False, True):
+        W, mom = W0.clone(), mom0.clone()
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ws.zero_()
+        gws = torch.zeros(1 << 22, dtype=torch.uint8, device=dev)
+        tune = dict(tbe_sort=1) if sort == "global" else {}
+        with ops.tuning(**tune):
+            if sort == "presorted":
+                assert ops.tbe_forward_presort(W0, row_base, T, B, idx, off, ws, mx,
+                                               error_flag=flag, lookup=False) is None
+            kw = dict(lr=0.3, eps=1e-8, momentum=mom, workspace=ws,
+                      max_lookups_per_table=0 if sort == "global" else mx, error_flag=flag,
+                      presorted=sort == "presorted")
+            first, second, outs = probs()
+            if defer:
+                role = ops.tbe_backward_defer(mode, W, row_base, T, B, idx, off, G, **kw)
+                fusable = D in (16, 32, 64, 128)
+                assert (role is not None) == fusable
+                assert ops.tbe_role_blocks(role) % 8 == 0
+                ops.gemm_group(first, gws, dev, role=role, phase=1)
+                ops.gemm_group([] if D == 16 else second, gws, dev, role=role, phase=2)
+                if D != 16:
+                    second = []
+            else:
+                ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, **kw)
+                ops.gemm_group(first, gws, dev)
+            if second:
+                ops.gemm_group(second, gws, dev)
+        torch.cuda.synchronize()
+        res.append((W.cpu(), mom.cpu(), flag.item(), [c.cpu() for c in outs]))
+    (w0, m0, f0, c0), (w1, m1, f1, c1) = res
+    assert torch.equal(w0, w1) and torch.equal(m0, m1)
+    assert f0 == f1 and f0 & ops.TBE_ERR_INDEX
+    for a, b in zip(c0, c1):
+        assert torch.equal(a, b)
+
+
+def test_gemm_group_role_rejects_a_foreign_role(ops):
+    """A role struct not filled by dlrm_tbe_backward_defer is refused (INVALID_ARG)."""
+    import ctypes
+    from dlrm_hip import _lib
+    role = _lib.TbeBwdRole()
+    ctypes.memset(ctypes.byref(role), 0x5a, ctypes.sizeof(role))
+    with pytest.raises(_lib.DLRMHipError):
+        ops.gemm_group([], None, dev, role=role, phase=1)
+
+
 def test_tbe_backward_tiled_sort_cap_violation(ops):
     """max_lookups_per_table underestimated (tiles cover 8192 of a table's 12800 lookups):
     that table is skipped (no update) and flagged; the others are updated."""

@@ -644,3 +644,55 @@ def test_bottom_backward_chain_schedule_vs_oracle(name, graph):
         ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
         assert ok, (s, msg)
     _compare_state(tr, ref)
+
+
+@pytest.mark.parametrize("name,sched,optimizer,at", [
+    ("c3_small", "partial", "sgd", (0, 1)), ("c3_small", "full", "sgd", (0, 1)),
+    ("c3_small", "chain", "sgd", (0, 1)), ("c2_small", "full", "sgd", (0, 1)),
+    ("c2_small", "partial", "rwsadagrad", (0, 1)), ("c3_small", "partial", "rwsadagrad", (0, 1)),
+    ("c3_small", "partial", "sgd", (0, 3)), ("c3_small", "partial", "sgd", (1, 2)),
+    ("c2_small", "full", "sgd", (2, 9))])
+@pytest.mark.parametrize("graph", [False, True])
+def test_tbe_update_roles_match_own_launches(name, sched, optimizer, at, graph):
+    """The embedding update's block and combine passes as extra workgroups of the first two
+    bottom-backward GEMM launches (tbe_role, dlrm_gemm_f32_group_role) vs their own
+    launches: 3 steps leave bitwise the same tables, momentum, dense parameters and
+    predictions, under each bottom-backward schedule (chain: one GEMM launch, so the
+    combine pass runs as a launch of its own), SGD and row-wise Adagrad, eager and
+    replayed from a captured graph; passes placed on later launches (tbe_role_at), the
+    second past the last launch (run as a launch of its own)."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function=c["loss"],
+                        learning_rate=c["lr"] if optimizer == "sgd" else 1e-3,
+                        optimizer=optimizer)
+    B = 256
+    res = []
+    for role in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.tbe_role = role
+        tr.tbe_role_at = at
+        tr.bot_sched = sched
+        batches = [tr.synthetic_batch(B, 1, seed=s) for s in range(3)]
+        if graph:
+            tr.step(batches[0])
+            run = tr.capture(batches[0])
+            for b in batches[1:]:
+                for src, dst in zip((b.X, b.offsets, b.indices, b.target),
+                                    (batches[0].X, batches[0].offsets, batches[0].indices,
+                                     batches[0].target)):
+                    dst.copy_(src)
+                run()
+        else:
+            for b in batches:
+                tr.step(b)
+        torch.cuda.synchronize()
+        tr.check_errors()
+        assert not tr._roles  # every deferred pass ran
+        mom = tr.momentum.cpu().clone() if tr.momentum is not None else None
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(), mom,
+                    tr._bufs[(B, B)]["prob"].cpu().clone()))
+    for a, b in zip(*res):
+        assert (a is None and b is None) or torch.equal(a, b)

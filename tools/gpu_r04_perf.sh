@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-4 perf session (one gpurun call):  bash tools/gpu_r04_perf.sh <stage>
 #   ab      - C3 / C2 / C3@B=256 bench lines, bottom-backward schedule partial vs chain
+#   ab2     - CFGS x SCHEDS bottom-backward schedule A/B
+#   role    - CFGS: the embedding update as GEMM-launch roles (--tbe-role 1) vs own launches
 #   trace   - one-step kernel timelines (C3 default, C2 default)
 #   sweep   - GEMM plan sweeps: Kaggle shapes at B=128 and C3 shapes at B=256 (fwd splits)
 set -o pipefail
@@ -23,6 +25,36 @@ ab)
     $B --batch 256 --bot-sched $s --steps 300 --warmup 30 > "$OUT/ab_b256_$s.json" \
       2> "$OUT/ab_b256_$s.err" || exit $?
     python -c "import json;d=json.load(open('$OUT/ab_b256_$s.json'));print('b256 $s',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+  done
+  ;;
+ab2)  # CFGS="terabyte kaggle b256" SCHEDS="partial full"
+  for cfg in ${CFGS:-terabyte kaggle b256}; do
+    for s in ${SCHEDS:-partial full}; do
+      if [ "$cfg" = b256 ]; then a="--batch 256"; else a="--config $cfg"; fi
+      $B $a --bot-sched $s --steps 300 --warmup 30 > "$OUT/ab_${cfg}_$s.json" \
+        2> "$OUT/ab_${cfg}_$s.err" || exit $?
+      python -c "import json;d=json.load(open('$OUT/ab_${cfg}_$s.json'));print('$cfg $s',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+    done
+  done
+  ;;
+role)  # the embedding update as GEMM-launch roles vs own launches
+  for cfg in ${CFGS:-terabyte kaggle b256}; do
+    for r in 0 1; do
+      if [ "$cfg" = b256 ]; then a="--batch 256"; else a="--config $cfg"; fi
+      $B $a --tbe-role $r --steps 300 --warmup 30 > "$OUT/role_${cfg}_$r.json" \
+        2> "$OUT/role_${cfg}_$r.err" || exit $?
+      python -c "import json;d=json.load(open('$OUT/role_${cfg}_$r.json'));print('$cfg role=$r',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+    done
+  done
+  ;;
+roleat)  # placement of the two passes: AT="0,1 0,2 ..."
+  for cfg in ${CFGS:-terabyte kaggle b256}; do
+    for at in ${AT:-0,1 0,2 0,3 1,2}; do
+      if [ "$cfg" = b256 ]; then a="--batch 256"; else a="--config $cfg"; fi
+      $B $a --tbe-role-at $at --steps 300 --warmup 30 > "$OUT/at_${cfg}_$at.json" \
+        2> "$OUT/at_${cfg}_$at.err" || exit $?
+      python -c "import json;d=json.load(open('$OUT/at_${cfg}_$at.json'));print('$cfg at=$at',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+    done
   done
   ;;
 trace)
