@@ -600,6 +600,12 @@ def main():
     ap.add_argument("--tbe-role", type=int, default=-1, help="A/B: 1 = the embedding update's "
                     "passes ride on the bottom-backward GEMM launches, 0 = own launches "
                     "(default: the trainer's)")
+    ap.add_argument("--sort-role", type=int, default=-1, help="A/B: 1 = the per-table sort "
+                    "rides on a top-MLP forward GEMM launch, 0 = in the lookup launch")
+    ap.add_argument("--sort-role-at", type=int, default=-1, help="A/B: which top-MLP forward "
+                    "GEMM launch carries the deferred sort")
+    ap.add_argument("--bottom-parts", type=int, default=-1, help="A/B: workgroups per 16-row "
+                    "block of the fused bottom MLP (1, 2, 4; 0 = auto)")
     ap.add_argument("--tbe-role-at", default="", help="A/B: bottom-backward launches "
                     "carrying the update's two passes, e.g. 0,2")
     ap.add_argument("--tune", default="", help="A/B: library plan overrides, e.g. "
@@ -655,6 +661,12 @@ def main():
         tr.bot_sched = args.bot_sched
     if args.tbe_role >= 0:
         tr.tbe_role = bool(args.tbe_role)
+    if args.sort_role >= 0:
+        tr.sort_role = bool(args.sort_role)
+    if args.sort_role_at >= 0:
+        tr.sort_role_at = args.sort_role_at
+    if args.bottom_parts >= 0:
+        tr.bottom_parts = args.bottom_parts
     if args.tbe_role_at:
         tr.tbe_role_at = tuple(int(v) for v in args.tbe_role_at.split(","))
     nb = 10  # the reference cycles 10 pre-generated batches (dlrm_data_pytorch.py:631)
@@ -849,7 +861,8 @@ def main():
                        "optimizer": c["optimizer"], "qr": c.get("qr"),
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
                        "hip_graph": use_graph, "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
-                       "tbe_role_at": list(tr.tbe_role_at),
+                       "tbe_role_at": list(tr.tbe_role_at), "bottom_parts": tr.bottom_parts,
+                       "sort_role": tr.sort_role, "sort_role_at": tr.sort_role_at,
                        "tune": args.tune or None},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,
             "comm": comm,

@@ -688,7 +688,8 @@ __global__ __launch_bounds__(WGM * WGN * 64, 4) void gemm_role_kernel(const Gemm
                                                                       const TbeBwdRole r) {
   __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
   const int b = blockIdx.x;
-  if (b < r.blocks) return tbe_role_run<PHASE>(r, b);
+  static_assert(sizeof(RoleSortLds) <= sizeof(smem), "the sort role's LDS fits the tile's");
+  if (b < r.blocks) return tbe_role_run<PHASE>(r, b, smem);
   group_body<BM, BN, WGM, WGN, 31>(g, b - r.blocks, smem);
 }
 
@@ -989,8 +990,10 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
       const dim3 grid(role->blocks + g.total), block(NT);
       if (phase == 1)
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 1>), grid, block, 0, st, g, *role);
-      else
+      else if (phase == 2)
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 2>), grid, block, 0, st, g, *role);
+      else
+        hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 3>), grid, block, 0, st, g, *role);
       DLRM_LAUNCH_CHECK("dlrm_gemm_f32_group_role");
       return DLRM_OK;
     }
@@ -1198,7 +1201,9 @@ extern "C" int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* prob
     if (n == 0) return DLRM_OK;
     return dlrm_gemm_f32_group(n, probs, workspace, workspace_bytes, stream);
   }
-  DLRM_ARG(phase == 1 || phase == 2, "%s: phase must be 1 or 2", name);
+  DLRM_ARG(phase == 1 || phase == 2 || phase == 3, "%s: phase must be 1, 2 or 3", name);
+  DLRM_ARG((phase == 3) == (r->T > 0), "%s: phase 3 takes a sort role (dlrm_tbe_sort_defer), "
+           "1 / 2 an update role", name);
   DLRM_ARG(n >= 0 && n <= kMaxGroup && (n == 0 || probs), "%s: 0..%d problems", name, kMaxGroup);
   Desc d[kMaxGroup];
   for (int i = 0; i < n; ++i) d[i] = desc_of(probs[i]);

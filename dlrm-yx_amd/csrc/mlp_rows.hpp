@@ -27,7 +27,7 @@ constexpr int kMlpTiles = 2;      // 16-column tiles per wave: out_width <= 16 *
 static_assert(kMlpTiles == 2, "mlp_rows_body dispatches mlp_kloop<1..2>");
 constexpr int kMlpMaxK = 528;     // input width rounded to 16, LDS capacity
 constexpr int kMlpPitch = kMlpMaxK + 4;
-constexpr int kMlpLdsFloats = 2 * kMlpRows * kMlpPitch;
+constexpr int kMlpLdsFloats = 2 * kMlpRows * kMlpPitch + 4;  // + the split chain's flag
 
 using mlp_f32x4 = __attribute__((ext_vector_type(4))) float;
 
@@ -42,6 +42,9 @@ struct MlpChain {
   int64_t ldw[DLRM_MLP_MAX_LAYERS];
   float* Y[DLRM_MLP_MAX_LAYERS];
   int64_t ldy[DLRM_MLP_MAX_LAYERS];
+  int parts;     // workgroups per 16-row block (1, 2, 4)
+  int split;     // the layer whose column tiles the parts share
+  int* tickets;  // per row block (parts > 1, split < layers - 1)
 };
 
 // K loop of one layer for this wave's NTW column tiles: acc[j] += A(16 x kp) . W_tile^T.
@@ -56,15 +59,16 @@ constexpr int kMlpRing = 8;
 
 // TW (the backward's data gradient): B[k][col] = W[k][col] (W used transposed: the k of
 // the product is W's row), four dword loads per chunk instead of one float4.
+// Tiles tb + wave + j * kMlpWaves (j < NTW).
 template <int NTW, bool TW = false>
 __device__ __forceinline__ void mlp_kloop(mlp_f32x4 (&acc)[kMlpTiles], const float* in,
-                                          __amdgpu_buffer_rsrc_t rw, int wave, int n, int kp,
-                                          int64_t ldw, int nch, int l16, int kq) {
+                                          __amdgpu_buffer_rsrc_t rw, int tb, int wave, int n,
+                                          int kp, int64_t ldw, int nch, int l16, int kq) {
   constexpr int P = kMlpPitch, NW = kMlpWaves, R = kMlpRing;
   auto fetch = [&](int c, float4 (&bv)[NTW]) {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
-      const int col = (wave + j * NW) * 16 + l16, k = c * 16 + 4 * kq;
+      const int col = (tb + wave + j * NW) * 16 + l16, k = c * 16 + 4 * kq;
       if constexpr (TW) {
         float e[4];
 #pragma unroll
@@ -115,13 +119,22 @@ __device__ __forceinline__ void mlp_kloop(mlp_f32x4 (&acc)[kMlpTiles], const flo
   }
 }
 
+// Split chains (mc.parts > 1): workgroup blk is part q = blk % parts of row block
+// blk / parts.  Layers before mc.split run whole in every part (part 0 writes their Y);
+// layer mc.split covers this part's tiles [tb, te) only; if more layers follow, the
+// outputs are published write-through (sc1 stores, drained, then an agent-scope ticket -
+// the MI355X guide's cross-XCD form, as in gemm.hip's split-K) and the last part to
+// arrive reads the others' columns back (sc1 loads) and runs the remaining layers.
 __device__ __forceinline__ void mlp_rows_body(const MlpChain& mc, int64_t blk, float* lds) {
   constexpr int RB = kMlpRows, P = kMlpPitch, NW = kMlpWaves, MT = kMlpTiles;
   constexpr int NT = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar tile tests
   const int kq = lane >> 4, l16 = lane & 15;
-  const int64_t r0 = blk * RB;
+  const int parts = mc.parts > 1 ? mc.parts : 1;
+  const int64_t rblk = blk / parts;
+  const int q = (int)(blk - rblk * parts);
+  const int64_t r0 = rblk * RB;
   float* in = lds;
   float* nx = lds + RB * P;
   {  // layer 0 input: X rows, zero-padded to a multiple of 16 columns
@@ -143,31 +156,70 @@ __device__ __forceinline__ void mlp_rows_body(const MlpChain& mc, int64_t blk, f
     // raw buffer loads over exactly W's rows (mlp_kloop)
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
         (void*)W, (short)0, (int)(((int64_t)(n - 1) * ldw + kp) * 4), 0x00020000);
+    const bool split = parts > 1 && l == mc.split;
+    const bool publish = split && l + 1 < mc.layers;  // the last part continues
+    const int tb = split ? q * ntile / parts : 0, te = split ? (q + 1) * ntile / parts : ntile;
+    const int mt = te - tb;  // this part's tiles
     mlp_f32x4 acc[MT];
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[j] = mlp_f32x4{0.f, 0.f, 0.f, 0.f};
-    const int nt_w = ntile > wave ? (ntile - wave + NW - 1) / NW : 0;  // this wave's tiles
+    const int nt_w = mt > wave ? (mt - wave + NW - 1) / NW : 0;  // this wave's tiles
     // the tile count is a template argument of the K loop: no branch inside it, so the
     // compiler's vmcnt accounting keeps the prefetched chunks in flight
     switch (nt_w) {
-      case 1: mlp_kloop<1>(acc, in, rw, wave, n, kp, ldw, nch, l16, kq); break;
-      case 2: mlp_kloop<2>(acc, in, rw, wave, n, kp, ldw, nch, l16, kq); break;
+      case 1: mlp_kloop<1>(acc, in, rw, tb, wave, n, kp, ldw, nch, l16, kq); break;
+      case 2: mlp_kloop<2>(acc, in, rw, tb, wave, n, kp, ldw, nch, l16, kq); break;
       default: break;
     }
     // epilogue: ReLU; register r of a 16x16 accumulator = row 4*kq + r, column l16
     float* Y = mc.Y[l];
     const int64_t ldy = mc.ldy[l];
+    const bool write_y = q == 0 || l >= mc.split;  // replicated layers: part 0 writes
+    const int64_t nrow = mc.rows - r0 < RB ? mc.rows - r0 : RB;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Y + r0 * ldy), (short)0, (int)(publish ? nrow * ldy * 4 : 0), 0x00020000);
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
-      const int col = (wave + j * NW) * 16 + l16;
-      if (col < n) {
+      const int col = (tb + wave + j * NW) * 16 + l16;
+      if (wave + j * NW < mt && col < n) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 4 * kq + r;
           const float v = fmaxf(acc[j][r], 0.f);
           nx[row * P + col] = v;
-          if (r0 + row < mc.rows) Y[(r0 + row) * ldy + col] = v;
+          if (publish) {  // write-through (sc1): read back by the last part to arrive
+            if (row < nrow)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), ry,
+                                                    (int)((row * ldy + col) * 4), 0, 16);
+          } else if (write_y && r0 + row < mc.rows) {
+            Y[(r0 + row) * ldy + col] = v;
+          }
         }
+      }
+    }
+    if (publish) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(lds + 2 * RB * P);  // past both activation buffers
+      if (tid == 0) {
+        const int t = __hip_atomic_fetch_add(mc.tickets + rblk, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == parts - 1;
+        if (last) __hip_atomic_store(mc.tickets + rblk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *reinterpret_cast<volatile int*>(flag) = last;
+      }
+      __syncthreads();
+      if (!*reinterpret_cast<volatile int*>(flag)) return;
+      // the other parts' columns of this block's rows (sc1 loads; rows past the batch: 0)
+      const int c0 = tb * 16, c1 = te * 16 < n ? te * 16 : n, other = n - (c1 - c0);
+      for (int e = tid; e < RB * other; e += NT) {
+        const int row = e / other, k = e - row * other;
+        const int col = k < c0 ? k : k + (c1 - c0);
+        float v = 0.f;
+        if (row < nrow)
+          v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            ry, (int)((row * ldy + col) * 4), 0, 16));
+        nx[row * P + col] = v;
       }
     }
     if (l + 1 < mc.layers) {  // next input: bias column 1, zeros to the 16-column boundary
@@ -229,8 +281,8 @@ __device__ __forceinline__ void mlp_rows_bwd_body(const MlpChain& mc, const MlpG
     for (int j = 0; j < MT; ++j) acc[j] = mlp_f32x4{0.f, 0.f, 0.f, 0.f};
     const int nt_w = ntile > wave ? (ntile - wave + NW - 1) / NW : 0;
     switch (nt_w) {
-      case 1: mlp_kloop<1, true>(acc, in, rw, wave, ncols, kdim, ldw, nch, l16, kq); break;
-      case 2: mlp_kloop<2, true>(acc, in, rw, wave, ncols, kdim, ldw, nch, l16, kq); break;
+      case 1: mlp_kloop<1, true>(acc, in, rw, 0, wave, ncols, kdim, ldw, nch, l16, kq); break;
+      case 2: mlp_kloop<2, true>(acc, in, rw, 0, wave, ncols, kdim, ldw, nch, l16, kq); break;
       default: break;
     }
     // epilogue: ReLU' of layer l-1's output (its forward activation Y_{l-1})
@@ -290,7 +342,24 @@ inline int mlp_chain_prepare(const dlrm_mlp_chain* c, MlpChain& mc) {
     mc.Y[l] = c->Y[l];
     mc.ldy[l] = c->ldy[l];
   }
+  mc.parts = c->parts > 1 ? c->parts : 1;
+  mc.split = c->split_layer;
+  mc.tickets = c->tickets;
+  if (mc.parts > 1) {
+    if (mc.parts != 2 && mc.parts != 4) return 0;
+    if (mc.split < 0 || mc.split >= c->layers) return 0;
+    if ((c->out_width[mc.split] + 15) / 16 < mc.parts) return 0;  // a tile per part
+    if (mc.split + 1 < c->layers) {
+      if (!c->tickets) return 0;
+      if ((int64_t)kMlpRows * c->ldy[mc.split] * 4 >= 0x7ff00000LL) return 0;  // 32-bit offsets
+    }
+  }
   return 1;
+}
+
+// Workgroups of the forward chain: parts per 16-row block.
+inline int64_t mlp_chain_blocks(const MlpChain& mc) {
+  return ((mc.rows + kMlpRows - 1) / kMlpRows) * mc.parts;
 }
 
 }  // namespace

@@ -28,6 +28,7 @@
 
 #include "mlp_rows.hpp"
 #include "tbe_bwd_roles.hpp"
+#include "tbe_sort.hpp"
 #include "tbe_common.hpp"
 
 namespace {
@@ -97,191 +98,7 @@ inline int64_t keys_grid(int T, int B) {
 // DLRM_TBE_ERR_TABLE_CAP is raised in *err.
 constexpr int kSegThreads = 1024, kSegItems = 4;
 constexpr int kSegCap = kSegThreads * kSegItems;  // lookups per table
-constexpr int kSegWaves = kSegThreads / 64;
-constexpr int kDigitBits = 8;
-
-struct SegSortLds {
-  uint32_t key[kSegCap];
-  int32_t pos[kSegCap];
-  uint32_t cnt[(1 << kDigitBits) * (kSegWaves + 1)];  // per (digit, wave): count, then offset
-  uint32_t wsum[kSegWaves];
-  int32_t bag[kSegCap];  // bag of each local position
-};
-
-// Stable LSD radix sort of kSegCap (key, pos) pairs, 8-bit digits.  Items sit in a
-// wave-striped arrangement: item u of lane l in wave w is element w*512 + u*64 + l.  A
-// digit's rank inside a wave comes from ballots (lanes holding the same digit, those below
-// this lane) plus the wave's running count of that digit in LDS; one scan over the
-// (digit, wave) counts gives every element its destination.  Order inside a digit is
-// (wave, item, lane) = element order: stable.
-__device__ __forceinline__ void seg_radix_sort(uint32_t (&key)[kSegItems],
-                                               int32_t (&pos)[kSegItems], int bits,
-                                               SegSortLds& sm) {
-  constexpr int NB = 1 << kDigitBits;
-  constexpr int NC = NB * kSegWaves;
-  constexpr int CPT = NC / kSegThreads;  // counters per thread in the scan
-  constexpr int CS = kSegWaves + 1;      // counter row stride: digits of one wave's lanes
-                                         // land in distinct LDS banks
-  static_assert(kSegWaves % CPT == 0, "scan entries of one thread share a digit");
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, l = tid & 63;
-  const uint64_t below = (1ull << l) - 1;
-  for (int s = 0; s < bits; s += kDigitBits) {
-    for (int i = tid; i < NB * CS; i += kSegThreads) sm.cnt[i] = 0;
-    __syncthreads();
-    uint32_t rank[kSegItems];
-    uint32_t dig[kSegItems];
-#pragma unroll
-    for (int u = 0; u < kSegItems; ++u) {
-      const uint32_t d = (key[u] >> s) & (NB - 1);
-      uint64_t peers = ~0ull;
-#pragma unroll
-      for (int b = 0; b < kDigitBits; ++b) {
-        const uint64_t bal = __ballot((d >> b) & 1);
-        peers &= ((d >> b) & 1) ? bal : ~bal;
-      }
-      const uint32_t r = __popcll(peers & below);
-      const uint32_t c = __popcll(peers);
-      const uint32_t base = sm.cnt[d * CS + w];
-      rank[u] = base + r;
-      dig[u] = d;
-      if (r == c - 1) sm.cnt[d * CS + w] = base + c;  // last peer publishes
-    }
-    __syncthreads();
-    // exclusive scan of cnt in (digit, wave) order
-    uint32_t v[CPT];
-    uint32_t tsum = 0;
-    // logical entries tid*CPT .. +CPT-1 = digit jd, waves jw .. jw+CPT-1
-    const int jd = (tid * CPT) / kSegWaves, jw = (tid * CPT) % kSegWaves;
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      v[k] = sm.cnt[jd * CS + jw + k];
-      tsum += v[k];
-    }
-    uint32_t inc = tsum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (l >= o) inc += y;
-    }
-    if (l == 63) sm.wsum[w] = inc;
-    __syncthreads();
-    uint32_t run = inc - tsum;
-    // waves before this one: all wave totals read at once (independent LDS reads)
-#pragma unroll
-    for (int k = 0; k < kSegWaves; ++k) run += k < w ? sm.wsum[k] : 0u;
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      sm.cnt[jd * CS + jw + k] = run;
-      run += v[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kSegItems; ++u) {
-      const uint32_t dst = sm.cnt[dig[u] * CS + w] + rank[u];
-      sm.key[dst] = key[u];
-      sm.pos[dst] = pos[u];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kSegItems; ++u) {
-      const int e = w * (kSegItems * 64) + u * 64 + l;
-      key[u] = sm.key[e];
-      pos[u] = sm.pos[e];
-    }
-    __syncthreads();
-  }
-}
-
-template <typename IdxT, typename OffT>
-__device__ __forceinline__ void segsort_body(
-    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
-    int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
-    int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err, int t,
-    SegSortLds& sm) {
-  const int tid = threadIdx.x;
-  if (t == T) {  // lookups outside every bag
-    const int64_t a = (int64_t)off[0], e = (int64_t)off[(int64_t)T * B];
-    for (int64_t p = tid; p < N; p += blockDim.x) {
-      if (p >= a && p < e) continue;
-      keys_out[p] = sentinel;
-      pos_out[p] = (int32_t)p;
-      bag_of[p] = -1;
-    }
-    return;
-  }
-  const int64_t s0 = (int64_t)off[(int64_t)t * B];
-  const int64_t n64 = (int64_t)off[(int64_t)(t + 1) * B] - s0;  // <= kSegCap (contract)
-  const int64_t rb = row_base[t];
-  const int64_t nrows = row_base[t + 1] - rb;
-  if (n64 > kSegCap) {  // contract violated: skip the table, report
-    for (int b = tid; b < B; b += blockDim.x) {
-      const int64_t a = (int64_t)off[(int64_t)t * B + b], e = (int64_t)off[(int64_t)t * B + b + 1];
-      for (int64_t p = a; p < e; ++p) bag_of[p] = t * B + b;
-    }
-    for (int64_t i = tid; i < n64; i += blockDim.x) {
-      keys_out[s0 + i] = sentinel;
-      pos_out[s0 + i] = (int32_t)(s0 + i);
-    }
-    if (tid == 0 && err) atomicOr(err, DLRM_TBE_ERR_TABLE_CAP);
-    return;
-  }
-  const int n = (int)n64;
-  int bits = 1;
-  while (bits < 32 && ((int64_t)1 << bits) <= nrows) ++bits;  // keys in [0, nrows]
-  const uint32_t pad = bits >= 32 ? 0xffffffffu : (uint32_t)(((uint64_t)1 << bits) - 1);
-  const int w = tid >> 6, l = tid & 63;
-  // all global loads of the table are issued before the first one is consumed (one
-  // memory latency, not one per loop trip): the lookup rows, then the bag offsets
-  IdxT rv[kSegItems];
-#pragma unroll
-  for (int u = 0; u < kSegItems; ++u) {
-    const int i = w * (kSegItems * 64) + u * 64 + l;  // wave-striped element order
-    rv[u] = i < n ? idx[s0 + i] : (IdxT)0;
-  }
-  // bag of each local position, in LDS; written out below in SORTED order (bag_of[i] =
-  // bag of the i-th sorted lookup), which spares the block kernel a dependent load
-  const OffT* toff = off + (int64_t)t * B;
-  constexpr int kBU = 4;  // bags per thread per round, loads in flight
-  for (int b0 = 0; b0 < B; b0 += kBU * kSegThreads) {
-    int64_t ba[kBU], be[kBU];
-#pragma unroll
-    for (int k = 0; k < kBU; ++k) {
-      const int b = b0 + k * kSegThreads + tid;
-      ba[k] = b < B ? (int64_t)toff[b] : 0;
-      be[k] = b < B ? (int64_t)toff[b + 1] : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kBU; ++k) {
-      const int32_t bag = t * B + b0 + k * kSegThreads + tid;
-      for (int64_t p = ba[k]; p < be[k]; ++p) sm.bag[p - s0] = bag;
-    }
-  }
-  uint32_t key[kSegItems];
-  int32_t pos[kSegItems];
-#pragma unroll
-  for (int u = 0; u < kSegItems; ++u) {
-    const int i = w * (kSegItems * 64) + u * 64 + l;
-    key[u] = pad;
-    pos[u] = i;
-    if (i < n) {
-      const int64_t r = (int64_t)rv[u];
-      key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
-      if (key[u] == (uint32_t)nrows && err) atomicOr(err, DLRM_TBE_ERR_INDEX);
-    }
-  }
-  __syncthreads();  // bags complete
-  seg_radix_sort(key, pos, bits, sm);
-#pragma unroll
-  for (int u = 0; u < kSegItems; ++u) {
-    const int i = w * (kSegItems * 64) + u * 64 + l;
-    if (i < n) {
-      keys_out[s0 + i] = key[u] < (uint32_t)nrows ? (uint32_t)(rb + key[u]) : sentinel;
-      pos_out[s0 + i] = (int32_t)(s0 + pos[u]);
-      bag_of[s0 + i] = sm.bag[pos[u]];
-    }
-  }
-}
+using SegSortLds = SegLds<kSegThreads, kSegItems, false>;
 
 template <typename IdxT, typename OffT>
 __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
@@ -289,8 +106,9 @@ __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
     int T, int B, int64_t N, uint32_t sentinel, uint32_t* __restrict__ keys_out,
     int32_t* __restrict__ pos_out, int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
   __shared__ SegSortLds sm;
-  segsort_body<IdxT, OffT>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of,
-                                err, blockIdx.x, sm);
+  segsort_body<kSegThreads, kSegItems, false, IdxT, OffT>(idx, off, row_base, T, B, N, sentinel,
+                                                          keys_out, pos_out, bag_of, err,
+                                                          blockIdx.x, sm);
 }
 
 // The forward gather and the backward's per-table sort in ONE launch: the sort depends only
@@ -315,8 +133,9 @@ __global__ __launch_bounds__(kPreThreads) void tbe_fwd_presort_kernel(
   __shared__ __attribute__((aligned(16))) PresortLds sm;
   const int b = blockIdx.x;
   if (b <= T) {
-    segsort_body<IdxT, OffT>(idx, off, row_base, T, B, N, sentinel, keys_out, pos_out, bag_of,
-                             err, b, sm.sort);
+    segsort_body<kSegThreads, kSegItems, false, IdxT, OffT>(idx, off, row_base, T, B, N,
+                                                            sentinel, keys_out, pos_out, bag_of,
+                                                            err, b, sm.sort);
     return;
   }
   if (b < T + 1 + mlp_blocks) {
@@ -1045,6 +864,55 @@ extern "C" int dlrm_tbe_backward_defer(
                       stream, name);
 }
 
+extern "C" int dlrm_tbe_sort_defer(const int64_t* row_base, int32_t T, int32_t B,
+                                   const void* indices, int32_t index_bits, const void* offsets,
+                                   int32_t offset_bits, int64_t num_lookups, int64_t total_rows,
+                                   int64_t D, int64_t max_lookups_per_table, void* workspace,
+                                   size_t workspace_bytes, int32_t* error_flag,
+                                   dlrm_tbe_bwd_role* role, dlrm_stream_t stream) {
+  const char* name = "dlrm_tbe_sort_defer";
+  DLRM_ARG(role, "%s: null role", name);
+  auto* r = reinterpret_cast<TbeBwdRole*>(role);
+  *r = TbeBwdRole{};
+  r->magic = kRoleMagic;
+  const int64_t N = num_lookups;
+  const bool keys32 = (uint64_t)total_rows < 0xFFFFFFFFull;
+  if (!presort_applies(keys32 ? 4 : 8, max_lookups_per_table, N) || N == 0 ||
+      T * (int64_t)B >= INT32_MAX)
+    return DLRM_OK;  // no per-table sort: the backward sorts itself (presorted is ignored)
+  DLRM_ARG(row_base && offsets && indices && workspace, "%s: null pointer", name);
+  DLRM_ARG(T > 0 && B > 0 && D > 0 && total_rows > 0, "%s: bad sizes", name);
+  DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: index_bits must be 32|64", name);
+  DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: offset_bits must be 32|64", name);
+  BwdWs<uint32_t> w = carve_bwd_ws<uint32_t>(workspace, N, D, bit_width_u64((uint64_t)total_rows));
+  DLRM_REQUIRE(workspace_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
+               name, workspace_bytes, w.total);
+  if (max_lookups_per_table > kRoleSortCap || B >= (1 << (31 - kPosBits))) {
+    // tables too long for the 256-thread role: the 1024-thread sort, launched now
+    hipStream_t st = dlrm::as_stream(stream);
+#define SEG(I, O)                                                                              \
+  hipLaunchKernelGGL((tbe_bwd_segsort_kernel<I, O>), dim3(T + 1), dim3(kSegThreads), 0, st,    \
+                     static_cast<const I*>(indices), static_cast<const O*>(offsets), row_base, T, \
+                     B, N, (uint32_t)total_rows, reinterpret_cast<uint32_t*>(w.keys_out),       \
+                     w.pos_out, w.bag_of, error_flag)
+    if (index_bits == 32 && offset_bits == 32) SEG(int32_t, int32_t);
+    else if (index_bits == 32) SEG(int32_t, int64_t);
+    else if (offset_bits == 32) SEG(int64_t, int32_t);
+    else SEG(int64_t, int64_t);
+#undef SEG
+    DLRM_LAUNCH_CHECK(name);
+    return DLRM_OK;
+  }
+  r->idx = indices, r->off = offsets, r->row_base = row_base, r->err = error_flag;
+  r->T = T, r->B = B, r->N = N, r->ibits = index_bits, r->obits = offset_bits;
+  r->sentinel = (uint32_t)total_rows;
+  r->keys = reinterpret_cast<const uint32_t*>(w.keys_out);
+  r->pos = w.pos_out;
+  r->bag_of = w.bag_of;
+  r->blocks = (int32_t)(dlrm::ceil_div((int64_t)T + 1, (int64_t)8) * 8);
+  return DLRM_OK;
+}
+
 extern "C" int32_t dlrm_tbe_bwd_role_blocks(const dlrm_tbe_bwd_role* role) {
   const auto* r = reinterpret_cast<const TbeBwdRole*>(role);
   return r && r->magic == kRoleMagic ? r->blocks : 0;
@@ -1125,7 +993,7 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
   int mlp_blocks = 0;
   if (bottom) {
     DLRM_ARG(mlp_chain_prepare(bottom, mc), "%s: unsupported bottom MLP chain", name);
-    mlp_blocks = (int)dlrm::ceil_div(bottom->rows, kMlpRows);
+    mlp_blocks = (int)mlp_chain_blocks(mc);
   }
   if (!presort_applies((uint64_t)total_rows < 0xFFFFFFFFull ? 4 : 8, max_lookups_per_table,
                        num_lookups) || num_lookups == 0 || T * (int64_t)B >= INT32_MAX) {
@@ -1190,7 +1058,7 @@ extern "C" int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t
   MlpChain mc{};
   DLRM_ARG(mlp_chain_prepare(chain, mc), "%s: unsupported chain", name);
   if (chain->rows == 0) return DLRM_OK;
-  hipLaunchKernelGGL(mlp_chain_kernel, dim3((unsigned)dlrm::ceil_div(chain->rows, kMlpRows)),
+  hipLaunchKernelGGL(mlp_chain_kernel, dim3((unsigned)mlp_chain_blocks(mc)),
                      dim3(kMlpWaves * 64), 0, dlrm::as_stream(stream), mc);
   DLRM_LAUNCH_CHECK(name);
   return DLRM_OK;

@@ -5,6 +5,7 @@
 #include <type_traits>
 
 #include "tbe_common.hpp"
+#include "tbe_sort.hpp"
 
 namespace {
 
@@ -502,6 +503,12 @@ struct TbeBwdRole {
   uint32_t sentinel, magic;
   int32_t B, ch, mode, lpb;
   int32_t blocks;  // workgroups of either pass; 0 = nothing deferred
+  // phase 3, the per-table sort (dlrm_tbe_sort_defer): writes keys / pos / bag_of
+  const void* idx;
+  const void* off;
+  const int64_t* row_base;
+  int32_t* err;
+  int32_t T, ibits, obits;
 };
 
 inline bool tbe_role_fusable(int mode, int lpb, const float* psw, int64_t grad_extent) {
@@ -529,8 +536,30 @@ __device__ __forceinline__ void tbe_role_lpb(const TbeBwdRole& r, int blk) {
     tbe_role_pass<PHASE, LPB, MODE_ADAGRAD>(r, blk);
 }
 
+// Phase 3: the per-table sort, 256 threads x 8 items (tables of <= 2048 lookups), bags
+// packed into the positions; the LDS image goes in the co-launched kernel's smem.
+constexpr int kRoleSortThreads = 256, kRoleSortItems = 8;
+using RoleSortLds = SegLds<kRoleSortThreads, kRoleSortItems, true>;
+constexpr int kRoleSortCap = kRoleSortThreads * kRoleSortItems;
+
+template <typename IdxT, typename OffT>
+__device__ __forceinline__ void tbe_role_sort(const TbeBwdRole& r, int blk, void* lds) {
+  if (blk > r.T) return;  // blocks are rounded up to a multiple of 8
+  segsort_body<kRoleSortThreads, kRoleSortItems, true, IdxT, OffT>(
+      static_cast<const IdxT*>(r.idx), static_cast<const OffT*>(r.off), r.row_base, r.T, r.B, r.N,
+      r.sentinel, const_cast<uint32_t*>(r.keys), const_cast<int32_t*>(r.pos),
+      const_cast<int32_t*>(r.bag_of), r.err, blk, *static_cast<RoleSortLds*>(lds));
+}
+
 template <int PHASE>
-__device__ __forceinline__ void tbe_role_run(const TbeBwdRole& r, int blk) {
+__device__ __forceinline__ void tbe_role_run(const TbeBwdRole& r, int blk, void* lds) {
+  if constexpr (PHASE == 3) {
+    if (r.ibits == 32 && r.obits == 32) tbe_role_sort<int32_t, int32_t>(r, blk, lds);
+    else if (r.ibits == 32) tbe_role_sort<int32_t, int64_t>(r, blk, lds);
+    else if (r.obits == 32) tbe_role_sort<int64_t, int32_t>(r, blk, lds);
+    else tbe_role_sort<int64_t, int64_t>(r, blk, lds);
+    return;
+  }
   switch (r.lpb) {
     case 4: tbe_role_lpb<PHASE, 4>(r, blk); break;
     case 8: tbe_role_lpb<PHASE, 8>(r, blk); break;

@@ -44,13 +44,14 @@ class MlpChain(ctypes.Structure):
     _fields_ = [("layers", c_int32), ("rows", c_int64), ("X", c_void_p), ("ldx", c_int64),
                 ("in_width", c_int64 * MLP_MAX_LAYERS), ("out_width", c_int64 * MLP_MAX_LAYERS),
                 ("W", c_void_p * MLP_MAX_LAYERS), ("ldw", c_int64 * MLP_MAX_LAYERS),
-                ("Y", c_void_p * MLP_MAX_LAYERS), ("ldy", c_int64 * MLP_MAX_LAYERS)]
+                ("Y", c_void_p * MLP_MAX_LAYERS), ("ldy", c_int64 * MLP_MAX_LAYERS),
+                ("parts", c_int32), ("split_layer", c_int32), ("tickets", c_void_p)]
 
 
 # name -> (restype, argtypes); mirrors include/dlrm_hip.h exactly.
 class TbeBwdRole(ctypes.Structure):
     """struct dlrm_tbe_bwd_role (include/dlrm_hip.h): a deferred embedding update."""
-    _fields_ = [("opaque", ctypes.c_uint64 * 20)]
+    _fields_ = [("opaque", ctypes.c_uint64 * 24)]
 
 
 P = c_void_p
@@ -118,6 +119,8 @@ SIGNATURES = {
                                           c_int64, c_float, c_float, c_int64, P, c_size_t, P,
                                           c_int32, P, P]),
     "dlrm_tbe_bwd_role_blocks": (c_int32, [P]),
+    "dlrm_tbe_sort_defer": (c_int32, [P, c_int32, c_int32, P, c_int32, P, c_int32, c_int64,
+                                      c_int64, c_int64, c_int64, P, c_size_t, P, P, P]),
     "dlrm_gemm_f32_splits": (c_int32, [P]),
     "dlrm_gemm_f32_partial_bytes": (c_size_t, [c_int64, c_int64, c_int32]),
     "dlrm_colsum_workspace_size": (c_size_t, [c_int64, c_int64]),

@@ -177,10 +177,21 @@ def tbe_forward(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
     return out
 
 
-def mlp_chain(X: torch.Tensor, layers) -> "_lib.MlpChain":
+def mlp_chain(X: torch.Tensor, layers, parts: int = 1, split_layer: int = -1,
+              tickets: Optional[torch.Tensor] = None) -> "_lib.MlpChain":
     """dlrm_mlp_chain for a bias-folded Linear+ReLU stack: ``X`` [rows, >= in_width[0]]
-    carries its own bias column; ``layers`` = [(W [n, >= kin], Y [rows, >= n], kin)]."""
+    carries its own bias column; ``layers`` = [(W [n, >= kin], Y [rows, >= n], kin)].
+    ``parts`` 2 / 4: that many workgroups per 16-row block, splitting layer ``split_layer``
+    (default: the largest in_width * out_width) by output columns; ``tickets``: zeroed int32
+    [ceil(rows / 16)] device buffer owned by this chain (allocated when None)."""
     c = _lib.MlpChain()
+    if parts > 1:
+        if split_layer < 0:
+            split_layer = max(range(len(layers)), key=lambda i: layers[i][2] * layers[i][0].shape[0])
+        if tickets is None:
+            tickets = torch.zeros((X.shape[0] + 15) // 16, dtype=torch.int32, device=X.device)
+        c.parts, c.split_layer, c.tickets = int(parts), int(split_layer), tickets.data_ptr()
+        c._keep = tickets  # the chain struct refers to it
     c.layers = len(layers)
     c.rows = X.shape[0]
     c.X = X.data_ptr()
@@ -400,6 +411,21 @@ def tbe_backward_defer(mode: str, weights: torch.Tensor, row_base: torch.Tensor,
               total_rows, _p(per_sample_weights), _p(grad_out), grad_batch_stride, lr, eps,
               int(max_lookups_per_table), _p(workspace), workspace.numel(), _p(error_flag),
               int(presorted), ctypes.byref(role), _stream(weights.device))
+    return role if tbe_role_blocks(role) > 0 else None
+
+
+def tbe_sort_defer(row_base: torch.Tensor, T: int, B: int, indices: torch.Tensor,
+                   offsets: torch.Tensor, total_rows: int, D: int, workspace: torch.Tensor,
+                   max_lookups_per_table: int, error_flag: Optional[torch.Tensor] = None):
+    """This batch's per-table sort as pass 3 of a later gemm_group(..., role=, phase=3)
+    (dlrm_tbe_sort_defer); the backward then runs with presorted=True.  None: nothing to
+    carry (the sort already ran, or the backward sorts itself)."""
+    _check_cuda(row_base, indices, offsets, workspace, error_flag)
+    role = _lib.TbeBwdRole()
+    _lib.call("dlrm_tbe_sort_defer", _p(row_base), T, B, _p(indices), _bits(indices),
+              _p(offsets), _bits(offsets), indices.numel(), int(total_rows), int(D),
+              int(max_lookups_per_table), _p(workspace), workspace.numel(), _p(error_flag),
+              ctypes.byref(role), _stream(indices.device))
     return role if tbe_role_blocks(role) > 0 else None
 
 

@@ -233,6 +233,17 @@ class DLRMTrainer:
         # one GPU: the embedding update's passes as extra workgroups of the bottom-MLP
         # backward's GEMM launches (dlrm_gemm_f32_group_role); False: launches of their own
         self.tbe_role = True
+        # one GPU, gather-fused batches: the per-table sort as a role of a top-MLP forward
+        # GEMM launch instead of the lookup launch (dlrm_tbe_sort_defer; the bottom MLP then
+        # gets the whole chip).  Off: measured slower at C3, C2 and B = 256 - the sort's
+        # workgroups stretch the GEMM launch that carries them by more than the lookup
+        # launch saves (profiles/r04_sort_role_ab.txt)
+        self.sort_role = False
+        self.sort_role_at = 0  # which top-MLP forward GEMM launch carries it
+        # bottom-MLP forward workgroups per 16-row block in the lookup launch (0 = auto)
+        self.bottom_parts = 0
+        self._cus = torch.cuda.get_device_properties(self.dev).multi_processor_count \
+            if torch.cuda.is_available() else 256
         self.tbe_role_at = (0, 1)  # bottom-backward launches carrying pass 1 and pass 2
         self._roles = []  # pending (role, phase) passes for the next _gemm launches
         self.gather_fused = False  # set by the last step
@@ -629,8 +640,26 @@ class DLRMTrainer:
                     h = out
 
         def fwd_single():  # one GPU: bottom MLP || lookup
-            chain = self._bottom_chain(batch, bufs) if presort and not c_fwd else None
+            # gather-fused one-hot batches: the per-table sort leaves the lookup launch for
+            # the first top-MLP GEMM launch (dlrm_tbe_sort_defer), so the bottom MLP has the
+            # whole chip (more workgroups per row block)
+            # (per-group timing passes, profile != None, keep every role in its own launch)
+            sort_role = gather and self.sort_role and not c_fwd and profile is None
+            chain = self._bottom_chain(batch, bufs, sort_wgs=0 if sort_role else None) \
+                if presort and not c_fwd else None
             self.bottom_fused = chain is not None
+            if chain is not None and sort_role:
+                with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
+                        record_function("module::forward_pass::bottom_mlp"), prof("tbe_fwd"):
+                    idx, off = st["csr"] = self._phys_csr(batch, B)
+                    ops.mlp_chain_forward(chain, self.dev)
+                    role = ops.tbe_sort_defer(self.row_base, self.T_phys, B, idx, off,
+                                              self.weights.shape[0], D,
+                                              self._ws_tbe(idx.numel()), batch.max_per_table,
+                                              error_flag=self.tbe_error_flag)
+                    if role is not None:  # rides on top-MLP forward launch sort_role_at
+                        self._roles = [None] * self.sort_role_at + [(role, 3)]
+                return
             if chain is not None:
                 # the bottom MLP forward runs as a role of the lookup launch
                 with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
@@ -816,7 +845,12 @@ class DLRMTrainer:
             # the embedding update's two HBM-bound passes ride as extra workgroups on the
             # first two (MFMA-bound) bottom-backward launches: overlap with no cross-queue
             # dependency (dlrm_tbe_backward_defer / dlrm_gemm_f32_group_role)
-            deferred = (self.tbe_role and not c_bot and self.T_local > 0
+            while self._roles:  # a deferred sort no forward launch carried
+                if self._roles[0] is None:
+                    self._roles.pop(0)
+                else:
+                    self._gemm([])
+            deferred = (self.tbe_role and not c_bot and self.T_local > 0 and profile is None
                         and self.weights.dtype == torch.float32)
             if deferred:
                 role = emb_bwd(defer=True)
@@ -1027,13 +1061,36 @@ class DLRMTrainer:
             self._colsum(hin[:, :last.Kp], scale=dz, out=last.gW[0],
                          workspace=self._ws_colsum(Bl, last.Kp))
 
-    def _bottom_chain(self, batch: Batch, bufs, backward: bool = False):
+    def _bottom_chain(self, batch: Batch, bufs, backward: bool = False,
+                      sort_wgs: Optional[int] = None):
         """The bottom MLP as a dlrm_mlp_chain (None when unsupported; for the forward also
         when disabled or when there are no local tables to share the lookup launch with)."""
         if not backward and (not self.fuse_bottom or self.T_local == 0):
             return None
-        chain = ops.mlp_chain(batch.X, [(L.W, out, L.Kp)
-                                        for L, out in zip(self.bot, bufs["bot_act"])])
+        layers = [(L.W, out, L.Kp) for L, out in zip(self.bot, bufs["bot_act"])]
+        parts = 1
+        if not backward:
+            # several workgroups per 16-row block while the lookup launch still fits the
+            # chip in one wave (its T_local + 1 sort workgroups beside them): small batches
+            # then run the bottom MLP on 2-4x the CUs (mlp_rows.hpp, split chains)
+            nrb = (batch.X.shape[0] + 15) // 16
+            parts = self.bottom_parts
+            others = self.T_local + 1 if sort_wgs is None else sort_wgs
+            if parts <= 0:
+                parts = next((p for p in (4, 2) if nrb * p + others <= self._cus), 1)
+            widest = max(range(len(layers)), key=lambda i: layers[i][2] * layers[i][0].shape[0])
+            if (layers[widest][0].shape[0] + 15) // 16 < parts:
+                parts = 1
+            if parts > 1:
+                tk = bufs.get("mlp_tickets")
+                if tk is None or tk.numel() < nrb:
+                    tk = bufs["mlp_tickets"] = torch.zeros(nrb, dtype=torch.int32,
+                                                           device=self.dev)
+                chain = ops.mlp_chain(batch.X, layers, parts=parts, split_layer=widest,
+                                      tickets=tk)
+                if ops.mlp_chain_supported(chain):
+                    return chain
+        chain = ops.mlp_chain(batch.X, layers)
         return chain if ops.mlp_chain_supported(chain) else None
 
     def _ws_tbe(self, n: int) -> torch.Tensor:

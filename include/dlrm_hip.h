@@ -101,7 +101,9 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  *    at `partial`; dlrm_tbe_forward_presort's out = NULL (sort-only) mode is used by the
  *    engine (round 4).
  * 6: dlrm_tbe_backward_defer + dlrm_gemm_f32_group_role: the embedding backward's update
- *    passes as extra workgroups of grouped GEMM launches (round 4). */
+ *    passes (and dlrm_tbe_sort_defer: the per-table sort) as extra workgroups of grouped
+ *    GEMM launches; dlrm_mlp_chain gains parts /
+ *    split_layer / tickets (several workgroups per 16-row block) (round 4). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 
@@ -151,6 +153,15 @@ int dlrm_tbe_forward(const float* weights, int64_t D, const int64_t* row_base, i
  * pad4(out_width[l-1] + 1).  Only columns < out_width[l] of Y_l are written.  Supported
  * (dlrm_mlp_chain_supported): 1..4 layers, out_width <= 512, in_width rounded up to 16
  * <= 528, X and W 16-byte aligned with row strides % 4 == 0.
+ * parts (ABI v6; 0 or 1 = off): 2 or 4 workgroups share each 16-row block.  Layer
+ * split_layer's 16-column tiles are dealt out between them (each needs >= 1 tile), the
+ * layers before it are computed by every part (only part 0 writes their Y), and when
+ * split_layer is not the last layer the part that finishes its columns last - an
+ * agent-scope ticket in tickets[block], int32 [ceil(rows / 16)], zero before the first call
+ * and left zero by every call - reads the other parts' columns of Y_split (published
+ * write-through) and runs the remaining layers.  Same result as parts = 1, bit for bit:
+ * every output element is the same dot product in the same order.  Tickets are per chain:
+ * two launches in flight at once must not share them.
  */
 #define DLRM_MLP_MAX_LAYERS 4
 typedef struct dlrm_mlp_chain {
@@ -164,6 +175,9 @@ typedef struct dlrm_mlp_chain {
   int64_t ldw[DLRM_MLP_MAX_LAYERS];
   float* Y[DLRM_MLP_MAX_LAYERS];
   int64_t ldy[DLRM_MLP_MAX_LAYERS];
+  int32_t parts;       /* ABI v6 */
+  int32_t split_layer; /* ABI v6 */
+  int32_t* tickets;    /* ABI v6 */
 } dlrm_mlp_chain;
 
 /* 1 when dlrm_mlp_chain_forward / the fused forward can take this chain, else 0. */
@@ -342,7 +356,7 @@ int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_b
  * weights, momentum and grad_out must stay as they are.
  */
 typedef struct dlrm_tbe_bwd_role {
-  uint64_t opaque[20];
+  uint64_t opaque[24];
 } dlrm_tbe_bwd_role;
 int dlrm_tbe_backward_defer(int32_t mode, float* weights, float* momentum, int64_t D,
                             const int64_t* row_base, int32_t T, int32_t B,
@@ -355,6 +369,22 @@ int dlrm_tbe_backward_defer(int32_t mode, float* weights, float* momentum, int64
                             dlrm_tbe_bwd_role* role, dlrm_stream_t stream);
 /* Workgroups a deferred pass adds to the launch that carries it (0: nothing deferred). */
 int32_t dlrm_tbe_bwd_role_blocks(const dlrm_tbe_bwd_role* role);
+/*
+ * This batch's per-table sort (what dlrm_tbe_forward_presort's sort role does), deferred
+ * into a later grouped GEMM launch: *role becomes pass 3 for dlrm_gemm_f32_group_role,
+ * which must run before the backward (then called with presorted = 1, same indices,
+ * offsets and workspace).  Tables of <= 2048 lookups sort in 256-thread workgroups
+ * (LDS-light: the launch's GEMM tiles keep their occupancy); with a per-table bound in
+ * 2049..4096 the 1024-thread sort is launched here instead, and with none (or 64-bit row
+ * keys) nothing happens and the backward sorts itself - role->blocks == 0 in both cases.
+ * D: the embedding width (the workspace layout).  Bitwise the same sorted output as every
+ * other sort path.
+ */
+int dlrm_tbe_sort_defer(const int64_t* row_base, int32_t T, int32_t B, const void* indices,
+                        int32_t index_bits, const void* offsets, int32_t offset_bits,
+                        int64_t num_lookups, int64_t total_rows, int64_t D,
+                        int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes,
+                        int32_t* error_flag, dlrm_tbe_bwd_role* role, dlrm_stream_t stream);
 
 /*
  * Sparse-gradient values of an EmbeddingBag(sparse=True) backward
@@ -550,8 +580,8 @@ size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits);
 int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
                         size_t workspace_bytes, dlrm_stream_t stream);
 /* dlrm_gemm_f32_group plus pass `phase` (1 or 2) of a deferred embedding update
- * (dlrm_tbe_backward_defer) as extra workgroups of the same launch; n may be 0 (the pass
- * alone).  role == NULL, or a role with nothing deferred: dlrm_gemm_f32_group.  The
+ * (dlrm_tbe_backward_defer), or the deferred sort (phase 3, dlrm_tbe_sort_defer), as extra
+ * workgroups of the same launch; n may be 0 (the pass alone).  role == NULL, or a role with nothing deferred: dlrm_gemm_f32_group.  The
  * problems must not touch the update's buffers (weights, momentum, grad_out, workspace). */
 int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
                              size_t workspace_bytes, const dlrm_tbe_bwd_role* role,

@@ -696,3 +696,66 @@ def test_tbe_update_roles_match_own_launches(name, sched, optimizer, at, graph):
                     tr._bufs[(B, B)]["prob"].cpu().clone()))
     for a, b in zip(*res):
         assert (a is None and b is None) or torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name,B", [("c2_small", 128), ("c3_small", 256)])
+def test_bottom_parts_split_chain_matches_single(name, B):
+    """The fused bottom MLP with 2 / 4 workgroups per 16-row block (auto at these batch
+    sizes) vs one: 3 steps leave bitwise the same state (same dot products, same order)."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function=c["loss"],
+                        learning_rate=c["lr"])
+    res = []
+    for parts in (1, 2, 4):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.bottom_parts = parts
+        for s in range(3):
+            tr.step(tr.synthetic_batch(B, 1, seed=s))
+        torch.cuda.synchronize()
+        assert tr.bottom_fused
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
+                    tr._bufs[(B, B)]["prob"].cpu().clone()))
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name,B", [("c3_small", 512), ("c2_small", 128)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_sort_role_matches_lookup_launch_sort(name, B, graph):
+    """The per-table sort as a role of the first top-MLP GEMM launch (sort_role, with the
+    bottom MLP then split over more workgroups) vs inside the lookup launch: 3 steps leave
+    bitwise the same state, eager and replayed from a captured graph."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function=c["loss"],
+                        learning_rate=c["lr"])
+    res = []
+    for role in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.sort_role = role
+        batches = [tr.synthetic_batch(B, 1, seed=s) for s in range(3)]
+        if graph:
+            tr.step(batches[0])
+            run = tr.capture(batches[0])
+            for b in batches[1:]:
+                for src, dst in zip((b.X, b.offsets, b.indices, b.target),
+                                    (batches[0].X, batches[0].offsets, batches[0].indices,
+                                     batches[0].target)):
+                    dst.copy_(src)
+                run()
+        else:
+            for b in batches:
+                tr.step(b)
+        torch.cuda.synchronize()
+        tr.check_errors()
+        assert tr.gather_fused and not tr._roles
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
+                    tr._bufs[(B, B)]["prob"].cpu().clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

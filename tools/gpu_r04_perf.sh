@@ -57,6 +57,27 @@ roleat)  # placement of the two passes: AT="0,1 0,2 ..."
     done
   done
   ;;
+parts)  # fused bottom MLP: one workgroup per 16-row block vs the auto split
+  for cfg in ${CFGS:-kaggle b256}; do
+    for pp in 1 0; do
+      if [ "$cfg" = b256 ]; then a="--batch 256"; else a="--config $cfg"; fi
+      $B $a --bottom-parts $pp --steps 300 --warmup 30 > "$OUT/parts_${cfg}_$pp.json" \
+        2> "$OUT/parts_${cfg}_$pp.err" || exit $?
+      python -c "import json;d=json.load(open('$OUT/parts_${cfg}_$pp.json'));print('$cfg parts=$pp',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+    done
+  done
+  ;;
+sortab)  # the per-table sort: lookup launch vs a top-MLP forward launch (VARIANTS)
+  for cfg in ${CFGS:-terabyte kaggle b256}; do
+    for v in ${VARIANTS:-"--sort-role 0" "--sort-role 1 --sort-role-at 0" "--sort-role 1 --sort-role-at 1"}; do
+      if [ "$cfg" = b256 ]; then a="--batch 256"; else a="--config $cfg"; fi
+      tag=$(echo "$v" | tr -d ' -')
+      $B $a $v --steps 300 --warmup 30 > "$OUT/sort_${cfg}_$tag.json" \
+        2> "$OUT/sort_${cfg}_$tag.err" || exit $?
+      python -c "import json;d=json.load(open('$OUT/sort_${cfg}_$tag.json'));print('$cfg $v',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+    done
+  done
+  ;;
 trace)
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c3 ${BOT:+--bot-sched $BOT} || exit $?
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c2 --config kaggle ${BOT:+--bot-sched $BOT} || exit $?

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel timeline of one training step from a rocprofv3 kernel trace (kt_kernel_trace.csv):
-finds the last run of consecutive dispatches between two tbe_fwd launches (one hipGraph replay),
+finds the last run of consecutive dispatches between two step-opening launches - the lookup
+launch (tbe_fwd*) or, with the sort deferred, the bottom-MLP chain (mlp_chain_kernel) - i.e.
+one hipGraph replay,
 prints each kernel with its grid, duration and the idle gap before it."""
 import csv
 import re
@@ -16,7 +18,8 @@ def short(name):
 def main(path, which=-2):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "tbe_fwd" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(rows)
+              if "tbe_fwd" in r["Kernel_Name"] or re.search(r"\bmlp_chain_kernel\b", r["Kernel_Name"])]
     a, b = starts[which - 1], starts[which]
     step = rows[a:b]
     t0 = int(step[0]["Start_Timestamp"])
