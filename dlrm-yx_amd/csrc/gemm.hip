@@ -685,7 +685,7 @@ __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
 // twice that, and the GEMM tiles would run at half their occupancy).
 template <int BM, int BN, int WGM, int WGN, int PHASE>
 __global__ __launch_bounds__(WGM * WGN * 64, 4) void gemm_role_kernel(const GemmGroup g,
-                                                                      const TbeBwdRole r) {
+                                                                      const LaunchRole r) {
   __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
   const int b = blockIdx.x;
   static_assert(sizeof(RoleSortLds) <= sizeof(smem), "the sort role's LDS fits the tile's");
@@ -940,7 +940,7 @@ size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
 
 template <int BM, int BN, int WGM = 2, int WGN = 2>
 int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes,
-                 const TbeBwdRole* role, int phase, hipStream_t st) {
+                 const LaunchRole* role, int phase, hipStream_t st) {
   constexpr int NT = WGM * WGN * 64;
   GemmGroup g{};
   g.n = n;
@@ -992,8 +992,10 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 1>), grid, block, 0, st, g, *role);
       else if (phase == 2)
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 2>), grid, block, 0, st, g, *role);
-      else
+      else if (phase == 3)
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 3>), grid, block, 0, st, g, *role);
+      else
+        hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 4>), grid, block, 0, st, g, *role);
       DLRM_LAUNCH_CHECK("dlrm_gemm_f32_group_role");
       return DLRM_OK;
     }
@@ -1098,7 +1100,7 @@ size_t ws_for(int n, const Desc* d) {
 }
 
 int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st,
-        const TbeBwdRole* role = nullptr, int phase = 0) {
+        const LaunchRole* role = nullptr, int phase = 0) {
   DLRM_ARG(n >= (role ? 0 : 1) && n <= kMaxGroup, "dlrm_gemm_f32_group: 1..%d problems",
            kMaxGroup);
   Desc q[kMaxGroup];
@@ -1192,18 +1194,19 @@ extern "C" int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* probs, vo
 
 extern "C" int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* probs,
                                         void* workspace, size_t workspace_bytes,
-                                        const dlrm_tbe_bwd_role* role, int32_t phase,
+                                        const dlrm_launch_role* role, int32_t phase,
                                         dlrm_stream_t stream) {
   const char* name = "dlrm_gemm_f32_group_role";
-  const auto* r = reinterpret_cast<const TbeBwdRole*>(role);
+  const auto* r = reinterpret_cast<const LaunchRole*>(role);
   DLRM_ARG(!r || r->magic == kRoleMagic, "%s: role not filled by dlrm_tbe_backward_defer", name);
   if (!r || r->blocks == 0) {
     if (n == 0) return DLRM_OK;
     return dlrm_gemm_f32_group(n, probs, workspace, workspace_bytes, stream);
   }
-  DLRM_ARG(phase == 1 || phase == 2 || phase == 3, "%s: phase must be 1, 2 or 3", name);
-  DLRM_ARG((phase == 3) == (r->T > 0), "%s: phase 3 takes a sort role (dlrm_tbe_sort_defer), "
-           "1 / 2 an update role", name);
+  DLRM_ARG(phase >= 1 && phase <= 4, "%s: phase must be 1..4", name);
+  DLRM_ARG(role_kind_of_phase(phase) == r->kind,
+           "%s: phase %d does not match the role (1 / 2: dlrm_tbe_backward_defer, 3: "
+           "dlrm_tbe_sort_defer, 4: dlrm_head_step_defer)", name, (int)phase);
   DLRM_ARG(n >= 0 && n <= kMaxGroup && (n == 0 || probs), "%s: 0..%d problems", name, kMaxGroup);
   Desc d[kMaxGroup];
   for (int i = 0; i < n; ++i) d[i] = desc_of(probs[i]);

@@ -9,6 +9,8 @@
 //  * dlrm_sgd_update / dlrm_adagrad_update: torch.optim.SGD dense step and the dense
 //    branch of RWSAdagrad (optim/rwsadagrad.py:117-120) on a flat parameter bucket.
 #include "common.hpp"
+#include "head_roles.hpp"
+#include "tbe_bwd_roles.hpp"
 
 namespace {
 
@@ -45,12 +47,6 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(int64_t N, int64_t MS
   for (int64_t ms = 0; ms < MS; ++ms) s += part[ms * N + n];
   if (out) out[n] = accumulate ? out[n] + alpha * s : alpha * s;
   if (sgd_param) sgd_param[n] = fmaf(-lr, s, sgd_param[n]);
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
 }
 
 __global__ __launch_bounds__(256) void head_rows_kernel(int64_t M, int64_t K,
@@ -197,35 +193,16 @@ __global__ __launch_bounds__(256) void head_fused_rows_kernel(
 }
 
 // Column sums of the row-block partials -> weight gradient (stored, accumulated, or
-// applied as SGD to w); one wave per column: lane l sums blocks l, l+64, ... in order,
-// then a fixed xor-tree across lanes (deterministic).  The last workgroup also reduces the
-// per-row loss terms the same way.
+// applied as SGD to w) and the mean loss: head_roles.hpp.
 __global__ __launch_bounds__(256) void head_finalize_kernel(int64_t M, int64_t K, int64_t nblk,
                                                             const float* __restrict__ part,
                                                             float* __restrict__ w, float lr,
                                                             float* __restrict__ dw, int accumulate,
                                                             const float* __restrict__ row_loss,
                                                             float* __restrict__ loss_out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (k < K) {
-    float s = 0.f;
-    for (int64_t b = lane; b < nblk; b += 64) s += part[b * K + k];
-    s = wave_sum(s);
-    if (lane == 0) {
-      if (dw) dw[k] = accumulate ? dw[k] + s : s;
-      else if (lr != 0.f) w[k] = fmaf(-lr, s, w[k]);
-    }
-  }
-  if (blockIdx.x == gridDim.x - 1 && loss_out) {
-    __shared__ float red[4];
-    float s = 0.f;
-    for (int64_t i = threadIdx.x; i < M; i += 256) s += row_loss[i];
-    s = wave_sum(s);
-    if (lane == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) loss_out[0] = ((red[0] + red[1]) + red[2] + red[3]) / (float)M;
-  }
+  __shared__ float red[4];
+  head_finalize_body(M, K, nblk, part, w, lr, dw, accumulate, row_loss, loss_out, blockIdx.x,
+                     gridDim.x, red);
 }
 
 __global__ __launch_bounds__(256) void mean_kernel(int64_t M, const float* __restrict__ v,
@@ -527,13 +504,13 @@ extern "C" size_t dlrm_head_step_workspace_size(int64_t M, int64_t K) {
          (size_t)nblk * (K > 0 ? K : 1) * sizeof(float) + 256;
 }
 
-extern "C" int dlrm_head_step(int64_t M, int64_t K, const float* X, int64_t ldx, float* w,
-                              const float* target, int32_t loss_kind, float clamp_lo,
-                              float grad_scale, float* prob_out, float* dz_out, float* loss_out,
-                              float* dX, int64_t lddx, int32_t relu_mask, float* dw_out,
-                              int32_t accumulate, float lr, void* workspace,
-                              size_t workspace_bytes, dlrm_stream_t stream) {
-  const char* name = "dlrm_head_step";
+namespace {
+
+int head_step(int64_t M, int64_t K, const float* X, int64_t ldx, float* w, const float* target,
+              int32_t loss_kind, float clamp_lo, float grad_scale, float* prob_out,
+              float* dz_out, float* loss_out, float* dX, int64_t lddx, int32_t relu_mask,
+              float* dw_out, int32_t accumulate, float lr, void* workspace,
+              size_t workspace_bytes, LaunchRole* defer, dlrm_stream_t stream, const char* name) {
   DLRM_ARG(M > 0 && K > 0, "%s: bad sizes", name);
   DLRM_ARG(X && w && ldx >= K && target, "%s: null X/w/target", name);
   DLRM_ARG(loss_kind == DLRM_LOSS_MSE || loss_kind == DLRM_LOSS_BCE, "%s: bad loss", name);
@@ -556,10 +533,48 @@ extern "C" int dlrm_head_step(int64_t M, int64_t K, const float* X, int64_t ldx,
   else if (nc <= 12) HR(12); else if (nc <= 17) HR(17); else if (nc <= 24) HR(24); else HR(32);
 #undef HR
   DLRM_LAUNCH_CHECK(name);
+  if (defer) {  // the finalize pass rides on a later launch (dlrm_gemm_f32_group_role)
+    defer->head.M = M, defer->head.K = K, defer->head.nblk = nblk, defer->head.part = part;
+    defer->head.w = w, defer->head.dw = dw_out, defer->head.row_loss = row_loss;
+    defer->head.loss_out = loss_out, defer->head.lr = lr, defer->head.accumulate = accumulate;
+    defer->blocks = (int32_t)(dlrm::ceil_div(dlrm::ceil_div(K, (int64_t)4), (int64_t)8) * 8);
+    defer->kind = kRoleHead;
+    return DLRM_OK;
+  }
   hipLaunchKernelGGL(head_finalize_kernel, dim3(dlrm::ceil_div(K, 4)), dim3(256), 0, st, M, K,
                      nblk, part, w, lr, dw_out, accumulate, row_loss, loss_out);
   DLRM_LAUNCH_CHECK(name);
   return DLRM_OK;
+}
+
+}  // namespace
+
+extern "C" int dlrm_head_step(int64_t M, int64_t K, const float* X, int64_t ldx, float* w,
+                              const float* target, int32_t loss_kind, float clamp_lo,
+                              float grad_scale, float* prob_out, float* dz_out, float* loss_out,
+                              float* dX, int64_t lddx, int32_t relu_mask, float* dw_out,
+                              int32_t accumulate, float lr, void* workspace,
+                              size_t workspace_bytes, dlrm_stream_t stream) {
+  return head_step(M, K, X, ldx, w, target, loss_kind, clamp_lo, grad_scale, prob_out, dz_out,
+                   loss_out, dX, lddx, relu_mask, dw_out, accumulate, lr, workspace,
+                   workspace_bytes, nullptr, stream, "dlrm_head_step");
+}
+
+extern "C" int dlrm_head_step_defer(int64_t M, int64_t K, const float* X, int64_t ldx, float* w,
+                                    const float* target, int32_t loss_kind, float clamp_lo,
+                                    float grad_scale, float* prob_out, float* dz_out,
+                                    float* loss_out, float* dX, int64_t lddx, int32_t relu_mask,
+                                    float* dw_out, int32_t accumulate, float lr, void* workspace,
+                                    size_t workspace_bytes, dlrm_launch_role* role,
+                                    dlrm_stream_t stream) {
+  const char* name = "dlrm_head_step_defer";
+  DLRM_ARG(role, "%s: null role", name);
+  auto* r = reinterpret_cast<LaunchRole*>(role);
+  *r = LaunchRole{};
+  r->magic = kRoleMagic;
+  return head_step(M, K, X, ldx, w, target, loss_kind, clamp_lo, grad_scale, prob_out, dz_out,
+                   loss_out, dX, lddx, relu_mask, dw_out, accumulate, lr, workspace,
+                   workspace_bytes, r, stream, name);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -579,10 +579,10 @@ template <typename KeyT, typename IdxT, typename OffT>
 int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_base, int T, int B,
                const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
                const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
-               int64_t max_seg, int32_t* err, int presorted, TbeBwdRole* defer, hipStream_t st,
+               int64_t max_seg, int32_t* err, int presorted, LaunchRole* defer, hipStream_t st,
                const char* name) {
   if (defer) {  // until proven fusable: nothing deferred
-    *defer = TbeBwdRole{};
+    *defer = LaunchRole{};
     defer->magic = kRoleMagic;
   }
   if (N == 0) return DLRM_OK;
@@ -675,7 +675,7 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   if (blocks < 1) blocks = 1;
   if (defer && sizeof(KeyT) == 4 && vec4 && maxv == 1 && (per_table || bags) &&
       tbe_role_fusable(mode, lpb, psw, (int64_t)B * gbs)) {
-    TbeBwdRole& r = *defer;
+    LaunchRole& r = *defer;
     r.W = W, r.mom = mom, r.psw = psw, r.gout = gout, r.partial = w.partial;
     r.keys = reinterpret_cast<const uint32_t*>(w.keys_out);
     r.pos = w.pos_out;
@@ -685,6 +685,7 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
     r.B = B, r.ch = ch, r.mode = mode, r.lpb = lpb;
     // a multiple of 8 workgroups keeps the co-launched GEMM tiles' XCD remap aligned
     r.blocks = (int32_t)(dlrm::ceil_div(blocks, (int64_t)8) * 8);
+    r.kind = kRoleUpdate;
     return DLRM_OK;
   }
 #define LAUNCH2(LPB, VW, MV, MODE)                                                             \
@@ -742,7 +743,7 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
                  int B, const void* idx, int ib, const void* off, int ob, int64_t N,
                  int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
                  float eps, void* ws, size_t ws_bytes, int64_t max_seg, int32_t* err,
-                 int presorted, TbeBwdRole* defer, dlrm_stream_t stream, const char* name) {
+                 int presorted, LaunchRole* defer, dlrm_stream_t stream, const char* name) {
   DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
@@ -841,7 +842,7 @@ extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int
                       "dlrm_tbe_backward_dense");
 }
 
-static_assert(sizeof(TbeBwdRole) <= sizeof(dlrm_tbe_bwd_role), "dlrm_tbe_bwd_role too small");
+static_assert(sizeof(LaunchRole) <= sizeof(dlrm_launch_role), "dlrm_launch_role too small");
 
 extern "C" int dlrm_tbe_backward_defer(
     int32_t mode, float* weights, float* momentum, int64_t D, const int64_t* row_base,
@@ -849,13 +850,13 @@ extern "C" int dlrm_tbe_backward_defer(
     int32_t offset_bits, int64_t num_lookups, int64_t total_rows,
     const float* per_sample_weights, const float* grad_out, int64_t grad_batch_stride, float lr,
     float eps, int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes,
-    int32_t* error_flag, int32_t presorted, dlrm_tbe_bwd_role* role, dlrm_stream_t stream) {
+    int32_t* error_flag, int32_t presorted, dlrm_launch_role* role, dlrm_stream_t stream) {
   const char* name = "dlrm_tbe_backward_defer";
   DLRM_ARG(role, "%s: null role", name);
   DLRM_ARG(mode == 0 || mode == 1, "%s: mode must be 0 (sgd) or 1 (rowwise adagrad)", name);
   DLRM_ARG(mode == 0 || momentum, "%s: rowwise adagrad needs momentum", name);
-  auto* r = reinterpret_cast<TbeBwdRole*>(role);
-  *r = TbeBwdRole{};
+  auto* r = reinterpret_cast<LaunchRole*>(role);
+  *r = LaunchRole{};
   r->magic = kRoleMagic;
   return bwd_dispatch(mode == 0 ? MODE_SGD : MODE_ADAGRAD, weights, mode == 0 ? nullptr : momentum,
                       D, row_base, T, B, indices, index_bits, offsets, offset_bits, num_lookups,
@@ -869,11 +870,11 @@ extern "C" int dlrm_tbe_sort_defer(const int64_t* row_base, int32_t T, int32_t B
                                    int32_t offset_bits, int64_t num_lookups, int64_t total_rows,
                                    int64_t D, int64_t max_lookups_per_table, void* workspace,
                                    size_t workspace_bytes, int32_t* error_flag,
-                                   dlrm_tbe_bwd_role* role, dlrm_stream_t stream) {
+                                   dlrm_launch_role* role, dlrm_stream_t stream) {
   const char* name = "dlrm_tbe_sort_defer";
   DLRM_ARG(role, "%s: null role", name);
-  auto* r = reinterpret_cast<TbeBwdRole*>(role);
-  *r = TbeBwdRole{};
+  auto* r = reinterpret_cast<LaunchRole*>(role);
+  *r = LaunchRole{};
   r->magic = kRoleMagic;
   const int64_t N = num_lookups;
   const bool keys32 = (uint64_t)total_rows < 0xFFFFFFFFull;
@@ -910,11 +911,12 @@ extern "C" int dlrm_tbe_sort_defer(const int64_t* row_base, int32_t T, int32_t B
   r->pos = w.pos_out;
   r->bag_of = w.bag_of;
   r->blocks = (int32_t)(dlrm::ceil_div((int64_t)T + 1, (int64_t)8) * 8);
+  r->kind = kRoleSort;
   return DLRM_OK;
 }
 
-extern "C" int32_t dlrm_tbe_bwd_role_blocks(const dlrm_tbe_bwd_role* role) {
-  const auto* r = reinterpret_cast<const TbeBwdRole*>(role);
+extern "C" int32_t dlrm_role_blocks(const dlrm_launch_role* role) {
+  const auto* r = reinterpret_cast<const LaunchRole*>(role);
   return r && r->magic == kRoleMagic ? r->blocks : 0;
 }
 

@@ -1,9 +1,10 @@
 // Embedding backward update phases (sorted-run block pass + cross-block combine) as
 // device bodies: run by their own kernels (tbe_bwd.hip) or as extra workgroups of a
-// grouped GEMM launch (gemm.hip, TbeBwdRole).  See tbe_bwd.hip for the pipeline.
+// grouped GEMM launch (gemm.hip, LaunchRole).  See tbe_bwd.hip for the pipeline.
 #pragma once
 #include <type_traits>
 
+#include "head_roles.hpp"
 #include "tbe_common.hpp"
 #include "tbe_sort.hpp"
 
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_combine_kernel(
 // Fused instantiations: float4 rows with one chunk per lane (D = 4 * LPB, LPB 4..32), SGD
 // or row-wise Adagrad, 32-bit keys, bags by sorted position, no per-sample weights.
 constexpr uint32_t kRoleMagic = 0x7b3e0001u;
-struct TbeBwdRole {
+struct LaunchRole {
   float* W;
   float* mom;
   const uint32_t* keys;
@@ -509,7 +510,24 @@ struct TbeBwdRole {
   const int64_t* row_base;
   int32_t* err;
   int32_t T, ibits, obits;
+  int32_t kind;  // kRoleUpdate (phases 1, 2), kRoleSort (3), kRoleHead (4)
+  // phase 4, the head's finalize pass (dlrm_head_step_defer)
+  struct {
+    int64_t M, K, nblk;
+    const float* part;
+    float* w;
+    float* dw;
+    const float* row_loss;
+    float* loss_out;
+    float lr;
+    int32_t accumulate;
+  } head;
 };
+enum { kRoleNone = 0, kRoleUpdate = 1, kRoleSort = 2, kRoleHead = 3 };
+inline int role_kind_of_phase(int phase) {
+  return phase == 1 || phase == 2 ? kRoleUpdate : phase == 3 ? kRoleSort : phase == 4 ? kRoleHead
+                                                                                       : kRoleNone;
+}
 
 inline bool tbe_role_fusable(int mode, int lpb, const float* psw, int64_t grad_extent) {
   return (mode == MODE_SGD || mode == MODE_ADAGRAD) && lpb >= 4 && lpb <= 32 && !psw &&
@@ -517,7 +535,7 @@ inline bool tbe_role_fusable(int mode, int lpb, const float* psw, int64_t grad_e
 }
 
 template <int PHASE, int LPB, int MODE>
-__device__ __forceinline__ void tbe_role_pass(const TbeBwdRole& r, int blk) {
+__device__ __forceinline__ void tbe_role_pass(const LaunchRole& r, int blk) {
   if constexpr (PHASE == 1)
     tbe_bwd_block_body<LPB, 4, 1, uint32_t, MODE, true, 4, true>(r.W, r.mom, r.D, r.B, r.keys, r.pos,
                                                         r.bag_of, r.psw, r.gout, r.gbs, r.N,
@@ -529,7 +547,7 @@ __device__ __forceinline__ void tbe_role_pass(const TbeBwdRole& r, int blk) {
 }
 
 template <int PHASE, int LPB>
-__device__ __forceinline__ void tbe_role_lpb(const TbeBwdRole& r, int blk) {
+__device__ __forceinline__ void tbe_role_lpb(const LaunchRole& r, int blk) {
   if (r.mode == MODE_SGD)
     tbe_role_pass<PHASE, LPB, MODE_SGD>(r, blk);
   else
@@ -543,7 +561,7 @@ using RoleSortLds = SegLds<kRoleSortThreads, kRoleSortItems, true>;
 constexpr int kRoleSortCap = kRoleSortThreads * kRoleSortItems;
 
 template <typename IdxT, typename OffT>
-__device__ __forceinline__ void tbe_role_sort(const TbeBwdRole& r, int blk, void* lds) {
+__device__ __forceinline__ void tbe_role_sort(const LaunchRole& r, int blk, void* lds) {
   if (blk > r.T) return;  // blocks are rounded up to a multiple of 8
   segsort_body<kRoleSortThreads, kRoleSortItems, true, IdxT, OffT>(
       static_cast<const IdxT*>(r.idx), static_cast<const OffT*>(r.off), r.row_base, r.T, r.B, r.N,
@@ -552,7 +570,13 @@ __device__ __forceinline__ void tbe_role_sort(const TbeBwdRole& r, int blk, void
 }
 
 template <int PHASE>
-__device__ __forceinline__ void tbe_role_run(const TbeBwdRole& r, int blk, void* lds) {
+__device__ __forceinline__ void tbe_role_run(const LaunchRole& r, int blk, void* lds) {
+  if constexpr (PHASE == 4) {
+    head_finalize_body(r.head.M, r.head.K, r.head.nblk, r.head.part, r.head.w, r.head.lr,
+                       r.head.dw, r.head.accumulate, r.head.row_loss, r.head.loss_out, blk,
+                       r.blocks, static_cast<float*>(lds));
+    return;
+  }
   if constexpr (PHASE == 3) {
     if (r.ibits == 32 && r.obits == 32) tbe_role_sort<int32_t, int32_t>(r, blk, lds);
     else if (r.ibits == 32) tbe_role_sort<int32_t, int64_t>(r, blk, lds);

@@ -1,7 +1,7 @@
 // Per-table LDS radix sort of the embedding backward (tbe_bwd.hip's pipeline step 2) as a
 // workgroup-size-generic body: 1024 threads x 4 items in the lookup launch / the backward
 // (tbe_bwd.hip), 256 threads x 8 items as an extra role of a grouped GEMM launch (gemm.hip,
-// TbeBwdRole phase 3: the sort needs only the indices, so it can ride on any launch before
+// LaunchRole phase 3: the sort needs only the indices, so it can ride on any launch before
 // the update - its LDS passes are latency-bound, the GEMM tiles MFMA-bound).
 #pragma once
 #include "tbe_common.hpp"

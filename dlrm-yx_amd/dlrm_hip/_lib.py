@@ -49,9 +49,9 @@ class MlpChain(ctypes.Structure):
 
 
 # name -> (restype, argtypes); mirrors include/dlrm_hip.h exactly.
-class TbeBwdRole(ctypes.Structure):
-    """struct dlrm_tbe_bwd_role (include/dlrm_hip.h): a deferred embedding update."""
-    _fields_ = [("opaque", ctypes.c_uint64 * 24)]
+class LaunchRole(ctypes.Structure):
+    """struct dlrm_launch_role (include/dlrm_hip.h): a deferred embedding update."""
+    _fields_ = [("opaque", ctypes.c_uint64 * 32)]
 
 
 P = c_void_p
@@ -118,7 +118,10 @@ SIGNATURES = {
                                           c_int32, P, c_int32, c_int64, c_int64, P, P,
                                           c_int64, c_float, c_float, c_int64, P, c_size_t, P,
                                           c_int32, P, P]),
-    "dlrm_tbe_bwd_role_blocks": (c_int32, [P]),
+    "dlrm_role_blocks": (c_int32, [P]),
+    "dlrm_head_step_defer": (c_int32, [c_int64, c_int64, P, c_int64, P, P, c_int32, c_float,
+                                       c_float, P, P, P, P, c_int64, c_int32, P, c_int32,
+                                       c_float, P, c_size_t, P, P]),
     "dlrm_tbe_sort_defer": (c_int32, [P, c_int32, c_int32, P, c_int32, P, c_int32, c_int64,
                                       c_int64, c_int64, c_int64, P, c_size_t, P, P, P]),
     "dlrm_gemm_f32_splits": (c_int32, [P]),

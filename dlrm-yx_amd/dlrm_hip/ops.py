@@ -405,13 +405,13 @@ def tbe_backward_defer(mode: str, weights: torch.Tensor, row_base: torch.Tensor,
     need = tbe_backward_workspace_size(N, total_rows, D)
     if workspace is None:
         workspace = _ws("tbe_bwd", need, weights.device)
-    role = _lib.TbeBwdRole()
+    role = _lib.LaunchRole()
     _lib.call("dlrm_tbe_backward_defer", 0 if mode == "sgd" else 1, _p(weights), _p(momentum),
               D, _p(row_base), T, B, _p(indices), _bits(indices), _p(offsets), _bits(offsets), N,
               total_rows, _p(per_sample_weights), _p(grad_out), grad_batch_stride, lr, eps,
               int(max_lookups_per_table), _p(workspace), workspace.numel(), _p(error_flag),
               int(presorted), ctypes.byref(role), _stream(weights.device))
-    return role if tbe_role_blocks(role) > 0 else None
+    return role if role_blocks(role) > 0 else None
 
 
 def tbe_sort_defer(row_base: torch.Tensor, T: int, B: int, indices: torch.Tensor,
@@ -421,17 +421,17 @@ def tbe_sort_defer(row_base: torch.Tensor, T: int, B: int, indices: torch.Tensor
     (dlrm_tbe_sort_defer); the backward then runs with presorted=True.  None: nothing to
     carry (the sort already ran, or the backward sorts itself)."""
     _check_cuda(row_base, indices, offsets, workspace, error_flag)
-    role = _lib.TbeBwdRole()
+    role = _lib.LaunchRole()
     _lib.call("dlrm_tbe_sort_defer", _p(row_base), T, B, _p(indices), _bits(indices),
               _p(offsets), _bits(offsets), indices.numel(), int(total_rows), int(D),
               int(max_lookups_per_table), _p(workspace), workspace.numel(), _p(error_flag),
               ctypes.byref(role), _stream(indices.device))
-    return role if tbe_role_blocks(role) > 0 else None
+    return role if role_blocks(role) > 0 else None
 
 
-def tbe_role_blocks(role) -> int:
+def role_blocks(role) -> int:
     """Workgroups a deferred update pass adds to the launch carrying it (0: none)."""
-    return 0 if role is None else _lib.query("dlrm_tbe_bwd_role_blocks", ctypes.byref(role))
+    return 0 if role is None else _lib.query("dlrm_role_blocks", ctypes.byref(role))
 
 
 def tbe_expand_grad(D: int, T: int, B: int, offsets: torch.Tensor, num_lookups: int,
@@ -779,19 +779,25 @@ def head_step(X: torch.Tensor, w: torch.Tensor, target: torch.Tensor, loss: str 
               prob: Optional[torch.Tensor] = None, dz: Optional[torch.Tensor] = None,
               loss_out: Optional[torch.Tensor] = None, dX: Optional[torch.Tensor] = None,
               relu_mask: bool = True, dw: Optional[torch.Tensor] = None, accumulate: bool = False,
-              lr: float = 0.0, workspace: Optional[torch.Tensor] = None):
+              lr: float = 0.0, workspace: Optional[torch.Tensor] = None, defer: bool = False):
     """Fused head (dlrm_head_step): X [M, K] with the folded bias column, w [K] (updated in
-    place by SGD when lr != 0 and dw is None)."""
+    place by SGD when lr != 0 and dw is None).  ``defer``: the second launch (column sums,
+    update, mean loss) becomes the returned role, pass 4 of a later gemm_group
+    (dlrm_head_step_defer); w / dw / loss_out / workspace untouched until then."""
     M, K = X.shape
     need = _lib.query("dlrm_head_step_workspace_size", M, K)
     if workspace is None or workspace.numel() < need:
         workspace = _ws("head_step", need, X.device)
     _check_cuda(X, w, target)
-    _lib.call("dlrm_head_step", M, K, _p(X), X.stride(0), _p(w), _p(target),
-              LOSS_BCE if loss == "bce" else LOSS_MSE, float(clamp_lo), float(grad_scale),
-              _p(prob), _p(dz), _p(loss_out), _p(dX), dX.stride(0) if dX is not None else 0,
-              int(relu_mask), _p(dw), int(accumulate), float(lr), _p(workspace),
-              workspace.numel(), _stream(X.device))
+    args = (M, K, _p(X), X.stride(0), _p(w), _p(target),
+            LOSS_BCE if loss == "bce" else LOSS_MSE, float(clamp_lo), float(grad_scale),
+            _p(prob), _p(dz), _p(loss_out), _p(dX), dX.stride(0) if dX is not None else 0,
+            int(relu_mask), _p(dw), int(accumulate), float(lr), _p(workspace), workspace.numel())
+    if defer:
+        role = _lib.LaunchRole()
+        _lib.call("dlrm_head_step_defer", *args, ctypes.byref(role), _stream(X.device))
+        return role
+    _lib.call("dlrm_head_step", *args, _stream(X.device))
     return prob, dz, loss_out
 
 

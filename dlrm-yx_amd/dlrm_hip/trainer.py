@@ -240,6 +240,8 @@ class DLRMTrainer:
         # launch saves (profiles/r04_sort_role_ab.txt)
         self.sort_role = False
         self.sort_role_at = 0  # which top-MLP forward GEMM launch carries it
+        # one GPU: the head's finalize pass as a role of the top-MLP backward's first launch
+        self.head_role = True
         # bottom-MLP forward workgroups per 16-row block in the lookup launch (0 = auto)
         self.bottom_parts = 0
         self._cus = torch.cuda.get_device_properties(self.dev).multi_processor_count \
@@ -704,14 +706,19 @@ class DLRMTrainer:
             G = bufs["g"]
             gi = 0
             gview = G[gi][:, :last.Kp]
+            # one GPU: the head's second launch (column sums + update + mean loss) rides on
+            # the top-MLP backward's first GEMM launch (dlrm_head_step_defer)
+            head_role = self.head_role and not dist and profile is None and len(self.top) > 1
             with record_function("## Loss Compute ##"), prof("head"):
-                ops.head_step(h[:, :last.Kp], last.W[0, :last.Kp], batch.target,
-                              cfg.loss_function, cfg.loss_threshold, 1.0, prob=bufs["prob"],
-                              dz=bufs["dz"], loss_out=bufs["loss"], dX=gview,
-                              relu_mask=len(self.top) > 1,
-                              dw=None if fused_opt else last.gW[0, :last.Kp],
-                              lr=lr if fused_opt else 0.0,
-                              workspace=self._ws_head_step(Bl, last.Kp))
+                r = ops.head_step(h[:, :last.Kp], last.W[0, :last.Kp], batch.target,
+                                  cfg.loss_function, cfg.loss_threshold, 1.0, prob=bufs["prob"],
+                                  dz=bufs["dz"], loss_out=bufs["loss"], dX=gview,
+                                  relu_mask=len(self.top) > 1,
+                                  dw=None if fused_opt else last.gW[0, :last.Kp],
+                                  lr=lr if fused_opt else 0.0,
+                                  workspace=self._ws_head_step(Bl, last.Kp), defer=head_role)
+                if head_role:
+                    self._roles = [x for x in self._roles if x is not None] + [(r, 4)]
             g = gview
             rq = []  # reduce jobs riding on the next launch; G rotates over three buffers
             bwd = record_function("## Backward ##")

@@ -101,8 +101,8 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  *    at `partial`; dlrm_tbe_forward_presort's out = NULL (sort-only) mode is used by the
  *    engine (round 4).
  * 6: dlrm_tbe_backward_defer + dlrm_gemm_f32_group_role: the embedding backward's update
- *    passes (and dlrm_tbe_sort_defer: the per-table sort) as extra workgroups of grouped
- *    GEMM launches; dlrm_mlp_chain gains parts /
+ *    passes (and dlrm_tbe_sort_defer: the per-table sort; dlrm_head_step_defer: the head's
+ *    finalize pass) as extra workgroups of grouped GEMM launches (dlrm_launch_role); dlrm_mlp_chain gains parts /
  *    split_layer / tickets (several workgroups per 16-row block) (round 4). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
@@ -355,9 +355,9 @@ int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int64_t* row_b
  * role passes are no-ops.  Until both phases have run, the workspace,
  * weights, momentum and grad_out must stay as they are.
  */
-typedef struct dlrm_tbe_bwd_role {
-  uint64_t opaque[24];
-} dlrm_tbe_bwd_role;
+typedef struct dlrm_launch_role {
+  uint64_t opaque[32];
+} dlrm_launch_role;
 int dlrm_tbe_backward_defer(int32_t mode, float* weights, float* momentum, int64_t D,
                             const int64_t* row_base, int32_t T, int32_t B,
                             const void* indices, int32_t index_bits, const void* offsets,
@@ -366,9 +366,9 @@ int dlrm_tbe_backward_defer(int32_t mode, float* weights, float* momentum, int64
                             int64_t grad_batch_stride, float lr, float eps,
                             int64_t max_lookups_per_table, void* workspace,
                             size_t workspace_bytes, int32_t* error_flag, int32_t presorted,
-                            dlrm_tbe_bwd_role* role, dlrm_stream_t stream);
+                            dlrm_launch_role* role, dlrm_stream_t stream);
 /* Workgroups a deferred pass adds to the launch that carries it (0: nothing deferred). */
-int32_t dlrm_tbe_bwd_role_blocks(const dlrm_tbe_bwd_role* role);
+int32_t dlrm_role_blocks(const dlrm_launch_role* role);
 /*
  * This batch's per-table sort (what dlrm_tbe_forward_presort's sort role does), deferred
  * into a later grouped GEMM launch: *role becomes pass 3 for dlrm_gemm_f32_group_role,
@@ -384,7 +384,7 @@ int dlrm_tbe_sort_defer(const int64_t* row_base, int32_t T, int32_t B, const voi
                         int32_t index_bits, const void* offsets, int32_t offset_bits,
                         int64_t num_lookups, int64_t total_rows, int64_t D,
                         int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes,
-                        int32_t* error_flag, dlrm_tbe_bwd_role* role, dlrm_stream_t stream);
+                        int32_t* error_flag, dlrm_launch_role* role, dlrm_stream_t stream);
 
 /*
  * Sparse-gradient values of an EmbeddingBag(sparse=True) backward
@@ -579,12 +579,13 @@ int32_t dlrm_gemm_f32_splits(const dlrm_gemm_problem* problem);
 size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits);
 int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
                         size_t workspace_bytes, dlrm_stream_t stream);
-/* dlrm_gemm_f32_group plus pass `phase` (1 or 2) of a deferred embedding update
- * (dlrm_tbe_backward_defer), or the deferred sort (phase 3, dlrm_tbe_sort_defer), as extra
- * workgroups of the same launch; n may be 0 (the pass alone).  role == NULL, or a role with nothing deferred: dlrm_gemm_f32_group.  The
+/* dlrm_gemm_f32_group plus pass `phase` of a deferred role as extra workgroups of the same
+ * launch: 1 / 2 the embedding update (dlrm_tbe_backward_defer), 3 the per-table sort
+ * (dlrm_tbe_sort_defer), 4 the head's finalize pass (dlrm_head_step_defer); n may be 0
+ * (the pass alone).  role == NULL, or a role with nothing deferred: dlrm_gemm_f32_group.  The
  * problems must not touch the update's buffers (weights, momentum, grad_out, workspace). */
 int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
-                             size_t workspace_bytes, const dlrm_tbe_bwd_role* role,
+                             size_t workspace_bytes, const dlrm_launch_role* role,
                              int32_t phase, dlrm_stream_t stream);
 
 /* Workspace for dlrm_colsum_f32 (deterministic two-pass column reduction). */
@@ -631,6 +632,17 @@ int dlrm_head_step(int64_t M, int64_t K, const float* X, int64_t ldx, float* w,
                    float* prob_out, float* dz_out, float* loss_out, float* dX, int64_t lddx,
                    int32_t relu_mask, float* dw_out, int32_t accumulate, float lr,
                    void* workspace, size_t workspace_bytes, dlrm_stream_t stream);
+/* dlrm_head_step with its second launch (the column sums, the weight update and the mean
+ * loss) deferred: *role becomes pass 4 of a later dlrm_gemm_f32_group_role (typically the
+ * top-MLP backward's first launch, which reads dX but not w).  The workspace, w, dw_out
+ * and loss_out must stay as they are until then; prob_out / dz_out / dX are written here.
+ * (ABI v6) */
+int dlrm_head_step_defer(int64_t M, int64_t K, const float* X, int64_t ldx, float* w,
+                         const float* target, int32_t loss_kind, float clamp_lo,
+                         float grad_scale, float* prob_out, float* dz_out, float* loss_out,
+                         float* dX, int64_t lddx, int32_t relu_mask, float* dw_out,
+                         int32_t accumulate, float lr, void* workspace, size_t workspace_bytes,
+                         dlrm_launch_role* role, dlrm_stream_t stream);
 
 /* Elementwise: dX[m][k] = dz[m] * w[k] * (relu_mask ? (X[m][k] > 0) : 1). */
 int dlrm_outer_drelu(int64_t M, int64_t K, const float* dz, const float* w, const float* X,

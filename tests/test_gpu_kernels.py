@@ -518,6 +518,57 @@ def test_head_step_fused(ops, loss, clamp, M, K):
     assert ok, msg
 
 
+@pytest.mark.parametrize("M,K", [(2048, 260), (37, 13), (128, 260)])
+@pytest.mark.parametrize("sgd", [True, False])
+def test_head_step_deferred_into_gemm_launch(ops, M, K, sgd):
+    """dlrm_head_step_defer + its finalize pass as pass 4 of a grouped GEMM launch (or of an
+    otherwise empty one): prob, dz, dX, the loss and the weight update / gradient bitwise
+    the two-launch dlrm_head_step's; the GEMM result bitwise the plain launch's."""
+    torch.manual_seed(M + K)
+    X = torch.randn(M, K, device=dev).relu()
+    X[:, K - 1] = 1.0
+    w0 = torch.randn(K, device=dev) * 0.1
+    t = torch.rand(M, device=dev).round()
+    A1, B1 = torch.randn(300, 260, device=dev), torch.randn(260, 512, device=dev)
+    res = []
+    for defer in (False, True):
+        w = w0.clone()
+        prob, dz, L = (torch.empty(M, device=dev), torch.empty(M, device=dev),
+                       torch.empty(1, device=dev))
+        dX = torch.empty(M, K, device=dev)
+        dw = None if sgd else torch.full((K,), 0.25, device=dev)
+        kw = dict(prob=prob, dz=dz, loss_out=L, dX=dX, relu_mask=True, dw=dw,
+                  accumulate=not sgd, lr=0.5 if sgd else 0.0)
+        p1, c1 = ops.gemm_problem(A1, B1)
+        if defer:
+            role = ops.head_step(X, w, t, "bce", 0.0, 1.0, defer=True, **kw)
+            assert ops.role_blocks(role) % 8 == 0 and ops.role_blocks(role) * 4 >= K
+            ops.gemm_group([p1] if M != 37 else [], None, dev, role=role, phase=4)
+            if M == 37:
+                ops.gemm_group([p1], None, dev)
+        else:
+            ops.head_step(X, w, t, "bce", 0.0, 1.0, **kw)
+            ops.gemm_group([p1], None, dev)
+        torch.cuda.synchronize()
+        res.append([v.cpu() for v in (w, prob, dz, L, dX, c1)] + ([dw.cpu()] if dw is not None else []))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_gemm_group_role_phase_must_match_the_role(ops):
+    """A role used with another kind's phase (an update role as pass 3 / 4, a head role
+    as pass 1) is refused (INVALID_ARG) before anything is launched."""
+    from dlrm_hip import _lib
+    X = torch.rand(64, 20, device=dev)
+    role = ops.head_step(X, torch.rand(20, device=dev), torch.rand(64, device=dev), "mse",
+                         defer=True, lr=0.1)
+    for ph in (1, 2, 3):
+        with pytest.raises(_lib.DLRMHipError):
+            ops.gemm_group([], None, dev, role=role, phase=ph)
+    ops.gemm_group([], None, dev, role=role, phase=4)
+    torch.cuda.synchronize()
+
+
 def test_dense_optimizers(ops):
     torch.manual_seed(5)
     p, g = torch.randn(1000), torch.randn(1000)
@@ -1093,7 +1144,7 @@ def test_tbe_backward_deferred_into_gemm_launches(ops, mode, D, sort):
                 role = ops.tbe_backward_defer(mode, W, row_base, T, B, idx, off, G, **kw)
                 fusable = D in (16, 32, 64, 128)
                 assert (role is not None) == fusable
-                assert ops.tbe_role_blocks(role) % 8 == 0
+                assert ops.role_blocks(role) % 8 == 0
                 ops.gemm_group(first, gws, dev, role=role, phase=1)
                 ops.gemm_group([] if D == 16 else second, gws, dev, role=role, phase=2)
                 if D != 16:
@@ -1178,7 +1229,7 @@ def test_gemm_group_role_rejects_a_foreign_role(ops):
     """A role struct not filled by dlrm_tbe_backward_defer is refused (INVALID_ARG)."""
     import ctypes
     from dlrm_hip import _lib
-    role = _lib.TbeBwdRole()
+    role = _lib.LaunchRole()
     ctypes.memset(ctypes.byref(role), 0x5a, ctypes.sizeof(role))
     with pytest.raises(_lib.DLRMHipError):
         ops.gemm_group([], None, dev, role=role, phase=1)

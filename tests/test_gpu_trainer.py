@@ -759,3 +759,40 @@ def test_sort_role_matches_lookup_launch_sort(name, B, graph):
                     tr._bufs[(B, B)]["prob"].cpu().clone()))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name,B", [("c3_small", 512), ("c2_small", 128)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_head_role_matches_two_launch_head(name, B, graph):
+    """The head's finalize pass as a role of the top-MLP backward's first launch
+    (head_role) vs its own launch: 3 steps leave bitwise the same state and loss."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function=c["loss"],
+                        learning_rate=c["lr"])
+    res = []
+    for role in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.head_role = role
+        batches = [tr.synthetic_batch(B, 1, seed=s) for s in range(3)]
+        if graph:
+            tr.step(batches[0])
+            run = tr.capture(batches[0])
+            for b in batches[1:]:
+                for src, dst in zip((b.X, b.offsets, b.indices, b.target),
+                                    (batches[0].X, batches[0].offsets, batches[0].indices,
+                                     batches[0].target)):
+                    dst.copy_(src)
+                run()
+        else:
+            for b in batches:
+                tr.step(b)
+        torch.cuda.synchronize()
+        assert not tr._roles
+        bufs = tr._bufs[(B, B)]
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
+                    bufs["prob"].cpu().clone(), bufs["loss"].cpu().clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -78,6 +78,17 @@ sortab)  # the per-table sort: lookup launch vs a top-MLP forward launch (VARIAN
     done
   done
   ;;
+flag)  # FLAG=--xyz: bench lines with $FLAG 0 and $FLAG 1 (CFGS)
+  for cfg in ${CFGS:-terabyte kaggle b256}; do
+    for val in 0 1; do
+      if [ "$cfg" = b256 ]; then a="--batch 256"; else a="--config $cfg"; fi
+      tag="${FLAG#--}_$val"
+      $B $a $FLAG $val --steps 300 --warmup 30 > "$OUT/${cfg}_$tag.json" 2> "$OUT/${cfg}_$tag.err" \
+        || exit $?
+      python -c "import json;d=json.load(open('$OUT/${cfg}_$tag.json'));print('$cfg $FLAG $val',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+    done
+  done
+  ;;
 trace)
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c3 ${BOT:+--bot-sched $BOT} || exit $?
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c2 --config kaggle ${BOT:+--bot-sched $BOT} || exit $?
