@@ -13,9 +13,10 @@ import sys
 from collections import defaultdict
 
 GROUPS = [
-    ("gemm", ("gemm_group_kernel", "gemm_generic_kernel", "gemm_rowsum_kernel",
+    # gemm_role_kernel: GEMM launches that also carry a deferred TBE / head pass
+    ("gemm", ("gemm_group_kernel", "gemm_role_kernel", "gemm_generic_kernel", "gemm_rowsum_kernel",
               "gemm_f32_", "gemm_splitk_reduce_kernel")),
-    ("tbe_fwd", ("tbe_fwd_kernel", "tbe_fwd_presort_kernel")),  # presort: + sort + bottom MLP
+    ("tbe_fwd", ("tbe_fwd_kernel", "tbe_fwd_presort_kernel", "mlp_chain_kernel")),  # + sort, bottom MLP
     ("tbe_bwd", ("tbe_bwd_", "tbe_tiled_", "rocprim")),
     ("qr", ("qr_",)),
     ("interaction", ("interact_",)),
