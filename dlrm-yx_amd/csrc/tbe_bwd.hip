@@ -673,9 +673,14 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   int64_t blocks = dlrm::ceil_div(dlrm::ceil_div(nblocks, gpw), 4);
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  if (defer && sizeof(KeyT) == 4 && vec4 && maxv == 1 && (per_table || bags) &&
-      tbe_role_fusable(mode, lpb, psw, (int64_t)B * gbs)) {
-    LaunchRole& r = *defer;
+  // the lean passes (4 gradient rows in flight per lane group at <= 128 VGPRs: twice the
+  // resident waves of the 16-in-flight kernels, C1 block pass 100 -> ~65 us) wherever they
+  // apply - deferred into later launches, or launched here
+  if (sizeof(KeyT) == 4 && vec4 && maxv == 1 && (per_table || bags) &&
+      tbe_role_fusable(mode, lpb, psw, (int64_t)B * gbs) &&
+      (defer || dlrm::tuning(DLRM_TUNE_TBE_LEAN) != 1)) {
+    LaunchRole local{};
+    LaunchRole& r = defer ? *defer : local;
     r.W = W, r.mom = mom, r.psw = psw, r.gout = gout, r.partial = w.partial;
     r.keys = reinterpret_cast<const uint32_t*>(w.keys_out);
     r.pos = w.pos_out;
@@ -686,6 +691,11 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
     // a multiple of 8 workgroups keeps the co-launched GEMM tiles' XCD remap aligned
     r.blocks = (int32_t)(dlrm::ceil_div(blocks, (int64_t)8) * 8);
     r.kind = kRoleUpdate;
+    r.magic = kRoleMagic;
+    if (defer) return DLRM_OK;
+    hipLaunchKernelGGL(tbe_update_pass_kernel<1>, dim3(r.blocks), dim3(256), 0, st, r);
+    hipLaunchKernelGGL(tbe_update_pass_kernel<2>, dim3(r.blocks), dim3(256), 0, st, r);
+    DLRM_LAUNCH_CHECK(name);
     return DLRM_OK;
   }
 #define LAUNCH2(LPB, VW, MV, MODE)                                                             \

@@ -592,4 +592,11 @@ __device__ __forceinline__ void tbe_role_run(const LaunchRole& r, int blk, void*
   }
 }
 
+// The update passes as launches of their own (the backward's default wherever the lean
+// variant applies; same bodies as the GEMM-launch roles).
+template <int PHASE>
+__global__ __launch_bounds__(256, 4) void tbe_update_pass_kernel(const LaunchRole r) {
+  tbe_role_run<PHASE>(r, blockIdx.x, nullptr);
+}
+
 }  // namespace

@@ -116,12 +116,15 @@ const char* dlrm_last_error(void);
  *   DLRM_TUNE_GEMM_SPLIT : K splits of every FULL problem (with DLRM_TUNE_GEMM_TILE)
  *   DLRM_TUNE_TBE_BLOCK  : sorted lookups per TBE-backward block (16 or 64)
  *   DLRM_TUNE_TBE_SORT   : 1 = the device-wide radix sort even where the tiled per-table
- *                          sort applies */
+ *                          sort applies
+ *   DLRM_TUNE_TBE_LEAN   : 1 = the non-deferred backward's update passes as the
+ *                          16-rows-in-flight kernels even where the lean ones apply (ABI v6) */
 enum dlrm_tune_key {
   DLRM_TUNE_GEMM_TILE = 1,
   DLRM_TUNE_GEMM_SPLIT = 2,
   DLRM_TUNE_TBE_BLOCK = 3,
-  DLRM_TUNE_TBE_SORT = 4
+  DLRM_TUNE_TBE_SORT = 4,
+  DLRM_TUNE_TBE_LEAN = 5
 };
 int dlrm_set_tuning(int32_t key, int64_t value);
 int64_t dlrm_get_tuning(int32_t key);

@@ -1235,6 +1235,30 @@ def test_gemm_group_role_rejects_a_foreign_role(ops):
         ops.gemm_group([], None, dev, role=role, phase=1)
 
 
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
+@pytest.mark.parametrize("sort,D", [("per_table", 128), ("tiled", 64), ("global", 16),
+                                    ("tiled", 32)])
+def test_tbe_backward_lean_passes_match_16_in_flight(ops, mode, sort, D):
+    """The lean update passes (4 gradient rows in flight per lane group, the default where
+    they apply) vs the 16-in-flight kernels (DLRM_TUNE_TBE_LEAN = 1): bitwise the same
+    tables and momentum - the rows in flight change the load schedule, not the add order."""
+    L = 1 if sort == "per_table" else 40
+    rows, B = [3, 5000, 700, 90000], 256
+    T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 23, invalid=True)
+    W0 = torch.randn(sum(rows), D, device=dev) * 0.1
+    mom0 = torch.rand(sum(rows), device=dev)
+    res = []
+    for lean in (0, 1):
+        W, mom = W0.clone(), mom0.clone()
+        with ops.tuning(tbe_lean=lean, tbe_sort=1 if sort == "global" else 0):
+            ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8,
+                             momentum=mom,
+                             max_lookups_per_table=0 if sort == "global" else B * L)
+        torch.cuda.synchronize()
+        res.append((W.cpu(), mom.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
 def test_tbe_backward_tiled_sort_cap_violation(ops):
     """max_lookups_per_table underestimated (tiles cover 8192 of a table's 12800 lookups):
     that table is skipped (no update) and flagged; the others are updated."""
