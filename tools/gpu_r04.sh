@@ -39,6 +39,10 @@ configs)
       || exit $?
     echo "$cfg: $(head -c 200 "$OUT/bench_$cfg.json")"
   done
+  # the C3 widths at the W = 8 per-rank batch
+  timeout -k 10 400 python bench.py --batch 256 > "$OUT/bench_b256.json" 2> "$OUT/bench_b256.err" \
+    || exit $?
+  echo "b256: $(head -c 200 "$OUT/bench_b256.json")"
   ;;
 esac
 # (pmc only: bash tools/gpu_r04.sh pmc)
