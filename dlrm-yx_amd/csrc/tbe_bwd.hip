@@ -212,7 +212,49 @@ struct TiledPass {
   const int32_t* bag_of;  // non-null: the sorted values are BAGS (bag_of[position], read
                           // coalesced in pass 0) instead of positions, so the block kernel
                           // reads each lookup's bag in sorted order (no dependent gather)
+  // per-table passes (not global): a table of nrows rows needs ceil(bit_width(nrows) / DB)
+  // passes, at most npass; pass ps of such a table reads / writes the (ka, pa) or the
+  // final (ko, po) pair so that its own last pass lands in (ko, po), and passes past its
+  // own count skip it (e.g. 1 M-row tables in an 8 M-row call: 2 passes of 10 bits, not 3)
+  uint32_t* ka;
+  int32_t* pa;
+  uint32_t* ko;
+  int32_t* po;
+  int ps, npass;
 };
+
+// The pass as table t sees it (global mode: the host's ping-pong as given).
+struct PassView {
+  bool skip, first, last;
+  const uint32_t* kin;
+  const int32_t* pin;
+  uint32_t* kout;
+  int32_t* pout;
+};
+
+template <int DB>
+__device__ __forceinline__ PassView pass_view(const TiledPass& a, int64_t nrows) {
+  PassView v{};
+  if (a.global) {
+    v.first = a.first, v.last = a.last, v.kin = a.kin, v.pin = a.pin;
+    v.kout = a.kout, v.pout = a.pout;
+    return v;
+  }
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) <= nrows) ++bits;  // keys in [0, nrows]
+  int passes = (bits + DB - 1) / DB;
+  if (passes > a.npass) passes = a.npass;
+  v.skip = a.ps >= passes;
+  v.first = a.ps == 0;
+  v.last = a.ps == passes - 1;
+  const bool out_final = ((passes - 1 - a.ps) & 1) == 0;
+  const bool in_final = ((passes - a.ps) & 1) == 0;
+  v.kout = out_final ? a.ko : a.ka;
+  v.pout = out_final ? a.po : a.pa;
+  v.kin = a.ps == 0 ? nullptr : (in_final ? a.ko : a.ka);
+  v.pin = a.ps == 0 ? nullptr : (in_final ? a.po : a.pa);
+  return v;
+}
 
 template <int DB>
 struct TiledLds {
@@ -226,23 +268,23 @@ struct TiledLds {
 // Element e of tile j of table t: wave-striped (e = w*64*IT + u*64 + l), position
 // s + j*kTile + e.  Loads this thread's IT (key, pos, valid).
 template <int IT, typename IdxT>
-__device__ __forceinline__ void tiled_load(const TiledPass& a, const IdxT* __restrict__ idx,
-                                           int64_t s, int64_t n, int j, int64_t nrows,
-                                           uint32_t (&key)[IT], int32_t (&pos)[IT],
-                                           bool (&ok)[IT]) {
+__device__ __forceinline__ void tiled_load(const TiledPass& a, const PassView& v,
+                                           const IdxT* __restrict__ idx, int64_t s, int64_t n,
+                                           int j, int64_t nrows, uint32_t (&key)[IT],
+                                           int32_t (&pos)[IT], bool (&ok)[IT]) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
 #pragma unroll
   for (int u = 0; u < IT; ++u) {
     const int64_t e = (int64_t)j * kTile + w * (IT * 64) + u * 64 + l;
     ok[u] = e < n;
     const int64_t p = s + (ok[u] ? e : 0);
-    if (a.first && !a.global) {
+    if (v.first && !a.global) {
       const int64_t r = (int64_t)idx[p];
       key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
       pos[u] = a.bag_of ? a.bag_of[p] : (int32_t)p;
     } else {
-      key[u] = a.kin[p];
-      pos[u] = (a.first && a.bag_of) ? a.bag_of[p] : a.pin[p];  // (global pass 0: pin[p] = p)
+      key[u] = v.kin[p];
+      pos[u] = (v.first && a.bag_of) ? a.bag_of[p] : v.pin[p];  // (global pass 0: pin[p] = p)
     }
   }
 }
@@ -267,16 +309,18 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
   __shared__ uint32_t cnt[NB];
   const int t = blockIdx.x / a.J, j = blockIdx.x - (blockIdx.x / a.J) * a.J;
   int64_t s, n;
+  const int64_t nrows = a.row_base[t + 1] - a.row_base[t];
+  const PassView v = pass_view<DB>(a, nrows);
+  if (v.skip) return;
   if (!tiled_range(a, off, t, s, n)) {
-    if (a.first && j == 0 && threadIdx.x == 0 && a.err) atomicOr(a.err, DLRM_TBE_ERR_TABLE_CAP);
+    if (v.first && j == 0 && threadIdx.x == 0 && a.err) atomicOr(a.err, DLRM_TBE_ERR_TABLE_CAP);
     return;
   }
-  const int64_t nrows = a.row_base[t + 1] - a.row_base[t];
   for (int d = threadIdx.x; d < NB; d += kTileThreads) cnt[d] = 0;
   uint32_t key[kTileItems];
   int32_t pos[kTileItems];
   bool ok[kTileItems];
-  tiled_load<kTileItems>(a, idx, s, n, j, nrows, key, pos, ok);
+  tiled_load<kTileItems>(a, v, idx, s, n, j, nrows, key, pos, ok);
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < kTileItems; ++u)
@@ -302,14 +346,16 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const Tile
   const int t = blockIdx.x;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   int64_t s, n;
+  const PassView v = pass_view<DB>(a, a.row_base[t + 1] - a.row_base[t]);
+  if (v.skip) return;
   const bool fits = off_bits == 32
                         ? tiled_range(a, static_cast<const int32_t*>(off_v), t, s, n)
                         : tiled_range(a, static_cast<const int64_t*>(off_v), t, s, n);
   if (!fits) {
-    if (a.last)  // the table's range holds sentinels (no update)
+    if (v.last)  // the table's range holds sentinels (no update)
       for (int64_t i = tid; i < n; i += kTileThreads) {
-        a.kout[s + i] = a.sentinel;
-        a.pout[s + i] = (int32_t)(s + i);
+        v.kout[s + i] = a.sentinel;
+        v.pout[s + i] = (int32_t)(s + i);
       }
     return;
   }
@@ -382,15 +428,17 @@ __global__ __launch_bounds__(kScatThreads) void tbe_tiled_scatter_kernel(
   __shared__ TiledLds<DB> sm;
   const int t = blockIdx.x / a.J, j = blockIdx.x - (blockIdx.x / a.J) * a.J;
   int64_t s, n;
-  if (!tiled_range(a, off, t, s, n)) return;
-  if ((int64_t)j * kTile >= n) return;  // empty tile (uniform)
   const int64_t rb = a.row_base[t];
   const int64_t nrows = a.row_base[t + 1] - rb;
+  const PassView v = pass_view<DB>(a, nrows);
+  if (v.skip) return;
+  if (!tiled_range(a, off, t, s, n)) return;
+  if ((int64_t)j * kTile >= n) return;  // empty tile (uniform)
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   uint32_t key[kScatItems];
   int32_t pos[kScatItems];
   bool ok[kScatItems];
-  tiled_load<kScatItems>(a, idx, s, n, j, nrows, key, pos, ok);
+  tiled_load<kScatItems>(a, v, idx, s, n, j, nrows, key, pos, ok);
   for (int i = tid; i < NB * CS; i += kScatThreads) sm.cnt[i] = 0;
   __syncthreads();
   const uint64_t below = (1ull << l) - 1;
@@ -471,11 +519,11 @@ __global__ __launch_bounds__(kScatThreads) void tbe_tiled_scatter_kernel(
     const uint32_t k = sm.key[i];
     const uint32_t d = (k >> a.shift) & (NB - 1);
     const int64_t dst = s + h[d] + (i - sm.dstart[d]);
-    if (a.last && !a.global)
-      a.kout[dst] = k < (uint32_t)nrows ? (uint32_t)(rb + k) : a.sentinel;
+    if (v.last && !a.global)
+      v.kout[dst] = k < (uint32_t)nrows ? (uint32_t)(rb + k) : a.sentinel;
     else
-      a.kout[dst] = k;
-    a.pout[dst] = sm.pos[i];
+      v.kout[dst] = k;
+    v.pout[dst] = sm.pos[i];
   }
 }
 
@@ -495,17 +543,12 @@ void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base
   a.row_base = row_base, a.T = T, a.B = B, a.J = J, a.hist = hist, a.sentinel = sentinel;
   a.err = err;
   a.bag_of = bag_of;
-  // ping-pong so the last pass lands in (k_out, p_out)
-  uint32_t* kb[2] = {(npass & 1) ? k_out : k_a, (npass & 1) ? k_a : k_out};
-  int32_t* pb[2] = {(npass & 1) ? p_out : p_a, (npass & 1) ? p_a : p_out};
+  // per-table ping-pong (pass_view): each table's own last pass lands in (k_out, p_out)
+  a.ka = k_a, a.pa = p_a, a.ko = k_out, a.po = p_out;
+  a.npass = npass;
   for (int ps = 0; ps < npass; ++ps) {
     a.shift = ps * DB;
-    a.first = ps == 0;
-    a.last = ps == npass - 1;
-    a.kin = ps == 0 ? nullptr : kb[(ps - 1) & 1];
-    a.pin = ps == 0 ? nullptr : pb[(ps - 1) & 1];
-    a.kout = kb[ps & 1];
-    a.pout = pb[ps & 1];
+    a.ps = ps;
     hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(T * J), dim3(kTileThreads),
                        0, st, idx, off, a);
     hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(T), dim3(kTileThreads), 0, st, a,
@@ -600,11 +643,14 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   // large tables (> kSegCap lookups): the tiled per-table sort, its digit histograms in the
   // block kernel's partial buffer (free until the sort is done)
   const int64_t tiles_j = dlrm::ceil_div(max_seg > 0 ? max_seg : 1, (int64_t)kTile);
-  const int tdb = tiled_digit_bits(end_bit);
+  const int tdb = tiled_digit_bits(end_bit);  // the device-wide sort (global keys)
+  // the tiled sort passes over each table's OWN key bits (pass_view): 10-bit digits never
+  // need more passes than 8-bit ones there, and only the tables that need them run them
+  const int64_t part_space = (int64_t)2 * dlrm::ceil_div(N, (int64_t)CH) * D;
+  const int tdb_t = (int64_t)T * tiles_j * (1 << 10) <= part_space ? 10 : tdb;
   const bool tiled = !per_table && sizeof(KeyT) == 4 && max_seg > kSegCap &&
                      N < (int64_t)0x7fffffff && (int64_t)T * tiles_j < (int64_t)INT32_MAX &&
-                     (int64_t)T * tiles_j * (1 << tdb) <=
-                         (int64_t)2 * dlrm::ceil_div(N, (int64_t)CH) * D &&
+                     (int64_t)T * tiles_j * (1 << tdb_t) <= part_space &&
                      dlrm::tuning(DLRM_TUNE_TBE_SORT) != 1;
   // the tiled and global sorts carry each lookup's bag (not its position) when no
   // per-sample weights need the position: the block kernel then reads bags in sorted order
@@ -626,7 +672,7 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
     auto* ko = reinterpret_cast<uint32_t*>(w.keys_out);
     auto* ki = reinterpret_cast<uint32_t*>(w.keys_in);
     auto* hist = reinterpret_cast<uint32_t*>(w.partial);
-    if (tdb == 10)
+    if (tdb_t == 10)
       launch_tiled_sort<IdxT, OffT, 10>(static_cast<const IdxT*>(idx),
                                         static_cast<const OffT*>(off), row_base, T, B,
                                         (int)tiles_j, end_bit, ki, w.pos_in, ko, w.pos_out, hist,

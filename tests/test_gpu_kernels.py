@@ -1259,6 +1259,27 @@ def test_tbe_backward_lean_passes_match_16_in_flight(ops, mode, sort, D):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
+def test_tbe_backward_tiled_sort_per_table_pass_counts(ops, mode):
+    """Tables needing 1, 3, 1 and 2 passes of 10-bit digits in one call (2, 21, 10 and 16
+    key bits; the call's 21 global bits ask for 3): each table runs only its own passes,
+    its last one landing in the output buffers - bitwise the device-wide sort's update."""
+    rows, B, L, D = [3, 2_000_000, 700, 40000], 256, 40, 16
+    T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 29)
+    W0 = torch.randn(sum(rows), D, device=dev) * 0.1
+    mom0 = torch.rand(sum(rows), device=dev)
+    res = []
+    for tiled in (True, False):
+        W, mom = W0.clone(), mom0.clone()
+        with ops.tuning(tbe_sort=0 if tiled else 1):
+            ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8,
+                             momentum=mom, max_lookups_per_table=B * L)
+        torch.cuda.synchronize()
+        res.append((W.cpu(), mom.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert not torch.equal(res[0][0], W0.cpu())
+
+
 def test_tbe_backward_tiled_sort_cap_violation(ops):
     """max_lookups_per_table underestimated (tiles cover 8192 of a table's 12800 lookups):
     that table is skipped (no update) and flagged; the others are updated."""
