@@ -221,6 +221,9 @@ struct TiledPass {
   uint32_t* ko;
   int32_t* po;
   int ps, npass;
+  // the scan in chunks of JC tiles, C per table: csum[t][c][digit] = the chunk's counts
+  uint32_t* csum;
+  int C, JC;
 };
 
 // The pass as table t sees it (global mode: the host's ping-pong as given).
@@ -330,11 +333,63 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
   for (int d = threadIdx.x; d < NB; d += kTileThreads) h[d] = cnt[d];
 }
 
-// One workgroup per table: exclusive scan of its NB * J counts in (digit, tile) order.
-// hist is [t][j][d]: thread d walks the tiles of digit d (coalesced across the threads,
-// 32 loads in flight: the C1 shape's J = 50 tiles in two round trips), the digit totals
-// are scanned across the workgroup, then each thread rewrites its digit's column with
-// base + running count.
+// The exclusive scan of a table's NB * J counts in (digit, tile) order, in two launches
+// over chunks of JC tiles (a table of C chunks gets C workgroups in each: the device-wide
+// sort's one segment of J = N / 4096 tiles no longer walks in one workgroup - C1 shape
+// 2 x 51 -> ~2 x 5 us).  hist is [t][j][d]; a thread owns DPT digits.
+//   csum: workgroup (t, c) sums each digit over its chunk's tiles -> csum[t][c][d];
+//   scan: workgroup (t, c) adds up the chunk sums (all chunks: the digit totals, scanned
+//         across the workgroup; chunks < c: this chunk's start) and rewrites its tiles'
+//         counts as base + running count.
+constexpr int kScanChunk = 16, kMaxScanChunks = 64;
+// One chunk (the scan walks the tiles itself, no csum launch) up to kScanOneChunk tiles
+// per table: the per-table sort's tables (C1: 50 tiles) keep one launch of T workgroups.
+constexpr int kScanOneChunk = 64;
+inline void plan_scan_chunks(TiledPass& a) {
+  a.JC = (a.J + kMaxScanChunks - 1) / kMaxScanChunks;
+  if (a.JC < kScanChunk) a.JC = kScanChunk;
+  if (a.J <= kScanOneChunk) a.JC = a.J > 0 ? a.J : 1;
+  a.C = (a.J + a.JC - 1) / a.JC;
+}
+
+template <int DB>
+__global__ __launch_bounds__(kTileThreads) void tbe_tiled_csum_kernel(const TiledPass a,
+                                                                      const void* off_v,
+                                                                      int off_bits) {
+  constexpr int NB = 1 << DB;
+  constexpr int DPT = NB / kTileThreads > 0 ? NB / kTileThreads : 1;  // digits per thread
+  const int t = blockIdx.x / a.C, c = blockIdx.x - (blockIdx.x / a.C) * a.C;
+  const int tid = threadIdx.x;
+  int64_t s, n;
+  const PassView v = pass_view<DB>(a, a.row_base[t + 1] - a.row_base[t]);
+  if (v.skip) return;
+  const bool fits = off_bits == 32
+                        ? tiled_range(a, static_cast<const int32_t*>(off_v), t, s, n)
+                        : tiled_range(a, static_cast<const int64_t*>(off_v), t, s, n);
+  const int d0 = tid * DPT;
+  if (!fits || d0 >= NB) return;
+  const uint32_t* h = a.hist + (int64_t)t * a.J * NB;
+  const int j0 = c * a.JC, j1 = j0 + a.JC < a.J ? j0 + a.JC : a.J;
+  constexpr int U = 32 / DPT;
+  uint32_t tot[DPT];
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) tot[q] = 0;
+  for (int jj = j0; jj < j1; jj += U) {
+    uint32_t x[U][DPT];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < DPT; ++q)
+        x[u][q] = (jj + u < j1) ? h[(int64_t)(jj + u) * NB + d0 + q] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < DPT; ++q) tot[q] += x[u][q];
+  }
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) a.csum[((int64_t)t * a.C + c) * NB + d0 + q] = tot[q];
+}
+
 template <int DB>
 __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const TiledPass a,
                                                                       const void* off_v,
@@ -343,7 +398,7 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const Tile
   constexpr int DPT = NB / kTileThreads > 0 ? NB / kTileThreads : 1;  // digits per thread
   static_assert(NB % kTileThreads == 0 || kTileThreads % NB == 0, "digit map");
   __shared__ uint32_t wsum[kTileWaves];
-  const int t = blockIdx.x;
+  const int t = blockIdx.x / a.C, c = blockIdx.x - (blockIdx.x / a.C) * a.C;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   int64_t s, n;
   const PassView v = pass_view<DB>(a, a.row_base[t + 1] - a.row_base[t]);
@@ -352,7 +407,7 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const Tile
                         ? tiled_range(a, static_cast<const int32_t*>(off_v), t, s, n)
                         : tiled_range(a, static_cast<const int64_t*>(off_v), t, s, n);
   if (!fits) {
-    if (v.last)  // the table's range holds sentinels (no update)
+    if (v.last && c == 0)  // the table's range holds sentinels (no update)
       for (int64_t i = tid; i < n; i += kTileThreads) {
         v.kout[s + i] = a.sentinel;
         v.pout[s + i] = (int32_t)(s + i);
@@ -360,27 +415,45 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const Tile
     return;
   }
   uint32_t* h = a.hist + (int64_t)t * a.J * NB;
-  const int J = a.J;
+  const int j0 = c * a.JC, j1 = j0 + a.JC < a.J ? j0 + a.JC : a.J;
   constexpr int U = 32 / DPT;
   // digits d0 .. d0+DPT-1 of this thread (NB < threads: the first NB threads only)
   const int d0 = tid * DPT;
   const bool active = d0 < NB;
-  uint32_t tot[DPT];
+  uint32_t tot[DPT], pre[DPT];
 #pragma unroll
-  for (int q = 0; q < DPT; ++q) tot[q] = 0;
-  if (active)
-    for (int j0 = 0; j0 < J; j0 += U) {
-      uint32_t v[U][DPT];
+  for (int q = 0; q < DPT; ++q) tot[q] = pre[q] = 0;
+  if (active && a.C == 1) {  // one chunk: the digit totals straight from the tiles
+    for (int jj = j0; jj < j1; jj += U) {
+      uint32_t x[U][DPT];
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int q = 0; q < DPT; ++q)
-          v[u][q] = (j0 + u < J) ? h[(int64_t)(j0 + u) * NB + d0 + q] : 0u;
+          x[u][q] = (jj + u < j1) ? h[(int64_t)(jj + u) * NB + d0 + q] : 0u;
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int q = 0; q < DPT; ++q) tot[q] += v[u][q];
+        for (int q = 0; q < DPT; ++q) tot[q] += x[u][q];
     }
+  } else if (active) {
+    const uint32_t* cs = a.csum + (int64_t)t * a.C * NB;
+    for (int c0 = 0; c0 < a.C; c0 += U) {
+      uint32_t x[U][DPT];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < DPT; ++q)
+          x[u][q] = (c0 + u < a.C) ? cs[(int64_t)(c0 + u) * NB + d0 + q] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < DPT; ++q) {
+          tot[q] += x[u][q];
+          if (c0 + u < c) pre[q] += x[u][q];
+        }
+    }
+  }
   uint32_t tsum = 0;
 #pragma unroll
   for (int q = 0; q < DPT; ++q) tsum += tot[q];
@@ -399,23 +472,23 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const Tile
   uint32_t run[DPT];
 #pragma unroll
   for (int q = 0; q < DPT; ++q) {
-    run[q] = base;
+    run[q] = base + pre[q];
     base += tot[q];
   }
-  for (int j0 = 0; j0 < J; j0 += U) {
-    uint32_t v[U][DPT];
+  for (int jj = j0; jj < j1; jj += U) {
+    uint32_t x[U][DPT];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int q = 0; q < DPT; ++q)
-        v[u][q] = (j0 + u < J) ? h[(int64_t)(j0 + u) * NB + d0 + q] : 0u;
+        x[u][q] = (jj + u < j1) ? h[(int64_t)(jj + u) * NB + d0 + q] : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int q = 0; q < DPT; ++q)
-        if (j0 + u < J) {
-          h[(int64_t)(j0 + u) * NB + d0 + q] = run[q];
-          run[q] += v[u][q];
+        if (jj + u < j1) {
+          h[(int64_t)(jj + u) * NB + d0 + q] = run[q];
+          run[q] += x[u][q];
         }
   }
 }
@@ -546,12 +619,17 @@ void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base
   // per-table ping-pong (pass_view): each table's own last pass lands in (k_out, p_out)
   a.ka = k_a, a.pa = p_a, a.ko = k_out, a.po = p_out;
   a.npass = npass;
+  plan_scan_chunks(a);
+  a.csum = hist + (size_t)T * J * (1 << DB);  // after the per-tile counts
   for (int ps = 0; ps < npass; ++ps) {
     a.shift = ps * DB;
     a.ps = ps;
     hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(T * J), dim3(kTileThreads),
                        0, st, idx, off, a);
-    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(T), dim3(kTileThreads), 0, st, a,
+    if (a.C > 1)
+      hipLaunchKernelGGL((tbe_tiled_csum_kernel<DB>), dim3(T * a.C), dim3(kTileThreads), 0, st,
+                         a, static_cast<const void*>(off), off_bits);
+    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(T * a.C), dim3(kTileThreads), 0, st, a,
                        static_cast<const void*>(off), off_bits);
     hipLaunchKernelGGL((tbe_tiled_scatter_kernel<IdxT, OffT, DB>), dim3(T * J),
                        dim3(kScatThreads), 0, st, idx, off, a);
@@ -576,6 +654,8 @@ bool launch_global_sort(const IdxT* idx, const OffT* off, const int64_t* row_bas
   a.J = (int)dlrm::ceil_div(N, (int64_t)kTile);
   a.global = 1;
   a.n_all = N;
+  plan_scan_chunks(a);
+  a.csum = hist + (size_t)a.J * (1 << DB);
   for (int ps = 0; ps < npass; ++ps) {
     const bool fwd = (ps & 1) == 0;  // x -> y on even passes
     a.shift = ps * DB;
@@ -587,7 +667,10 @@ bool launch_global_sort(const IdxT* idx, const OffT* off, const int64_t* row_bas
     a.pout = fwd ? p_y : p_x;
     hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(a.J), dim3(kTileThreads), 0,
                        st, idx, off, a);
-    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(1), dim3(kTileThreads), 0, st, a,
+    if (a.C > 1)
+      hipLaunchKernelGGL((tbe_tiled_csum_kernel<DB>), dim3(a.C), dim3(kTileThreads), 0, st, a,
+                         static_cast<const void*>(off), (int)sizeof(OffT) * 8);
+    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(a.C), dim3(kTileThreads), 0, st, a,
                        static_cast<const void*>(off), (int)sizeof(OffT) * 8);
     hipLaunchKernelGGL((tbe_tiled_scatter_kernel<IdxT, OffT, DB>), dim3(a.J), dim3(kScatThreads),
                        0, st, idx, off, a);
@@ -603,6 +686,7 @@ struct BwdWs {
   int32_t* pos_out;
   int32_t* bag_of;
   float* partial;  // block partials; the sorts' digit histograms before the block kernel
+  size_t partial_words;
   size_t total;
 };
 
@@ -617,8 +701,10 @@ BwdWs<KeyT> carve_bwd_ws(void* base, int64_t N, int64_t D, int end_bit) {
   w.bag_of = c.take<int32_t>(N);
   (void)end_bit;
   const size_t part = (size_t)2 * ((N + CH - 1) / CH) * D;
-  const size_t hist = (size_t)((N + kTile - 1) / kTile) * 1024;  // global sort, 10-bit digits
-  w.partial = c.take<float>(part > hist ? part : hist);
+  // global sort, 10-bit digits: per-tile counts + the scan's chunk sums
+  const size_t hist = (size_t)((N + kTile - 1) / kTile) * 1024 + (size_t)kMaxScanChunks * 1024;
+  w.partial_words = part > hist ? part : hist;
+  w.partial = c.take<float>(w.partial_words);
   w.total = c.used + 256;
   return w;
 }
@@ -646,11 +732,13 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   const int tdb = tiled_digit_bits(end_bit);  // the device-wide sort (global keys)
   // the tiled sort passes over each table's OWN key bits (pass_view): 10-bit digits never
   // need more passes than 8-bit ones there, and only the tables that need them run them
-  const int64_t part_space = (int64_t)2 * dlrm::ceil_div(N, (int64_t)CH) * D;
-  const int tdb_t = (int64_t)T * tiles_j * (1 << 10) <= part_space ? 10 : tdb;
+  const int64_t part_space = (int64_t)w.partial_words;
+  // per-tile counts + the scan's chunk sums (at most kMaxScanChunks per table)
+  const int64_t sort_words = (int64_t)T * (tiles_j + kMaxScanChunks);
+  const int tdb_t = sort_words * (1 << 10) <= part_space ? 10 : tdb;
   const bool tiled = !per_table && sizeof(KeyT) == 4 && max_seg > kSegCap &&
                      N < (int64_t)0x7fffffff && (int64_t)T * tiles_j < (int64_t)INT32_MAX &&
-                     (int64_t)T * tiles_j * (1 << tdb_t) <= part_space &&
+                     sort_words * (1 << tdb_t) <= part_space &&
                      dlrm::tuning(DLRM_TUNE_TBE_SORT) != 1;
   // the tiled and global sorts carry each lookup's bag (not its position) when no
   // per-sample weights need the position: the block kernel then reads bags in sorted order

@@ -1280,6 +1280,25 @@ def test_tbe_backward_tiled_sort_per_table_pass_counts(ops, mode):
     assert not torch.equal(res[0][0], W0.cpu())
 
 
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
+def test_tbe_backward_device_wide_sort_chunked_scan(ops, mode):
+    """The device-wide sort at the C1 lookup count (1.64 M lookups: 400 tiles, the scan in
+    25 chunks of 16 over two launches) vs the tiled per-table sort (50 tiles per table, one
+    chunk): bitwise the same update."""
+    rows, B, L, D = [100000] * 8, 2048, 100, 16
+    T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 37)
+    W0 = torch.randn(sum(rows), D, device=dev) * 0.1
+    mom0 = torch.rand(sum(rows), device=dev)
+    res = []
+    for mx in (B * L, 0):
+        W, mom = W0.clone(), mom0.clone()
+        ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8, momentum=mom,
+                         max_lookups_per_table=mx)
+        torch.cuda.synchronize()
+        res.append((W.cpu(), mom.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
 def test_tbe_backward_tiled_sort_cap_violation(ops):
     """max_lookups_per_table underestimated (tiles cover 8192 of a table's 12800 lookups):
     that table is skipped (no update) and flagged; the others are updated."""
