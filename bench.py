@@ -600,6 +600,8 @@ def main():
     ap.add_argument("--tbe-role", type=int, default=-1, help="A/B: 1 = the embedding update's "
                     "passes ride on the bottom-backward GEMM launches, 0 = own launches "
                     "(default: the trainer's)")
+    ap.add_argument("--full-last-wgrad", type=int, default=-1, help="A/B: 1 = the step's last "
+                    "wgrad reduces its K split inside its own launch (no trailing REDUCE launch)")
     ap.add_argument("--head-role", type=int, default=-1, help="A/B: 1 = the head's finalize "
                     "pass rides on the top-MLP backward's first launch, 0 = own launch")
     ap.add_argument("--sort-role", type=int, default=-1, help="A/B: 1 = the per-table sort "
@@ -663,6 +665,8 @@ def main():
         tr.bot_sched = args.bot_sched
     if args.tbe_role >= 0:
         tr.tbe_role = bool(args.tbe_role)
+    if args.full_last_wgrad >= 0:
+        tr.full_last_wgrad = bool(args.full_last_wgrad)
     if args.head_role >= 0:
         tr.head_role = bool(args.head_role)
     if args.sort_role >= 0:
@@ -867,7 +871,7 @@ def main():
                        "hip_graph": use_graph, "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
                        "tbe_role_at": list(tr.tbe_role_at), "bottom_parts": tr.bottom_parts,
                        "sort_role": tr.sort_role, "sort_role_at": tr.sort_role_at,
-                       "head_role": tr.head_role,
+                       "head_role": tr.head_role, "full_last_wgrad": tr.full_last_wgrad,
                        "tune": args.tune or None},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,
             "comm": comm,

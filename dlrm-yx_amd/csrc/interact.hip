@@ -466,6 +466,154 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArg
   }
 }
 
+// Backward v4: one wave per (sample, 32-column block of D) - D / 32 waves per sample (one
+// for D <= 32).  The wave stages its block of T (F rows x 32 columns, rows >= F zero) and
+// the sample's dR row in its own LDS, builds S = G + G^T from the pairs as v3 does,
+// computes dT_blk = S T_blk on MFMA (16 k-steps) and writes each gradient row's 32 block
+// columns straight from the accumulators (a half-wave per row: 128 contiguous bytes).  At
+// D = 128 the batch runs four times v3's waves with a quarter of its LDS each, so a
+// sample's column blocks no longer run one after another in one wave.  Same products,
+// same k order per element as v3: bitwise the same gradients.  Measured (r04_ibwd): Kaggle
+// (D 16) 8.5 -> 6.8 us, but C3 (D 128) 20.6 -> 29.8 us - each of a sample's four waves
+// rebuilds S and re-reads dR - so it is the default only for D <= 32 (one wave per sample);
+// tuning INTERACT_BWD = 3 / 4 forces v3 / v4.
+inline bool use_v4(int D) {
+  const int t = dlrm::tuning(DLRM_TUNE_INTERACT_BWD);
+  return t == 4 || (t != 3 && D <= 32);
+}
+
+template <int RPI>
+__device__ __forceinline__ const float* row_ptr_n(const FeatArgs& fa, int F, int64_t b, int i0,
+                                                  int sub) {
+  const float* p = fa.ptr[0];
+  int64_t bs = 0;
+#pragma unroll
+  for (int j = 0; j < RPI; ++j) {
+    const int f = i0 + j;
+    const float* pj = f < F ? fa.ptr[f] : fa.ptr[0];
+    const int64_t bj = f < F ? fa.bs[f] : 0;
+    if (sub == j) p = pj, bs = bj;
+  }
+  return p + b * bs;
+}
+
+template <int D, bool GATHER>
+__global__ __launch_bounds__(256) void interact_dot_bwd_v4(int B, int F, FeatArgs fa, int self,
+                                                           const float* __restrict__ gout,
+                                                           int64_t ld_g, GradArgs ga,
+                                                           int relu_x, int vec_g, GatherArgs gt) {
+  constexpr int CB = D < 32 ? D : 32;       // columns per wave
+  constexpr int NBLK = D / CB;              // waves per sample
+  constexpr int TP = CB + 4;                // T-block row pitch
+  constexpr int GP = D + 32 * 33 / 2 + 4;   // dR row: x part + <= 528 pairs
+  constexpr int C4 = CB / 4, RPI = 64 / C4, NI = 32 / RPI;
+  constexpr int NG = (GP / 4 + 63) / 64;    // float4 of the dR row per lane (vec_g)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = lane >> 5, l32 = lane & 31;
+  float* Tl = lds + wave * (32 * TP + GP);
+  float* Gl = Tl + 32 * TP;
+  const int sub = lane / C4, c = lane - sub * C4;
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  const int width = D + npairs;
+  int64_t rb_lo = 0, nrows = 0;  // gather: lane f's table bounds (once per kernel)
+  if (GATHER && lane >= 1 && lane < F) {
+    rb_lo = gt.row_base[lane - 1];
+    nrows = gt.row_base[lane] - rb_lo;
+  }
+  const int64_t nunits = (int64_t)B * NBLK;
+  for (int64_t u0 = (int64_t)blockIdx.x * 4; u0 < nunits; u0 += (int64_t)gridDim.x * 4) {
+    const int64_t u = u0 + wave;
+    const bool active = u < nunits;
+    const int64_t b = active ? u / NBLK : 0;
+    const int c0 = active ? (int)(u - (u / NBLK) * NBLK) * CB : 0;
+    {
+      // the block's rows and the dR row, all loads in flight before the first LDS write
+      const int64_t grow = GATHER ? gather_row(gt, F, B, b, lane, rb_lo, nrows, false) : 0;
+      float4 v[NI];
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        if constexpr (GATHER) {
+          const int f = q * RPI + sub;
+          const int64_t g = __shfl(grow, f < 64 ? f : 0, 64);
+          const float* src = (f >= 1 && g >= 0) ? gt.W + g * D : fa.ptr[0] + b * fa.bs[0];
+          v[q] = *reinterpret_cast<const float4*>(src + c0 + 4 * c);
+          if (f >= 1 && g < 0) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          const float* src = row_ptr_n<RPI>(fa, F, b, q * RPI, sub);
+          v[q] = *reinterpret_cast<const float4*>(src + c0 + 4 * c);
+        }
+      }
+      const float* gsrc = gout + b * ld_g;
+      const int w4 = vec_g ? width / 4 : 0;
+      float4 gv[NG];
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int q = lane + 64 * k;
+        gv[k] = q < w4 ? *reinterpret_cast<const float4*>(gsrc + 4 * q)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const int f = q * RPI + sub;
+        *reinterpret_cast<float4*>(Tl + f * TP + 4 * c) =
+            f < F ? v[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int q = lane + 64 * k;
+        if (4 * q < GP) *reinterpret_cast<float4*>(Gl + 4 * q) = gv[k];
+      }
+      if (active)
+        for (int q = 4 * w4 + lane; q < width; q += 64) Gl[q] = gsrc[q];
+    }
+    __syncthreads();
+    if (active) {
+      // S row l32, columns k = 16h + s: symmetric scatter of dR's pair gradients
+      float sv[16], bv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = 16 * h + s, i = l32;
+        float x = 0.f;
+        if (i < F && k < F) {
+          if (i == k)
+            x = self ? 2.f * Gl[D + pair_index(i, i, true)] : 0.f;
+          else
+            x = Gl[D + (i > k ? pair_index(i, k, self) : pair_index(k, i, self))];
+        }
+        sv[s] = x;
+        bv[s] = l32 < CB ? Tl[(16 * h + s) * TP + l32] : 0.f;
+      }
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sv[s], bv[s], acc, 0, 0, 0);
+      if (l32 < CB) {
+        const int n = c0 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          // rows i0 (h = 0) and i0 + 4 (h = 1): row pointers picked from uniform arguments
+          const int i0 = (r & 3) + 8 * (r >> 2), i = i0 + 4 * h;
+          if (i < F) {
+            float x = acc[r];
+            if (i == 0) {
+              x += Gl[n];
+              if (relu_x && !(Tl[l32] > 0.f)) x = 0.f;
+            }
+            float* p0 = ga.ptr[i0 < kMaxF ? i0 : 0];
+            float* p1 = ga.ptr[i0 + 4 < kMaxF ? i0 + 4 : 0];
+            const int64_t s0 = ga.bs[i0 < kMaxF ? i0 : 0], s1 = ga.bs[i0 + 4 < kMaxF ? i0 + 4 : 0];
+            float* dst = h ? p1 + b * s1 : p0 + b * s0;
+            dst[n] = x;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------- generic VALU path (F > 32) --
 __global__ __launch_bounds__(256) void interact_dot_fwd_generic(int B, int F, int D, FeatArgs fa,
                                                                 int self, float* __restrict__ out,
@@ -659,6 +807,19 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
     if ((reinterpret_cast<uintptr_t>(ga.ptr[f]) & 15) || (ga.bs[f] & 3)) grads_aligned = false;
   if (fast && grads_aligned) {
     const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
+    if (use_v4(D)) {
+      const int nblk = D > 32 ? D / 32 : 1, cb = D < 32 ? D : 32;
+      const size_t lds = 4 * (32 * (size_t)(cb + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
+      const int grid = (int)std::min<int64_t>(dlrm::ceil_div((int64_t)B * nblk, 4), 8192);
+#define L4B(DD)                                                                               \
+  hipLaunchKernelGGL((interact_dot_bwd_v4<DD, false>), dim3(grid), dim3(256), lds, st, B, F, fa, \
+                     self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g,      \
+                     GatherArgs{})
+      if (D == 16) L4B(16); else if (D == 32) L4B(32); else if (D == 64) L4B(64); else L4B(128);
+#undef L4B
+      DLRM_LAUNCH_CHECK(name);
+      return DLRM_OK;
+    }
     const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
     const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
 #define L3B(DD)                                                                               \
@@ -792,9 +953,21 @@ extern "C" int dlrm_interact_dot_backward_gather(
   for (int f = 0; f < F; ++f) fa.ptr[f] = x, fa.bs[f] = x_bstride;
   const GatherArgs gt{weights, row_base, indices, nullptr};
   const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
+  hipStream_t st = dlrm::as_stream(stream);
+  if (use_v4(D)) {
+    const int nblk = D > 32 ? D / 32 : 1, cb = D < 32 ? D : 32;
+    const size_t lds4 = 4 * (32 * (size_t)(cb + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
+    const int grid4 = (int)std::min<int64_t>(dlrm::ceil_div((int64_t)B * nblk, 4), 8192);
+#define L4G(DD)                                                                               \
+  hipLaunchKernelGGL((interact_dot_bwd_v4<DD, true>), dim3(grid4), dim3(256), lds4, st, B, F, fa, \
+                     self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g, gt)
+    if (D == 16) L4G(16); else if (D == 32) L4G(32); else if (D == 64) L4G(64); else L4G(128);
+#undef L4G
+    DLRM_LAUNCH_CHECK(name);
+    return DLRM_OK;
+  }
   const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
   const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
-  hipStream_t st = dlrm::as_stream(stream);
 #define L3G(DD)                                                                               \
   hipLaunchKernelGGL((interact_dot_bwd_v3<DD, true>), dim3(grid), dim3(256), lds, st, B, F, fa,  \
                      self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g, gt)

@@ -118,13 +118,17 @@ const char* dlrm_last_error(void);
  *   DLRM_TUNE_TBE_SORT   : 1 = the device-wide radix sort even where the tiled per-table
  *                          sort applies
  *   DLRM_TUNE_TBE_LEAN   : 1 = the non-deferred backward's update passes as the
- *                          16-rows-in-flight kernels even where the lean ones apply (ABI v6) */
+ *                          16-rows-in-flight kernels even where the lean ones apply (ABI v6)
+ *   DLRM_TUNE_INTERACT_BWD : the dot-interaction backward's kernel: 3 = one wave per sample
+ *                          (v3), 4 = one wave per sample x 32-column block (v4); default v4
+ *                          for D <= 32, v3 above (ABI v6) */
 enum dlrm_tune_key {
   DLRM_TUNE_GEMM_TILE = 1,
   DLRM_TUNE_GEMM_SPLIT = 2,
   DLRM_TUNE_TBE_BLOCK = 3,
   DLRM_TUNE_TBE_SORT = 4,
-  DLRM_TUNE_TBE_LEAN = 5
+  DLRM_TUNE_TBE_LEAN = 5,
+  DLRM_TUNE_INTERACT_BWD = 6
 };
 int dlrm_set_tuning(int32_t key, int64_t value);
 int64_t dlrm_get_tuning(int32_t key);

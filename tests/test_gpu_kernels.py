@@ -875,6 +875,40 @@ def test_interact_backward_relu_x_and_paths(ops, path, D):
     assert ok, msg
 
 
+@pytest.mark.parametrize("D", [16, 32, 64, 128])
+@pytest.mark.parametrize("F,self_int", [(2, False), (9, True), (27, False), (32, False)])
+@pytest.mark.parametrize("gather", [False, True])
+def test_interact_backward_v4_matches_v3(ops, D, F, self_int, gather):
+    """The interaction backward as one wave per sample x 32-column block (v4, forced by
+    DLRM_TUNE_INTERACT_BWD = 4; the default for D <= 32) vs one wave per sample (v3, forced
+    by 3; the default above) and the default pick: bitwise the same gradients -
+    every element is the same 32-deep MFMA sum - pooled and gather-fused, ReLU' of x fused,
+    a ragged batch (B = 203) and strided x."""
+    torch.manual_seed(D * 10 + F)
+    T, B = F - 1, 203
+    rows = [int(r) for r in torch.randint(1, 500, (T,))]
+    row_base = torch.tensor([0] + list(np.cumsum(rows)), dtype=torch.int64, device=dev)
+    W = torch.randn(int(row_base[-1]), D, device=dev)
+    idx = torch.cat([torch.randint(0, n, (B,)) for n in rows]).to(torch.int32).to(dev)
+    off = torch.arange(T * B + 1, dtype=torch.int32, device=dev)
+    x = torch.randn(B, D + 4, device=dev)[:, :D]
+    E = ops.tbe_forward(W, row_base, T, B, idx, off)
+    npairs = F * (F + 1) // 2 if self_int else F * (F - 1) // 2
+    gR = torch.randn(B, D + npairs, device=dev)
+    res = []
+    for v in (4, 3, 0):
+        with ops.tuning(interact_bwd=v):
+            if gather:
+                g = ops.interact_backward_gather(x, W, row_base, idx, gR, self_int, relu_x=True)
+            else:
+                g = ops.interact_backward("dot", x, E, gR, self_int, relu_x=True)
+        torch.cuda.synchronize()
+        res.append([t.cpu().clone() for t in g])
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert torch.equal(a, b)
+
+
 def _mlp_ref(X, layers):
     """fp64 reference of the bias-folded ReLU chain (trainer layout)."""
     h = X.double()

@@ -89,6 +89,17 @@ flag)  # FLAG=--xyz: bench lines with $FLAG 0 and $FLAG 1 (CFGS)
     done
   done
   ;;
+tune)  # TUNE=key=value: bench lines without and with --tune $TUNE (CFGS)
+  for cfg in ${CFGS:-terabyte kaggle b256}; do
+    for on in 0 1; do
+      if [ "$cfg" = b256 ]; then a="--batch 256"; else a="--config $cfg"; fi
+      if [ $on = 1 ]; then t="--tune $TUNE"; else t=""; fi
+      $B $a $t --steps 300 --warmup 30 > "$OUT/tune_${cfg}_$on.json" 2> "$OUT/tune_${cfg}_$on.err" \
+        || exit $?
+      python -c "import json;d=json.load(open('$OUT/tune_${cfg}_$on.json'));print('$cfg tune=$on $TUNE',d['value'],d['ms_per_step'],d['ms_per_step_p10_p50_p90'])"
+    done
+  done
+  ;;
 trace)
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c3 ${BOT:+--bot-sched $BOT} || exit $?
   bash tools/step_trace.sh gpurun_out/${OUTNAME:-r04_perf}/trace_c2 --config kaggle ${BOT:+--bot-sched $BOT} || exit $?
