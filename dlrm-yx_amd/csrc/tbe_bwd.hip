@@ -224,6 +224,10 @@ struct TiledPass {
   // the scan in chunks of JC tiles, C per table: csum[t][c][digit] = the chunk's counts
   uint32_t* csum;
   int C, JC;
+  // wide scan (tiles per table <= kWideScanMaxJ): hist[t][j][d] becomes the count of digit
+  // d in the table's tiles before j, csum[t][0][d] the digit's total; the scatter adds the
+  // digit's start (the exclusive scan of the totals) itself
+  int wide;
 };
 
 // The pass as table t sees it (global mode: the host's ping-pong as given).
@@ -264,6 +268,7 @@ struct TiledLds {
   uint32_t cnt[(1 << DB) * (kScatWaves + 1)];  // per (digit, wave)
   uint32_t dstart[1 << DB];                     // tile-local start of each digit
   uint32_t wsum[kScatWaves];
+  uint32_t dbase[1 << DB];                      // wide scan: the digit's start in the table
   uint32_t key[kTile];                          // the tile in digit order
   int32_t pos[kTile];
 };
@@ -493,6 +498,70 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_scan_kernel(const Tile
   }
 }
 
+// Wide scan: workgroup (t, g) takes digits [64 g, 64 g + 64) of table t - a lane per digit,
+// wave w the tiles [w JW, (w + 1) JW) - and rewrites each (tile, digit) count as the digit's
+// count over the earlier tiles; the digit totals go to csum[t][0][d].  T * 2^DB / 64
+// workgroups, each one round of loads (the one-chunk scan: T workgroups walking all J
+// tiles of all digits, C1 11.3 us).
+constexpr int kWideScanMaxJ = 2048;
+template <int DB>
+__global__ __launch_bounds__(kTileThreads) void tbe_tiled_wide_scan_kernel(const TiledPass a,
+                                                                           const void* off_v,
+                                                                           int off_bits) {
+  constexpr int NB = 1 << DB, G = NB / 64;
+  __shared__ uint32_t ws[kTileWaves][64];
+  const int t = blockIdx.x / G, g = blockIdx.x - (blockIdx.x / G) * G;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  int64_t s, n;
+  const PassView v = pass_view<DB>(a, a.row_base[t + 1] - a.row_base[t]);
+  if (v.skip) return;
+  const bool fits = off_bits == 32
+                        ? tiled_range(a, static_cast<const int32_t*>(off_v), t, s, n)
+                        : tiled_range(a, static_cast<const int64_t*>(off_v), t, s, n);
+  if (!fits) {
+    if (v.last && g == 0)  // the table's range holds sentinels (no update)
+      for (int64_t i = tid; i < n; i += kTileThreads) {
+        v.kout[s + i] = a.sentinel;
+        v.pout[s + i] = (int32_t)(s + i);
+      }
+    return;
+  }
+  const int d = g * 64 + l;
+  uint32_t* h = a.hist + (int64_t)t * a.J * NB + d;
+  const int JW = (a.J + kTileWaves - 1) / kTileWaves;
+  const int j0 = w * JW, j1 = j0 + JW < a.J ? j0 + JW : a.J;
+  constexpr int U = 8;
+  uint32_t sum = 0;
+  for (int jj = j0; jj < j1; jj += U) {
+    uint32_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = jj + u < j1 ? h[(int64_t)(jj + u) * NB] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) sum += x[u];
+  }
+  ws[w][l] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kTileWaves; ++k) {
+    const uint32_t y = ws[k][l];
+    run += k < w ? y : 0u;
+    tot += y;
+  }
+  for (int jj = j0; jj < j1; jj += U) {
+    uint32_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = jj + u < j1 ? h[(int64_t)(jj + u) * NB] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (jj + u < j1) {
+        h[(int64_t)(jj + u) * NB] = run;
+        run += x[u];
+      }
+  }
+  if (w == 0) a.csum[(int64_t)t * NB + d] = tot;
+}
+
 template <typename IdxT, typename OffT, int DB>
 __global__ __launch_bounds__(kScatThreads) void tbe_tiled_scatter_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const TiledPass a) {
@@ -573,6 +642,33 @@ __global__ __launch_bounds__(kScatThreads) void tbe_tiled_scatter_kernel(
       run += tot[q];
     }
   __syncthreads();
+  if (a.wide) {  // the digits' starts in the table: exclusive scan of the digit totals
+    const uint32_t* dt = a.csum + (int64_t)t * NB;
+    uint32_t x[DPT], xs = 0;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+      x[q] = d0 + q < NB ? dt[d0 + q] : 0u;
+      xs += x[q];
+    }
+    uint32_t xi = xs;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(xi, o, 64);
+      if (l >= o) xi += y;
+    }
+    if (l == 63) sm.wsum[w] = xi;  // (the tile-local reads of wsum are behind the barrier)
+    __syncthreads();
+    uint32_t xr = xi - xs;
+#pragma unroll
+    for (int k = 0; k < kScatWaves; ++k) xr += k < w ? sm.wsum[k] : 0u;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q)
+      if (d0 + q < NB) {
+        sm.dbase[d0 + q] = xr;
+        xr += x[q];
+      }
+    __syncthreads();
+  }
   // stage the tile in digit order, then write it out: consecutive threads take
   // consecutive elements, so each digit's elements go out as one contiguous run
 #pragma unroll
@@ -591,7 +687,7 @@ __global__ __launch_bounds__(kScatThreads) void tbe_tiled_scatter_kernel(
     if (i >= nt) continue;
     const uint32_t k = sm.key[i];
     const uint32_t d = (k >> a.shift) & (NB - 1);
-    const int64_t dst = s + h[d] + (i - sm.dstart[d]);
+    const int64_t dst = s + h[d] + (a.wide ? sm.dbase[d] : 0u) + (i - sm.dstart[d]);
     if (v.last && !a.global)
       v.kout[dst] = k < (uint32_t)nrows ? (uint32_t)(rb + k) : a.sentinel;
     else
@@ -621,16 +717,21 @@ void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base
   a.npass = npass;
   plan_scan_chunks(a);
   a.csum = hist + (size_t)T * J * (1 << DB);  // after the per-tile counts
+  a.wide = J <= kWideScanMaxJ && (1 << DB) % 64 == 0 && dlrm::tuning(DLRM_TUNE_TBE_SORT) != 2;
   for (int ps = 0; ps < npass; ++ps) {
     a.shift = ps * DB;
     a.ps = ps;
     hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(T * J), dim3(kTileThreads),
                        0, st, idx, off, a);
-    if (a.C > 1)
+    if (a.wide)
+      hipLaunchKernelGGL((tbe_tiled_wide_scan_kernel<DB>), dim3(T * ((1 << DB) / 64)),
+                         dim3(kTileThreads), 0, st, a, static_cast<const void*>(off), off_bits);
+    else if (a.C > 1)
       hipLaunchKernelGGL((tbe_tiled_csum_kernel<DB>), dim3(T * a.C), dim3(kTileThreads), 0, st,
                          a, static_cast<const void*>(off), off_bits);
-    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(T * a.C), dim3(kTileThreads), 0, st, a,
-                       static_cast<const void*>(off), off_bits);
+    if (!a.wide)
+      hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(T * a.C), dim3(kTileThreads), 0, st,
+                         a, static_cast<const void*>(off), off_bits);
     hipLaunchKernelGGL((tbe_tiled_scatter_kernel<IdxT, OffT, DB>), dim3(T * J),
                        dim3(kScatThreads), 0, st, idx, off, a);
   }
@@ -656,6 +757,7 @@ bool launch_global_sort(const IdxT* idx, const OffT* off, const int64_t* row_bas
   a.n_all = N;
   plan_scan_chunks(a);
   a.csum = hist + (size_t)a.J * (1 << DB);
+  a.wide = a.J <= kWideScanMaxJ && (1 << DB) % 64 == 0 && dlrm::tuning(DLRM_TUNE_TBE_SORT) != 2;
   for (int ps = 0; ps < npass; ++ps) {
     const bool fwd = (ps & 1) == 0;  // x -> y on even passes
     a.shift = ps * DB;
@@ -667,11 +769,16 @@ bool launch_global_sort(const IdxT* idx, const OffT* off, const int64_t* row_bas
     a.pout = fwd ? p_y : p_x;
     hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(a.J), dim3(kTileThreads), 0,
                        st, idx, off, a);
-    if (a.C > 1)
+    if (a.wide)
+      hipLaunchKernelGGL((tbe_tiled_wide_scan_kernel<DB>), dim3((1 << DB) / 64),
+                         dim3(kTileThreads), 0, st, a, static_cast<const void*>(off),
+                         (int)sizeof(OffT) * 8);
+    else if (a.C > 1)
       hipLaunchKernelGGL((tbe_tiled_csum_kernel<DB>), dim3(a.C), dim3(kTileThreads), 0, st, a,
                          static_cast<const void*>(off), (int)sizeof(OffT) * 8);
-    hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(a.C), dim3(kTileThreads), 0, st, a,
-                       static_cast<const void*>(off), (int)sizeof(OffT) * 8);
+    if (!a.wide)
+      hipLaunchKernelGGL((tbe_tiled_scan_kernel<DB>), dim3(a.C), dim3(kTileThreads), 0, st, a,
+                         static_cast<const void*>(off), (int)sizeof(OffT) * 8);
     hipLaunchKernelGGL((tbe_tiled_scatter_kernel<IdxT, OffT, DB>), dim3(a.J), dim3(kScatThreads),
                        0, st, idx, off, a);
   }

@@ -116,7 +116,8 @@ const char* dlrm_last_error(void);
  *   DLRM_TUNE_GEMM_SPLIT : K splits of every FULL problem (with DLRM_TUNE_GEMM_TILE)
  *   DLRM_TUNE_TBE_BLOCK  : sorted lookups per TBE-backward block (16 or 64)
  *   DLRM_TUNE_TBE_SORT   : 1 = the device-wide radix sort even where the tiled per-table
- *                          sort applies
+ *                          sort applies; 2 = the tiled passes' digit scan as the chunked
+ *                          (csum / scan) launches instead of the wide scan (ABI v6)
  *   DLRM_TUNE_TBE_LEAN   : 1 = the non-deferred backward's update passes as the
  *                          16-rows-in-flight kernels even where the lean ones apply (ABI v6)
  *   DLRM_TUNE_INTERACT_BWD : the dot-interaction backward's kernel: 3 = one wave per sample

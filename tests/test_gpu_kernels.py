@@ -1297,17 +1297,56 @@ def test_tbe_backward_lean_passes_match_16_in_flight(ops, mode, sort, D):
 def test_tbe_backward_tiled_sort_per_table_pass_counts(ops, mode):
     """Tables needing 1, 3, 1 and 2 passes of 10-bit digits in one call (2, 21, 10 and 16
     key bits; the call's 21 global bits ask for 3): each table runs only its own passes,
-    its last one landing in the output buffers - bitwise the device-wide sort's update."""
+    its last one landing in the output buffers - with the wide digit scan (default), the
+    chunked scan (DLRM_TUNE_TBE_SORT = 2) and the device-wide sort (1): bitwise the same
+    update."""
     rows, B, L, D = [3, 2_000_000, 700, 40000], 256, 40, 16
     T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 29)
     W0 = torch.randn(sum(rows), D, device=dev) * 0.1
     mom0 = torch.rand(sum(rows), device=dev)
     res = []
-    for tiled in (True, False):
+    for sort in (0, 2, 1):
         W, mom = W0.clone(), mom0.clone()
-        with ops.tuning(tbe_sort=0 if tiled else 1):
+        with ops.tuning(tbe_sort=sort):
             ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8,
                              momentum=mom, max_lookups_per_table=B * L)
+        torch.cuda.synchronize()
+        res.append((W.cpu(), mom.cpu()))
+    for other in res[1:]:
+        assert torch.equal(res[0][0], other[0]) and torch.equal(res[0][1], other[1])
+    assert not torch.equal(res[0][0], W0.cpu())
+
+
+@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
+@pytest.mark.parametrize("case", ["c1", "invalid", "hot", "two_tiles", "global"])
+def test_tbe_backward_wide_scan_matches_chunked_scan(ops, mode, case):
+    """The tiled sort's digit scan as one wide launch (a workgroup per 64 digits, the
+    scatter adding each digit's start) vs the chunked csum / scan launches
+    (DLRM_TUNE_TBE_SORT = 2): bitwise the same update at the C1 shape (8 x 1e5 rows, L 100:
+    50 tiles per table), invalid and outside-bag lookups with a 3-pass (2^20-row) table,
+    hot rows (long runs of one digit across tiles), tables of two tiles, and the device-
+    wide sort's one segment (no per-table bound: 400 tiles)."""
+    if case in ("c1", "global"):
+        rows, B, L, D, inv = [100000] * 8, 2048, 100, 64, False
+    elif case == "invalid":
+        rows, B, L, D, inv = [3, 70000, 1 << 20, 900], 512, 37, 16, True
+    elif case == "hot":
+        rows, B, L, D, inv = [50000, 3000], 1024, 60, 32, False
+    else:
+        rows, B, L, D, inv = [4000, 9000], 64, 70, 16, False
+    T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 41, invalid=inv)
+    if case == "hot":  # most lookups on a few rows: the same digit in every tile
+        hot = (torch.rand(idx.shape, device=dev) < 0.8)
+        idx = torch.where(hot, idx % 7, idx)
+    W0 = torch.randn(sum(rows), D, device=dev) * 0.1
+    mom0 = torch.rand(sum(rows), device=dev)
+    mx = 0 if case == "global" else B * L
+    res = []
+    for sort in (0, 2):
+        W, mom = W0.clone(), mom0.clone()
+        with ops.tuning(tbe_sort=sort):
+            ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8,
+                             momentum=mom, max_lookups_per_table=mx)
         torch.cuda.synchronize()
         res.append((W.cpu(), mom.cpu()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
@@ -1339,13 +1378,15 @@ def test_tbe_backward_tiled_sort_cap_violation(ops):
     rows, B, L, D = [5000, 6000], 128, 100, 16
     T, lo, li, off, idx, row_base, G = _tbe_bwd_case(rows, B, L, D, 9)
     W0 = torch.randn(sum(rows), D, device=dev)
-    W = W0.clone()
-    flag = torch.zeros(1, dtype=torch.int32, device=dev)
-    ops.tbe_backward("sgd", W, row_base, T, B, idx, off, G, lr=0.5,
-                     max_lookups_per_table=8000, error_flag=flag)
-    torch.cuda.synchronize()
-    assert int(flag.item()) & 2  # TBE_ERR_TABLE_CAP
-    assert torch.equal(W, W0)  # both tables overflow their 2 tiles: nothing updated
+    for sort in (0, 2):  # wide / chunked digit scan
+        W = W0.clone()
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        with ops.tuning(tbe_sort=sort):
+            ops.tbe_backward("sgd", W, row_base, T, B, idx, off, G, lr=0.5,
+                             max_lookups_per_table=8000, error_flag=flag)
+        torch.cuda.synchronize()
+        assert int(flag.item()) & 2  # TBE_ERR_TABLE_CAP
+        assert torch.equal(W, W0)  # both tables overflow their 2 tiles: nothing updated
 
 
 def _c1_case(dist: str, seed: int):

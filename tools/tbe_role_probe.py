@@ -39,8 +39,12 @@ def case(T, R, D, L, B):
         ops.gemm_group([], None, dev, role=r, phase=2)
 
     tr = timeit(roles, n=10)
+    with ops.tuning(tbe_sort=2):
+        t3 = timeit(lambda: ops.tbe_backward("sgd", W, rb, T, B, idx, off, G, lr=1e-9,
+                                             workspace=ws, max_lookups_per_table=mx), n=10)
     print(f"T={T} R={R} D={D} L={L} B={B}: bwd+sgd {ts * 1e6:.1f} us (16-in-flight passes "
-          f"{t16 * 1e6:.1f} us), as roles (alone) {tr * 1e6:.1f} us", flush=True)
+          f"{t16 * 1e6:.1f} us), as roles (alone) {tr * 1e6:.1f} us, "
+          f"chunked digit scan {t3 * 1e6:.1f} us", flush=True)
 
 
 if __name__ == "__main__":
