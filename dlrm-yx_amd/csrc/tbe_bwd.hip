@@ -43,18 +43,22 @@ namespace {
 // written straight into the sorted arrays (keys / pos then point at keys_out / pos_out).
 constexpr int kBagWaves = 4;     // bags per 256-thread workgroup
 constexpr int kOutsideBlocks = 16;
+// (as a device function over 256-thread virtual blocks: the tiled sort's first launch runs
+// it beside its pass-0 digit counts, tbe_keys_hist_kernel)
 template <typename IdxT, typename OffT, typename KeyT, bool KEYS>
-__global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
-    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
-    int T, int B, int64_t N, KeyT sentinel, KeyT* __restrict__ keys, int32_t* __restrict__ pos,
-    int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
+__device__ __forceinline__ void keys_body(
+    int64_t blk, int tid, const IdxT* __restrict__ idx, const OffT* __restrict__ off,
+    const int64_t* __restrict__ row_base, int T, int B, int64_t N, KeyT sentinel,
+    KeyT* __restrict__ keys, int32_t* __restrict__ pos, int32_t* __restrict__ bag_of,
+    int32_t* __restrict__ err) {
+  constexpr int kDim = 256;
   const int64_t nb = (int64_t)T * B;
   const int64_t bag_blocks = (nb + kBagWaves - 1) / kBagWaves;
-  const int lane = threadIdx.x & 63;
-  if ((int64_t)blockIdx.x >= bag_blocks) {  // lookups outside every bag
+  const int lane = tid & 63;
+  if (blk >= bag_blocks) {  // lookups outside every bag
     const int64_t a = (int64_t)off[0], e = (int64_t)off[nb];
-    const int64_t stride = (int64_t)kOutsideBlocks * blockDim.x;
-    const int64_t g = ((int64_t)blockIdx.x - bag_blocks) * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)kOutsideBlocks * kDim;
+    const int64_t g = (blk - bag_blocks) * kDim + tid;
     auto mark = [&](int64_t p) {  // (the tiled sort keeps these: -1 reads as "no bag" too
       keys[p] = sentinel;          //  when the sorted values are bags)
       pos[p] = KEYS ? (int32_t)p : -1;
@@ -64,7 +68,7 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
     for (int64_t p = e + g; p < N; p += stride) mark(p);
     return;
   }
-  const int64_t bag = (int64_t)blockIdx.x * kBagWaves + (threadIdx.x >> 6);
+  const int64_t bag = blk * kBagWaves + (tid >> 6);
   if (bag >= nb) return;
   const int t = (int)(bag / B);
   const int64_t a = (int64_t)off[bag], e = (int64_t)off[bag + 1];
@@ -79,6 +83,15 @@ __global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
     }
     bag_of[p] = ok ? (int32_t)bag : -1;
   }
+}
+
+template <typename IdxT, typename OffT, typename KeyT, bool KEYS>
+__global__ __launch_bounds__(256) void tbe_bwd_keys_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const int64_t* __restrict__ row_base,
+    int T, int B, int64_t N, KeyT sentinel, KeyT* __restrict__ keys, int32_t* __restrict__ pos,
+    int32_t* __restrict__ bag_of, int32_t* __restrict__ err) {
+  keys_body<IdxT, OffT, KeyT, KEYS>(blockIdx.x, threadIdx.x, idx, off, row_base, T, B, N, sentinel,
+                                    keys, pos, bag_of, err);
 }
 
 inline int64_t keys_grid(int T, int B) {
@@ -275,7 +288,7 @@ struct TiledLds {
 
 // Element e of tile j of table t: wave-striped (e = w*64*IT + u*64 + l), position
 // s + j*kTile + e.  Loads this thread's IT (key, pos, valid).
-template <int IT, typename IdxT>
+template <int IT, typename IdxT, bool WITH_POS = true>
 __device__ __forceinline__ void tiled_load(const TiledPass& a, const PassView& v,
                                            const IdxT* __restrict__ idx, int64_t s, int64_t n,
                                            int j, int64_t nrows, uint32_t (&key)[IT],
@@ -289,10 +302,11 @@ __device__ __forceinline__ void tiled_load(const TiledPass& a, const PassView& v
     if (v.first && !a.global) {
       const int64_t r = (int64_t)idx[p];
       key[u] = (r >= 0 && r < nrows) ? (uint32_t)r : (uint32_t)nrows;
-      pos[u] = a.bag_of ? a.bag_of[p] : (int32_t)p;
+      if (WITH_POS) pos[u] = a.bag_of ? a.bag_of[p] : (int32_t)p;
     } else {
       key[u] = v.kin[p];
-      pos[u] = (v.first && a.bag_of) ? a.bag_of[p] : v.pin[p];  // (global pass 0: pin[p] = p)
+      if (WITH_POS)  // (global pass 0: pin[p] = p)
+        pos[u] = (v.first && a.bag_of) ? a.bag_of[p] : v.pin[p];
     }
   }
 }
@@ -311,11 +325,11 @@ __device__ __forceinline__ bool tiled_range(const TiledPass& a, const OffT* __re
 }
 
 template <typename IdxT, typename OffT, int DB>
-__global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
-    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const TiledPass a) {
+__device__ __forceinline__ void hist_body(const IdxT* __restrict__ idx,
+                                          const OffT* __restrict__ off, const TiledPass& a,
+                                          int blk, uint32_t* cnt) {
   constexpr int NB = 1 << DB;
-  __shared__ uint32_t cnt[NB];
-  const int t = blockIdx.x / a.J, j = blockIdx.x - (blockIdx.x / a.J) * a.J;
+  const int t = blk / a.J, j = blk - (blk / a.J) * a.J;
   int64_t s, n;
   const int64_t nrows = a.row_base[t + 1] - a.row_base[t];
   const PassView v = pass_view<DB>(a, nrows);
@@ -328,7 +342,7 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
   uint32_t key[kTileItems];
   int32_t pos[kTileItems];
   bool ok[kTileItems];
-  tiled_load<kTileItems>(a, v, idx, s, n, j, nrows, key, pos, ok);
+  tiled_load<kTileItems, IdxT, false>(a, v, idx, s, n, j, nrows, key, pos, ok);
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < kTileItems; ++u)
@@ -336,6 +350,44 @@ __global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
   __syncthreads();
   uint32_t* h = a.hist + ((int64_t)t * a.J + j) * NB;
   for (int d = threadIdx.x; d < NB; d += kTileThreads) h[d] = cnt[d];
+}
+
+template <typename IdxT, typename OffT, int DB>
+__global__ __launch_bounds__(kTileThreads) void tbe_tiled_hist_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const TiledPass a) {
+  __shared__ uint32_t cnt[1 << DB];
+  hist_body<IdxT, OffT, DB>(idx, off, a, blockIdx.x, cnt);
+}
+
+// The tiled sort's first launch: pass 0's digit counts (workgroups [0, T J): they read only
+// the indices) beside the bag-parallel keys pass (the rest, four 256-thread keys blocks per
+// workgroup: bag_of and the outside-bag sentinels, read first by pass 0's scatter).
+struct KeysArgs {
+  const int64_t* row_base;
+  int T, B;
+  int64_t N;
+  uint32_t sentinel;
+  uint32_t* keys;
+  int32_t* pos;
+  int32_t* bag_of;
+  int32_t* err;
+  int64_t blocks;  // 256-thread keys blocks (keys_grid)
+};
+
+template <typename IdxT, typename OffT, int DB>
+__global__ __launch_bounds__(kTileThreads) void tbe_keys_hist_kernel(
+    const IdxT* __restrict__ idx, const OffT* __restrict__ off, const TiledPass a,
+    const KeysArgs k) {
+  __shared__ uint32_t cnt[1 << DB];
+  const int nh = a.T * a.J;
+  if ((int)blockIdx.x < nh) {
+    hist_body<IdxT, OffT, DB>(idx, off, a, blockIdx.x, cnt);
+    return;
+  }
+  const int64_t vb = ((int64_t)blockIdx.x - nh) * (kTileThreads / 256) + (threadIdx.x >> 8);
+  if (vb < k.blocks)
+    keys_body<IdxT, OffT, uint32_t, false>(vb, threadIdx.x & 255, idx, off, k.row_base, k.T, k.B,
+                                           k.N, k.sentinel, k.keys, k.pos, k.bag_of, k.err);
 }
 
 // The exclusive scan of a table's NB * J counts in (digit, tile) order, in two launches
@@ -706,7 +758,8 @@ template <typename IdxT, typename OffT, int DB>
 void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base, int T, int B,
                        int J, int bits, uint32_t* k_a, int32_t* p_a, uint32_t* k_out,
                        int32_t* p_out, uint32_t* hist, uint32_t sentinel, int32_t* err,
-                       int off_bits, const int32_t* bag_of, hipStream_t st) {
+                       int off_bits, const int32_t* bag_of, const KeysArgs& keys,
+                       hipStream_t st) {
   const int npass = (bits + DB - 1) / DB;
   TiledPass a{};
   a.row_base = row_base, a.T = T, a.B = B, a.J = J, a.hist = hist, a.sentinel = sentinel;
@@ -718,11 +771,25 @@ void launch_tiled_sort(const IdxT* idx, const OffT* off, const int64_t* row_base
   plan_scan_chunks(a);
   a.csum = hist + (size_t)T * J * (1 << DB);  // after the per-tile counts
   a.wide = J <= kWideScanMaxJ && (1 << DB) % 64 == 0 && dlrm::tuning(DLRM_TUNE_TBE_SORT) != 2;
+  // the keys pass rides on pass 0's count launch (tuning TBE_SORT 2: its own launch first)
+  const bool merged = dlrm::tuning(DLRM_TUNE_TBE_SORT) != 2 &&
+                      (int64_t)T * J + dlrm::ceil_div(keys.blocks, (int64_t)(kTileThreads / 256)) <
+                          (int64_t)INT32_MAX;
+  if (!merged)
+    hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, uint32_t, false>), dim3(keys.blocks),
+                       dim3(256), 0, st, idx, off, keys.row_base, keys.T, keys.B, keys.N,
+                       keys.sentinel, keys.keys, keys.pos, keys.bag_of, keys.err);
   for (int ps = 0; ps < npass; ++ps) {
     a.shift = ps * DB;
     a.ps = ps;
-    hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(T * J), dim3(kTileThreads),
-                       0, st, idx, off, a);
+    if (ps == 0 && merged)
+      hipLaunchKernelGGL((tbe_keys_hist_kernel<IdxT, OffT, DB>),
+                         dim3((unsigned)(T * J + dlrm::ceil_div(keys.blocks,
+                                                                (int64_t)(kTileThreads / 256)))),
+                         dim3(kTileThreads), 0, st, idx, off, a, keys);
+    else
+      hipLaunchKernelGGL((tbe_tiled_hist_kernel<IdxT, OffT, DB>), dim3(T * J), dim3(kTileThreads),
+                         0, st, idx, off, a);
     if (a.wide)
       hipLaunchKernelGGL((tbe_tiled_wide_scan_kernel<DB>), dim3(T * ((1 << DB) / 64)),
                          dim3(kTileThreads), 0, st, a, static_cast<const void*>(off), off_bits);
@@ -859,11 +926,9 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
                        w.pos_out, w.bag_of, err);
     DLRM_LAUNCH_CHECK(name);
   } else if (tiled) {
-    hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT, false>), dim3(keys_grid(T, B)),
-                       dim3(256), 0, st, static_cast<const IdxT*>(idx),
-                       static_cast<const OffT*>(off), row_base, T, B, N, sentinel, w.keys_out,
-                       w.pos_out, w.bag_of, err);
-    DLRM_LAUNCH_CHECK(name);
+    const KeysArgs ka{row_base, T, B, N, (uint32_t)sentinel,
+                      reinterpret_cast<uint32_t*>(w.keys_out), w.pos_out, w.bag_of, err,
+                      keys_grid(T, B)};
     auto* ko = reinterpret_cast<uint32_t*>(w.keys_out);
     auto* ki = reinterpret_cast<uint32_t*>(w.keys_in);
     auto* hist = reinterpret_cast<uint32_t*>(w.partial);
@@ -871,12 +936,14 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
       launch_tiled_sort<IdxT, OffT, 10>(static_cast<const IdxT*>(idx),
                                         static_cast<const OffT*>(off), row_base, T, B,
                                         (int)tiles_j, end_bit, ki, w.pos_in, ko, w.pos_out, hist,
-                                        (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, bags, st);
+                                        (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, bags, ka,
+                                        st);
     else
       launch_tiled_sort<IdxT, OffT, 8>(static_cast<const IdxT*>(idx),
                                        static_cast<const OffT*>(off), row_base, T, B,
                                        (int)tiles_j, end_bit, ki, w.pos_in, ko, w.pos_out, hist,
-                                       (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, bags, st);
+                                       (uint32_t)sentinel, err, (int)sizeof(OffT) * 8, bags, ka,
+                                       st);
     DLRM_LAUNCH_CHECK(name);
   } else {
     hipLaunchKernelGGL((tbe_bwd_keys_kernel<IdxT, OffT, KeyT, true>), dim3(keys_grid(T, B)),
