@@ -17,7 +17,7 @@ GROUPS = [
     ("gemm", ("gemm_group_kernel", "gemm_role_kernel", "gemm_generic_kernel", "gemm_rowsum_kernel",
               "gemm_f32_", "gemm_splitk_reduce_kernel")),
     ("tbe_fwd", ("tbe_fwd_kernel", "tbe_fwd_presort_kernel", "mlp_chain_kernel")),  # + sort, bottom MLP
-    ("tbe_bwd", ("tbe_bwd_", "tbe_tiled_", "rocprim")),
+    ("tbe_bwd", ("tbe_bwd_", "tbe_tiled_", "tbe_keys_hist_", "tbe_update_pass_", "rocprim")),
     ("qr", ("qr_",)),
     ("interaction", ("interact_",)),
     ("colsum", ("colsum_",)),
