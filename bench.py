@@ -7,7 +7,11 @@ synthetic DLRM — 26 tables with the terabyte row counts hashed to 1e7 (54,063,
 dot interaction, BCE, SGD lr 1.0, global batch 2048 (strong scaling over ranks, the
 reference methodology of bench/dlrm_s_benchmark.sh), one lookup per bag (Criteo one-hot).
 
-    python bench.py [--gpus N --steps K --warmup W]      # N>1 via torch.distributed.run
+    python bench.py [--gpus N --steps K --warmup W]
+        N > 1: one process per GPU.  Launched by torch.distributed.run (the driver's form)
+        or, when WORLD_SIZE is unset, bench.py starts torch.distributed.run itself (a child
+        process, before any GPU call) and returns its exit status.
+    python bench.py --emulate-world 8 --emulate-rank 2     # one rank of the W=8 job, 1 GPU
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 """
@@ -476,24 +480,61 @@ def comm_timing(tr, Bl: int, B: int, reps: int = 20):
                     "backward and the all-reduce the embedding backward"}
 
 
-def socket0_physical_cores(limit: int):
-    """One hardware thread per physical core of CPU package 0, within this process's allowed
-    CPUs (bench/dlrm_s_benchmark.sh:20-25 binds `numactl --physcpubind=<socket 0 physical
-    cores> -m 0`), at most ``limit`` of them (the GPU box's CPU share per GPU is 16)."""
-    allowed = sorted(os.sched_getaffinity(0))
-    seen, cores = set(), []
-    for cpu in allowed:
+def launch_ranks(n: int) -> int:
+    """bench.py --gpus N without torch.distributed.run's environment: start
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>` as a child
+    process (the driver's own launch form, rendezvous on 127.0.0.1), wait for it and return
+    its exit status.  Rank 0 of the child job prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
+def physical_cores():
+    """{package: [one hardware thread per physical core]} within this process's allowed
+    CPUs."""
+    seen, out = set(), {}
+    for cpu in sorted(os.sched_getaffinity(0)):
         base = f"/sys/devices/system/cpu/cpu{cpu}/topology"
         try:
             pkg = int(open(f"{base}/physical_package_id").read())
             core = int(open(f"{base}/core_id").read())
         except OSError:
             pkg, core = 0, cpu
-        if pkg != 0 or core in seen:
+        if (pkg, core) in seen:
             continue
-        seen.add(core)
-        cores.append(cpu)
-    return cores[:limit] if cores else allowed[:limit]
+        seen.add((pkg, core))
+        out.setdefault(pkg, []).append(cpu)
+    return out
+
+
+def socket0_physical_cores(limit: int):
+    """One hardware thread per physical core of CPU package 0, within this process's allowed
+    CPUs (bench/dlrm_s_benchmark.sh:20-25 binds `numactl --physcpubind=<socket 0 physical
+    cores> -m 0`), at most ``limit`` of them (the GPU box's CPU share per GPU is 16)."""
+    pc = physical_cores()
+    cores = pc.get(0) or next(iter(pc.values()), [])
+    return cores[:limit] if cores else sorted(os.sched_getaffinity(0))[:limit]
+
+
+def all_socket_cores(limit: int):
+    """The all-sockets secondary figure's cores: physical cores dealt round-robin over every
+    package, at most ``limit`` (the lease's CPU share)."""
+    pc = physical_cores()
+    lists = [pc[k] for k in sorted(pc)]
+    out = []
+    for i in range(max((len(v) for v in lists), default=0)):
+        for v in lists:
+            if i < len(v):
+                out.append(v[i])
+    return out[:limit]
 
 
 def cpu_model() -> str:
@@ -506,25 +547,55 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(c, seconds: float, config_name: str, max_cores: int = 16):
-    """The CPU oracle (a restatement of the reference step, pinned to its golden vectors and
-    calibrated against the reference's own DLRM_Net step: profiles/r03_cpu_calibration.json)
-    timed on this host: a CHILD process (no GPU runtime in it: HIP/CUDA devices hidden) pinned
-    to socket 0's physical cores, one torch thread per core; memory is first-touch on the
-    pinned cores' node (numactl is not in the image).  Bounded sample of the same workload."""
+# The GPU box's CPU share per GPU (its OMP_NUM_THREADS / MAX_JOBS are set to it; nproc
+# shows the whole machine): the CPU baseline never runs more threads than this.
+LEASE_CPU_SHARE = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+
+
+def _cpu_child_run(config_name: str, seconds: float, cores):
     import subprocess
-    cores = socket0_physical_cores(max_cores)
     env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
                ROCR_VISIBLE_DEVICES="", OMP_NUM_THREADS=str(len(cores)))
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", "--config", config_name,
            "--cpu-seconds", str(seconds), "--cpu-cores", ",".join(map(str, cores))]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=seconds * 4 + 240)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not line:
+        return {"error": f"cpu child rc={r.returncode}: {r.stderr[-400:]}"}
+    return json.loads(line[-1])
+
+
+def cpu_baseline(c, seconds: float, config_name: str, max_cores: int = 0):
+    """The CPU oracle (a restatement of the reference step, pinned to its golden vectors and
+    calibrated against the reference's own DLRM_Net step: profiles/r03_cpu_calibration.json)
+    timed on this host: a CHILD process (no GPU runtime in it: HIP/CUDA devices hidden) pinned
+    to socket 0's physical cores, one torch thread per core; memory is first-touch on the
+    pinned cores' node (numactl is not in the image).  Bounded sample of the same workload.
+    The methodology of bench/dlrm_s_benchmark.sh:20-25 binds ALL of socket 0's physical
+    cores; the lease gives this job LEASE_CPU_SHARE of them, which caps the thread count
+    (recorded with the affinity mask).  Secondary figure: the same number
+    of cores dealt over every socket."""
+    max_cores = max_cores or LEASE_CPU_SHARE
     try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True,
-                           timeout=seconds * 4 + 240)
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-        if r.returncode != 0 or not line:
-            return {"error": f"cpu child rc={r.returncode}: {r.stderr[-400:]}"}
-        return json.loads(line[-1])
+        cores = socket0_physical_cores(max_cores)
+        out = _cpu_child_run(config_name, seconds, cores)
+        if "error" in out:
+            return out
+        pc = physical_cores()
+        out.update({
+            "affinity_cpus": len(os.sched_getaffinity(0)),
+            "physical_cores_per_socket": {str(k): len(v) for k, v in sorted(pc.items())},
+            "lease_cpu_share": LEASE_CPU_SHARE,
+            "binding_note": f"socket 0 has {len(pc.get(0, []))} physical cores in this "
+                            f"process's affinity mask; the lease's CPU share caps the run at "
+                            f"{max_cores} threads (one per physical core)"})
+        alls = all_socket_cores(max_cores)
+        if len(pc) > 1 and alls:
+            sec = _cpu_child_run(config_name, max(seconds / 2, 4.0), alls)
+            out["all_sockets"] = {k: sec.get(k) for k in
+                                  ("value", "cores", "cpu_list", "ms_per_step",
+                                   "ms_per_step_p10_p50_p90", "error") if k in sec}
+        return out
     except Exception as e:  # noqa: BLE001 - reported; the headline line must still print
         return {"error": repr(e)}
 
@@ -565,15 +636,22 @@ def cpu_child(c, seconds: float, cores):
     for i in range(2):
         m.train_step(*batches[i % 4], c["lr"] * 0.01)
     n, t0 = 0, time.perf_counter()
+    times = []
     while True:
+        t1 = time.perf_counter()
         m.train_step(*batches[n % 4], c["lr"] * 0.01)
+        times.append(time.perf_counter() - t1)
         n += 1
         el = time.perf_counter() - t0
         if (el >= seconds and n >= 3) or n >= 2000:
             break
     capped = sum(1 for r in c["rows"] if r > cap)
+    times.sort()
+    q = lambda f: 1000.0 * times[min(len(times) - 1, int(f * len(times)))]  # noqa: E731
     print(json.dumps({
         "value": B * n / el, "unit": "samples/s", "cores": len(cores), "kind": "port",
+        "median_value": B / (q(0.5) / 1000.0),
+        "ms_per_step_p10_p50_p90": [round(q(0.1), 3), round(q(0.5), 3), round(q(0.9), 3)],
         "cpu_model": cpu_model(), "cpu_list": cores,
         "binding": "socket 0, one thread per physical core (os.sched_setaffinity; first-touch "
                    "memory on that node), torch threads = cores",
@@ -617,6 +695,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--emulate-world", type=int, default=0, help="one GPU runs rank "
+                    "--emulate-rank of a W-rank job: its tables over the global batch, the "
+                    "B/W dense batch, collectives replaced by same-size device copies "
+                    "(trainer.EmulatedComm); a builder's projection, not a multi-GPU figure")
+    ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-cores", default="", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -625,13 +709,26 @@ def main():
                   [int(v) for v in args.cpu_cores.split(",") if v])
         return
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not started by torch.distributed.run: start it as a CHILD process (nothing here
+        # has touched the GPU; never exec) and return its exit status
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("error: --gpus N>1 must be launched with torch.distributed.run", file=sys.stderr)
-            sys.exit(2)
+        print(f"error: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if args.launch_probe:  # launcher test: report the rank environment, touch no GPU
+        print(json.dumps({"probe": True, "rank": rank, "world": world,
+                          "local_rank": local_rank,
+                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+        return
+    emulated = args.emulate_world > 1
+    if emulated and (world > 1 or not 0 <= args.emulate_rank < args.emulate_world):
+        print("error: --emulate-world runs alone, with 0 <= --emulate-rank < W", file=sys.stderr)
+        sys.exit(2)
+    procs = world  # processes of this job; the trainer's rank count may be emulated
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     pg = None
@@ -640,7 +737,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         pg = dist.group.WORLD
 
-    from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+    from dlrm_hip.trainer import DLRMTrainer, EmulatedComm, TrainerConfig
     tune = None
     if args.tune:
         from dlrm_hip import ops
@@ -660,7 +757,13 @@ def main():
                         qr_collisions=qr["collisions"] if qr else 4,
                         qr_operation=qr["operation"] if qr else "mult",
                         qr_threshold=qr["threshold"] if qr else 200)
-    tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, process_group=pg, seed=1)
+    if emulated:
+        world, rank = args.emulate_world, args.emulate_rank
+        tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, comm=EmulatedComm(),
+                         seed=1)
+    else:
+        tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, process_group=pg,
+                         seed=1)
     if args.bot_sched:
         tr.bot_sched = args.bot_sched
     if args.tbe_role >= 0:
@@ -676,7 +779,7 @@ def main():
     if args.bottom_parts >= 0:
         tr.bottom_parts = args.bottom_parts
     if args.tbe_role_at:
-        tr.tbe_role_at = tuple(int(v) for v in args.tbe_role_at.split(","))
+        tr.tbe_role_at = tr._check_role_at(int(v) for v in args.tbe_role_at.split(","))
     nb = 10  # the reference cycles 10 pre-generated batches (dlrm_data_pytorch.py:631)
     batches = [tr.synthetic_batch(B, c["L"], seed=100 + i) for i in range(nb)]
     torch.cuda.synchronize()
@@ -716,7 +819,7 @@ def main():
         run_step(k)
 
     def barrier():
-        if world > 1:
+        if procs > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
@@ -731,11 +834,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     per_step = sorted(evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps))
+    gpu_event_ms = evs[0].elapsed_time(evs[-1])  # the timed region on the GPU's own clock
     pct = {q: round(per_step[min(len(per_step) - 1, int(q / 100 * len(per_step)))], 4)
            for q in (10, 50, 90)}
     barrier()
     el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if procs > 1:
         torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(el_t.item())
     value = B * args.steps / elapsed
@@ -845,22 +949,23 @@ def main():
         skew = skew_rate(tr, c, B, uniform_ms=elapsed / args.steps * 1000.0)
 
     comm = None
-    if world > 1:
+    if procs > 1:
         try:
             comm = comm_timing(tr, B // world, B)
         except Exception as e:  # noqa: BLE001 - reported; the headline line must still print
             comm = {"error": repr(e)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not emulated and not args.no_cpu_baseline:
         cpu = cpu_baseline(c, args.cpu_seconds, args.config)
 
-    if rank == 0:
+    if (rank == 0 and not emulated) or (emulated and local_rank == 0):
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1000.0, 4),
             "ms_per_step_p10_p50_p90": [pct[10], pct[50], pct[90]],
+            "gpu_event_ms_timed_region": round(gpu_event_ms, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (device-generated, reference distributions; random init)",
             "config": {"workload": c["workload"], "global_batch": B, "local_batch": Bl,
@@ -888,8 +993,17 @@ def main():
         }
         if cpu and "value" in cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        if emulated:
+            line["emulated"] = {
+                "world": world, "rank": rank, "local_batch": Bl,
+                "tables_this_rank": tr.T_local, "tables_per_rank": tr.tables_per_rank,
+                "what": "one GPU runs this rank's kernels at the W-rank shapes; the "
+                        "all-to-all is a same-size device copy and the all-reduce a no-op "
+                        "(trainer.EmulatedComm): the rank's compute schedule, not the "
+                        "fabric; value = global batch / this rank's step time",
+                "note": "builder-run projection; never a multi-GPU measurement"}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if procs > 1:
         torch.distributed.destroy_process_group()
 
 

@@ -923,6 +923,15 @@ void plan_launch(int n, const Desc* d, Tile& t, Plan* pl) {
   if (t.bm == 128 && t.bn == 128) t = Tile{64, 32, 2, 2};
 }
 
+// Split-K tickets (tiles of in-launch split problems) a launch on tile t needs.
+int64_t split_tiles(int n, const Desc* d, const Tile& t, const Plan* pl) {
+  int64_t tick = 0;
+  for (int i = 0; i < n; ++i)
+    if (pl[i].splits > 1 && d[i].mode == DLRM_GEMM_FULL)
+      tick += dlrm::ceil_div(d[i].M, t.bm) * dlrm::ceil_div(d[i].N, t.bn);
+  return tick;
+}
+
 // Split-K workspace: the fixed 64 KiB ticket head, then each problem's records.
 size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
   const int bm = t.bm, bn = t.bn;
@@ -1126,7 +1135,16 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st,
   plan_launch(m, q, t, pl);
   // a launch carrying an update pass runs 64x32 or 32x64 tiles (gemm_role_kernel; the tile
   // shape does not change any result, ws_for sizes the workspace for 64x32 too)
-  if (role && !(t == Tile{64, 32, 2, 2}) && !(t == Tile{32, 64, 2, 2})) t = Tile{64, 32, 2, 2};
+  if (role && !(t == Tile{64, 32, 2, 2}) && !(t == Tile{32, 64, 2, 2})) {
+    if (split_tiles(m, q, Tile{64, 32, 2, 2}, pl) > kTicketCap) {
+      // the smaller tile would need more split-K tickets than the workspace head holds:
+      // the role's pass runs as its own launch, then the group on its planned tile
+      const int rc = launch_group<64, 32>(0, q, pl, ws, ws_bytes, role, phase, st);
+      if (rc != DLRM_OK) return rc;
+      return run(m, q, ws, ws_bytes, st);
+    }
+    t = Tile{64, 32, 2, 2};
+  }
   const size_t need = group_ws_bytes(m, q, t, pl);
   if (need > 0 && (!ws || ws_bytes < need)) {  // no workspace: in-launch splits off
     // (PARTIAL / REDUCE plans pair with each other across launches: kept)

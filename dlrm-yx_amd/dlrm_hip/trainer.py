@@ -90,11 +90,23 @@ class _Layer:
 
 class DLRMTrainer:
     def __init__(self, cfg: TrainerConfig, device="cuda:0", rank: int = 0, world_size: int = 1,
-                 process_group=None, seed: int = 0, init: bool = True):
+                 process_group=None, seed: int = 0, init: bool = True, comm=None,
+                 force_dist: bool = False):
+        """``comm``: the step's collectives (default: TorchComm over ``process_group``, the
+        dense all-reduce on a second group of the same ranks); EmulatedComm runs rank
+        ``rank`` of ``world_size`` alone on one GPU (bench --emulate-world).
+        ``force_dist``: the multi-GPU schedule (all-to-all, gradient bucket, all-reduce)
+        even at world_size 1, on a 1-rank group (its tests run RCCL on one GPU)."""
         self.cfg = cfg
         self.dev = torch.device(device)
         self.rank, self.world = rank, world_size
         self.pg = process_group
+        self.distributed = world_size > 1 or bool(force_dist)
+        if self.distributed and comm is None:
+            if process_group is None:
+                raise ValueError("the multi-GPU schedule needs a process group (or a comm)")
+            comm = TorchComm(process_group)
+        self.comm = comm
         D = int(cfg.m_spa)
         if int(cfg.ln_bot[-1]) != D:
             raise ValueError("trainer needs ln_bot[-1] == m_spa (the reference splits wider "
@@ -184,7 +196,7 @@ class DLRMTrainer:
         sizes = [n * _pad4(k + 1) for n, k in specs]
         self.n_params = int(sum(sizes))
         self.params = torch.zeros(self.n_params, dtype=torch.float32, device=self.dev)
-        self.grads = torch.zeros_like(self.params) if (world_size > 1 or
+        self.grads = torch.zeros_like(self.params) if (self.distributed or
                                                       cfg.optimizer == "rwsadagrad") else None
         self.adagrad_sum = torch.zeros_like(self.params) if cfg.optimizer == "rwsadagrad" else None
         self.layers: List[_Layer] = []
@@ -199,6 +211,9 @@ class DLRMTrainer:
             o += n * kp
             self.layers.append(L)
         self.n_bot = len(ln_bot) - 1
+        # DDP buckets of the flat gradient (bottom layers first): the top MLP's gradients
+        # are complete after the top backward, the bottom's after the bottom backward
+        self.n_bot_params = int(sum(sizes[:self.n_bot]))
         self.bot = self.layers[:self.n_bot]
         self.top = self.layers[self.n_bot:]
         self._bufs = {}
@@ -531,7 +546,7 @@ class DLRMTrainer:
         if self.qr_active:  # pooled physical tables (quotient / remainder halves)
             bufs["P"] = torch.zeros((B, self.T_phys, D), **f32)
             bufs["dP"] = torch.zeros_like(bufs["P"])
-        if self.world > 1:
+        if self.distributed:
             bufs["recv"] = torch.zeros(self.T * Bl * D, **f32)
             bufs["drecv"] = torch.zeros_like(bufs["recv"])
         bufs["prob"] = torch.zeros(Bl, **f32)
@@ -545,7 +560,7 @@ class DLRMTrainer:
         then the embedding features in rank-major order (single GPU: table order)."""
         D = self.D
         x = bufs["dx"] if grad else bufs["bot_act"][-1][:, :D]
-        if self.world == 1:
+        if not self.distributed:
             return x, bufs["dE" if grad else "E"]
         flat = bufs["drecv" if grad else "recv"]
         feats, o = [], 0
@@ -596,7 +611,7 @@ class DLRMTrainer:
         fused_opt = self.grads is None  # single GPU SGD: updates fused into backward
         lr, elr = self.lr, self.emb_lr
         conc = self.concurrent and profile is None
-        dist = self.world > 1
+        dist = self.distributed
         c_fwd = conc and "fwd" in self.overlaps and not dist
         c_bot = conc and "bot" in self.overlaps and not dist
         st = {}  # state shared by the segments (collective handles, pending reductions)
@@ -616,6 +631,8 @@ class DLRMTrainer:
         emb_sizes = "-".join(str(int(cfg.ln_emb[t])) for t in self.local_tables)
 
         def lookup():  # embeddings (full batch, local tables)
+            if dist:
+                self._roles = []  # first segment: no pass of an aborted step carries over
             with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
                     prof("tbe_fwd"):
                 if self.T_local > 0:
@@ -637,11 +654,21 @@ class DLRMTrainer:
         def bottom_fwd():
             h = batch.X
             with record_function("module::forward_pass::bottom_mlp"):
+                if dist and profile is None:
+                    # several GPUs: the bottom MLP as one row-block chain launch (activations
+                    # in LDS between layers, mlp_rows.hpp) while the all-to-all is in flight
+                    chain = self._bottom_chain(batch, bufs, sort_wgs=0, standalone=True)
+                    if chain is not None:
+                        ops.mlp_chain_forward(chain, self.dev)
+                        return
                 for L, out in zip(self.bot, bufs["bot_act"]):
                     self._gemm([self._fwd(L, h, out)], side=c_fwd)
                     h = out
 
         def fwd_single():  # one GPU: bottom MLP || lookup
+            # first segment of the step: a launch role deferred by an aborted step (raw
+            # pointers of that step) must never ride on this step's launches
+            self._roles = []
             # gather-fused one-hot batches: the per-table sort leaves the lookup launch for
             # the first top-MLP GEMM launch (dlrm_tbe_sort_defer), so the bottom MLP has the
             # whole chip (more workgroups per row block)
@@ -685,7 +712,7 @@ class DLRMTrainer:
             if c_fwd:
                 s0.wait_stream(s1)
 
-        def middle():  # interaction, top MLP, head, top backward, interaction backward
+        def top():  # interaction, top MLP, head, top backward
             x, feats = self._features(bufs, Bl)
             with record_function("module::forward_pass::interaction"), prof("interaction_fwd"):
                 if gather:  # one-hot lookup fused: rows read straight from the tables
@@ -706,9 +733,9 @@ class DLRMTrainer:
             G = bufs["g"]
             gi = 0
             gview = G[gi][:, :last.Kp]
-            # one GPU: the head's second launch (column sums + update + mean loss) rides on
-            # the top-MLP backward's first GEMM launch (dlrm_head_step_defer)
-            head_role = self.head_role and not dist and profile is None and len(self.top) > 1
+            # the head's second launch (column sums + update or gradient + mean loss) rides
+            # on the top-MLP backward's first GEMM launch (dlrm_head_step_defer)
+            head_role = self.head_role and profile is None and len(self.top) > 1
             with record_function("## Loss Compute ##"), prof("head"):
                 r = ops.head_step(h[:, :last.Kp], last.W[0, :last.Kp], batch.target,
                                   cfg.loss_function, cfg.loss_threshold, 1.0, prob=bufs["prob"],
@@ -728,12 +755,18 @@ class DLRMTrainer:
                 inp = bufs["top_act"][li - 1] if li > 0 else bufs["R"]
                 gn = (gi + 1) % 3
                 dg = self._dgrad(L, g, inp if li > 0 else None, G[gn])
-                w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li))
+                # several GPUs: the top bucket is all-reduced right after this loop, so its
+                # last wgrad reduces its K split inside its own launch
+                w, r = self._wg(L, g, inp, fused_opt, lr, ("top", li), full=dist and li == 0)
                 if r is not None and self.group_wgrad:
                     # the split wgrad only writes partials (its update rides on the next
                     # launch's reduce job), so it may run beside the dgrad reading W
                     self._gemm([dg, w] + rq)
                     rq = [r]
+                elif not fused_opt:
+                    # the wgrad writes the gradient bucket, not W: beside the dgrad
+                    self._gemm([dg, w] + rq)
+                    rq = []
                 else:
                     # an unsplit wgrad updates W_l in its epilogue: it rides on the NEXT
                     # launch (dgrad of layer l-1 reads W_{l-1}, not W_l; its g_l buffer
@@ -741,6 +774,13 @@ class DLRMTrainer:
                     self._gemm([dg] + rq)
                     rq = [w]
                 g, gi = G[gn], gn
+            bwd.__exit__(None, None, None)
+            st.update(rq=rq, x=x, feats=feats, g=g)
+
+        def interaction_bwd():
+            x, feats, g = st.pop("x"), st.pop("feats"), st.pop("g")
+            bwd = record_function("## Backward ##")
+            bwd.__enter__()
             _, gfeats = self._features(bufs, Bl, grad=True)
             with prof("interaction_bwd"):  # + the backward of the bottom MLP's last ReLU
                 if gather:  # rows re-gathered (the embedding update comes later)
@@ -752,7 +792,10 @@ class DLRMTrainer:
                                           cfg.arch_interaction_itself, grad_x=bufs["gx"],
                                           grad_ly=gfeats, relu_x=True)
             bwd.__exit__(None, None, None)
-            st["rq"] = rq
+
+        def middle():  # interaction, top MLP, head, top backward, interaction backward
+            top()
+            interaction_bwd()
 
         def bottom_bwd_full():
             """Bottom-MLP backward with in-launch split-K wgrads (FULL, SGD fused): the
@@ -809,6 +852,9 @@ class DLRMTrainer:
                 w, r = self._wg(L, g, inp, fused_opt, lr, ("bot", li), last=li == 0)
                 if li > 0 and r is not None and self.group_wgrad:
                     self._gemm([self._dgrad(L, g, inp, bg[li % 2]), w] + rq, side=c_bot)
+                elif li > 0 and r is None and not fused_opt:
+                    # the wgrad writes the gradient bucket, not W: beside the dgrad
+                    self._gemm([self._dgrad(L, g, inp, bg[li % 2]), w] + rq, side=c_bot)
                 else:
                     if li > 0:
                         self._gemm([self._dgrad(L, g, inp, bg[li % 2])] + rq, side=c_bot)
@@ -860,9 +906,9 @@ class DLRMTrainer:
             deferred = (self.tbe_role and not c_bot and self.T_local > 0 and profile is None
                         and self.weights.dtype == torch.float32)
             if deferred:
+                a, b = self._check_role_at(self.tbe_role_at)
                 role = emb_bwd(defer=True)
                 if role is not None:  # pass p rides on bottom-backward launch tbe_role_at[p-1]
-                    a, b = self.tbe_role_at
                     self._roles = [None] * (b + 1)
                     self._roles[a], self._roles[b] = (role, 1), (role, 2)
             with side_if(c_bot, s1):
@@ -896,30 +942,60 @@ class DLRMTrainer:
             if not fused_opt:
                 segs.append(("gpu", dense_update))
             return segs + [("comm", done)]
-        # multi GPU (distributed_forward, dlrm_s_pytorch.py:686-730): the pooled-embedding
-        # all-to-all overlaps the bottom MLP; its reverse overlaps the bottom backward; the
-        # dense all-reduce overlaps the embedding backward
+        # multi GPU (distributed_forward, dlrm_s_pytorch.py:686-730; DDP :1626-1633):
+        #  * the pooled-embedding all-to-all overlaps the bottom MLP (one chain launch);
+        #  * the top MLP's gradient bucket is all-reduced as soon as the top backward is
+        #    done (DDP's per-module buckets), overlapping the interaction backward, the
+        #    bottom backward and the embedding update; the bottom bucket follows the bottom
+        #    backward.  The all-reduces run on a communicator of their own, so they never
+        #    queue the reverse all-to-all that the embedding update waits for;
+        #  * the reverse all-to-all overlaps the bottom backward.
+        def ar(bucket):
+            def start():
+                g = self.grads[self.n_bot_params:] if bucket == "top" else \
+                    self.grads[:self.n_bot_params]
+                st["ar_" + bucket] = self.comm.allreduce(g)
+            return start
+
+        def wait(key):
+            return lambda: st.pop(key).wait()
+
         return [
             ("gpu", lookup),
             ("comm", lambda: st.__setitem__("a2a", self._alltoall_fwd(bufs, Bl))),
             ("gpu", bottom_fwd),
-            ("comm", lambda: st.pop("a2a").wait()),  # All2All_Wait (extend_distributed.py:489)
-            ("gpu", middle),
+            ("comm", wait("a2a")),  # All2All_Wait (extend_distributed.py:489)
+            ("gpu", top),
+            ("comm", ar("top")),
+            ("gpu", interaction_bwd),
             ("comm", lambda: st.__setitem__("a2a", self._alltoall_bwd(bufs, Bl))),
             ("gpu", record_function("## Backward ##")(bottom_bwd)),
-            ("comm", lambda: st.__setitem__("ar", self._allreduce_dense())),
-            ("comm", lambda: st.pop("a2a").wait()),
+            ("comm", ar("bot")),
+            ("comm", wait("a2a")),
             ("gpu", record_function("## Backward ##")(emb_bwd)),
-            ("comm", lambda: st.pop("ar").wait()),
+            ("comm", wait("ar_top")),
+            ("comm", wait("ar_bot")),
             ("gpu", dense_update),
             ("comm", done),
         ]
+
+
+    @staticmethod
+    def _check_role_at(at):
+        """tbe_role_at = (a, b): the bottom-backward launches carrying the update's block
+        pass and its combine pass.  The combine pass reads what the block pass wrote, so it
+        must ride on a LATER launch: 0 <= a < b."""
+        a, b = (int(v) for v in at)
+        if not 0 <= a < b:
+            raise ValueError(f"tbe_role_at={tuple(at)}: need 0 <= a < b (the combine pass "
+                             "rides on a later launch than the block pass)")
+        return a, b
 
     def _gather_applies(self, batch: Batch) -> bool:
         """One-hot lookups gathered inside the dot interaction: one GPU, plain tables, every
         bag one index, and the lookup launch able to run its sort role alone (the per-table
         sort of dlrm_tbe_forward_presort: <= 4096 lookups per table, 32-bit row keys)."""
-        return (self.fuse_gather and batch.one_hot and self.world == 1 and not self.qr_active
+        return (self.fuse_gather and batch.one_hot and not self.distributed and not self.qr_active
                 and self.cfg.arch_interaction_op == "dot" and self.D in (16, 32, 64, 128)
                 and 1 <= self.T_local == self.T and self.T + 1 <= 32
                 and 0 < batch.max_per_table <= ops.TBE_PRESORT_SEG_CAP
@@ -1019,12 +1095,13 @@ class DLRMTrainer:
                                     **kw, **part)[0]
         return ops.gemm_problem(g[:, :L.N], inp[:, :L.Kp], trans_a=True, C=C, **kw, **part)[0]
 
-    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key, last=False):
+    def _wg(self, L: _Layer, g, inp, fused_opt, lr, key, last=False, full=False):
         """The wgrad of L as (problem, reduce job or None): split-K wgrads write partials
         into a per-layer buffer and their reduction (+ SGD) runs in the NEXT launch.  The
         last GEMM of the step (last=True) has no next launch to carry a reduce job: its
-        K split, if any, is reduced inside its own launch (FULL mode)."""
-        if last and self.full_last_wgrad:
+        K split, if any, is reduced inside its own launch (FULL mode), and so is a wgrad
+        whose result is needed right after its launch (full=True)."""
+        if full or (last and self.full_last_wgrad):
             return self._wgrad(L, g, inp, fused_opt, lr), None
         bufs = self._cur
         sp = bufs.setdefault("splits", {})
@@ -1069,10 +1146,11 @@ class DLRMTrainer:
                          workspace=self._ws_colsum(Bl, last.Kp))
 
     def _bottom_chain(self, batch: Batch, bufs, backward: bool = False,
-                      sort_wgs: Optional[int] = None):
+                      sort_wgs: Optional[int] = None, standalone: bool = False):
         """The bottom MLP as a dlrm_mlp_chain (None when unsupported; for the forward also
-        when disabled or when there are no local tables to share the lookup launch with)."""
-        if not backward and (not self.fuse_bottom or self.T_local == 0):
+        when disabled or, unless it runs as its own launch (standalone), when there are no
+        local tables to share the lookup launch with)."""
+        if not backward and (not self.fuse_bottom or (self.T_local == 0 and not standalone)):
             return None
         layers = [(L.W, out, L.Kp) for L, out in zip(self.bot, bufs["bot_act"])]
         parts = 1
@@ -1136,12 +1214,12 @@ class DLRMTrainer:
         [B/W, T_s*D] in rank order.  A rank that owns no table sends nothing (its E
         buffer is a 1-table placeholder: only the first sum(send) floats take part)."""
         send, recv = self._split_sizes(Bl)
-        return _a2a(bufs["recv"], bufs["E"].view(-1)[:sum(send)], recv, send, self.pg)
+        return self.comm.a2a(bufs["recv"], bufs["E"].view(-1)[:sum(send)], recv, send)
 
     def _alltoall_bwd(self, bufs, Bl):
         """All2All_Wait.backward (extend_distributed.py:489-508): reverse exchange."""
         send, recv = self._split_sizes(Bl)
-        return _a2a(bufs["dE"].view(-1)[:sum(send)], bufs["drecv"], send, recv, self.pg)
+        return self.comm.a2a(bufs["dE"].view(-1)[:sum(send)], bufs["drecv"], send, recv)
 
     def lookup_balance(self, B: int, L: int = 1):
         """Per-rank load of the table-wise sharding: tables, rows and lookups per step
@@ -1156,12 +1234,6 @@ class DLRMTrainer:
         return {"tables": tabs, "rows": rows, "lookups": look,
                 "lookup_max_over_mean": round(max(look) / mean, 3) if mean else None}
 
-    def _allreduce_dense(self):
-        """DDP gradient all-reduce (dlrm_s_pytorch.py:1626-1633) on the flat bucket; the
-        1/W average is folded into the update."""
-        return _allreduce(self.grads, self.pg)
-
-
 class _NullCtx:
     def __enter__(self):
         return self
@@ -1175,22 +1247,55 @@ class _Done:
         return None
 
 
-def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, pg):
-    import torch.distributed as dist
-    if out.is_cuda and dist.get_backend(pg) == "gloo":
-        # host-staged exchange (tests on a single GPU: several ranks, gloo)
-        o = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=pg)
-        out.copy_(o)
-        return _Done()
-    return dist.all_to_all_single(out, inp, out_splits, in_splits, group=pg, async_op=True)
+class TorchComm:
+    """The step's collectives on torch.distributed (backend nccl = RCCL over xGMI).  The
+    all-to-all runs on the trainer's process group; the dense all-reduce on a SECOND
+    group of the same ranks (its own communicator, so its own stream): a 9.5 MB gradient
+    all-reduce in flight never queues the reverse all-to-all the embedding update waits
+    for.  gloo groups with CUDA tensors (tests: several ranks on one GPU) stage through
+    the host, synchronously."""
+
+    def __init__(self, pg, dense_pg=None):
+        import torch.distributed as dist
+        self.pg = pg
+        if dense_pg is None:
+            dense_pg = dist.new_group(ranks=list(range(dist.get_world_size(pg))),
+                                      backend=dist.get_backend(pg))
+        self.dense_pg = dense_pg
+
+    def a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+        import torch.distributed as dist
+        if out.is_cuda and dist.get_backend(self.pg) == "gloo":
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.pg)
+            out.copy_(o)
+            return _Done()
+        return dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.pg,
+                                      async_op=True)
+
+    def allreduce(self, t: torch.Tensor):
+        import torch.distributed as dist
+        if t.is_cuda and dist.get_backend(self.dense_pg) == "gloo":
+            h = t.cpu()
+            dist.all_reduce(h, group=self.dense_pg)
+            t.copy_(h)
+            return _Done()
+        return dist.all_reduce(t, group=self.dense_pg, async_op=True)
 
 
-def _allreduce(t: torch.Tensor, pg):
-    import torch.distributed as dist
-    if t.is_cuda and dist.get_backend(pg) == "gloo":
-        h = t.cpu()
-        dist.all_reduce(h, group=pg)
-        t.copy_(h)
+class EmulatedComm:
+    """Rank r of a W-rank job on ONE GPU with no peers (bench --emulate-world): every
+    kernel of the step runs at rank r's W-rank shapes (its tables over the global batch,
+    the B/W local batch, the rank-major features).  The all-to-all becomes one device copy
+    of min(send, recv) bytes on the current stream (the rest of the receive buffer keeps
+    whatever it holds); the all-reduce does nothing.  Times the rank's own work, not the
+    fabric."""
+
+    def a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+        n = min(int(sum(out_splits)), int(sum(in_splits)))
+        if n:
+            out.view(-1)[:n].copy_(inp.reshape(-1)[:n])
         return _Done()
-    return dist.all_reduce(t, group=pg, async_op=True)
+
+    def allreduce(self, t: torch.Tensor):
+        return _Done()

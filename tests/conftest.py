@@ -44,25 +44,6 @@ def fp32_close(a, b, rtol=1e-5, atol=1e-5):
     return True, ""
 
 
-def fp32_close_relu_flips(a, b, max_bad_frac=2e-4, loose=1e-3):
-    """fp32_close for trained weights of WIDE ReLU MLPs after several steps: an activation
-    within an ulp of 0 can land on the other side of the ReLU in a different (equally valid)
-    fp32 summation order, which switches one sample's gradient through that unit on or off.
-    At most max(8, ``max_bad_frac`` of the elements) may exceed the 1e-5 bound, none by more
-    than ``loose`` * max(1, |ref|).  Used only where such flips are expected (C3 widths,
-    >= 2 steps)."""
-    import numpy as np
-    a = np.asarray(a, dtype=np.float64)
-    b = np.asarray(b, dtype=np.float64)
-    scale = np.maximum(1.0, np.abs(b))
-    err = np.abs(a - b)
-    n_bad = int((err > 1e-5 * scale).sum())
-    if n_bad > max(8, int(max_bad_frac * a.size)) or (err > loose * scale).any():
-        i = np.unravel_index(np.argmax(err / scale), a.shape)
-        return False, f"{n_bad} beyond 1e-5; worst at {i}: got {a[i]!r} ref {b[i]!r}"
-    return True, ""
-
-
 @pytest.fixture
 def golden():
     import numpy as np

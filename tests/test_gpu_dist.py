@@ -102,8 +102,8 @@ def _spawn(W, sharder, graph, fixture):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, W, port, sharder, q, graph, fixture))
-          for r in range(W)]
+    ps = [ctx.Process(target=_worker, args=(r, W, port, sharder, q, graph, fixture),
+                      daemon=True) for r in range(W)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(W))
@@ -191,19 +191,31 @@ def _c3_spec(W):
                 ln_top=[D + 27 * 26 // 2, 1024, 1024, 512, 256, 1]), alloc
 
 
-def _c3_model():
+# C4 (BASELINE configs[4]): --qr-flag --qr-collisions=4 --qr-operation=mult
+# --qr-threshold=200 --optimizer=rwsadagrad on the C3 model
+C4_QR = dict(qr_flag=True, qr_collisions=4, qr_operation="mult", qr_threshold=200)
+
+
+def _c3_model(c4=False):
     import oracle as O
     spec, _ = _c3_spec(2)
     np.random.seed(5)
-    return O.OracleDLRM(spec["m_spa"], spec["ln_emb"], spec["ln_bot"], spec["ln_top"],
-                        loss_function="bce")
+    m = O.OracleDLRM(spec["m_spa"], spec["ln_emb"], spec["ln_bot"], spec["ln_top"],
+                     loss_function="bce")
+    if c4:  # QR tables drawn from the torch RNG (tricks/qr_embedding_bag.py:152-154)
+        torch.manual_seed(5)
+        for k, n in enumerate(spec["ln_emb"]):
+            if n > C4_QR["qr_threshold"]:
+                m.emb_l[k] = O.QREmbeddingBagOracle(n, spec["m_spa"], C4_QR["qr_collisions"],
+                                                    C4_QR["qr_operation"])
+    return m
 
 
-def _c3_batches(B):
+def _c3_batches(B, count=2):
     rng = np.random.RandomState(12)
     spec, _ = _c3_spec(2)
     out = []
-    for _ in range(2):
+    for _ in range(count):
         X = torch.tensor(np.log1p(rng.rand(B, 13)).astype(np.float32))
         lS_o = torch.arange(B).repeat(len(spec["ln_emb"]), 1)
         lS_i = [torch.tensor(rng.randint(0, n, B)) for n in spec["ln_emb"]]
@@ -212,25 +224,34 @@ def _c3_batches(B):
     return out
 
 
-def _c3_worker(rank, W, port, q, B):
+def _c3_worker(rank, W, port, q, B, c4=False, lr=0.1, steps=2):
     try:
         sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd"), HERE]
         import torch.distributed as dist
+        import relu_align as RA
         from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=W)
         spec, alloc = _c3_spec(W)
-        cfg = TrainerConfig(**spec, loss_function="bce", learning_rate=0.1, allocation=alloc)
-        tr = DLRMTrainer.from_oracle(cfg, _c3_model(), device="cuda:0", rank=rank,
+        extra = dict(C4_QR, optimizer="rwsadagrad") if c4 else {}
+        cfg = TrainerConfig(**spec, loss_function="bce", learning_rate=lr, allocation=alloc,
+                            **extra)
+        tr = DLRMTrainer.from_oracle(cfg, _c3_model(c4), device="cuda:0", rank=rank,
                                      world_size=W, process_group=dist.group.WORLD)
-        res = {"Z": [], "E": [], "local": tr.local_tables}
-        for X, lS_o, lS_i, T in _c3_batches(B):
+        res = {"Z": [], "E": [], "masks": [], "local": tr.local_tables}
+        for X, lS_o, lS_i, T in _c3_batches(B, steps):
             Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
             res["Z"].append(Z.cpu().numpy())
             res["E"].append(float(E.cpu()))
+            res["masks"].append([m.numpy() for m in RA.engine_masks(tr, B // W, B)])
         tr.check_errors()
-        res["tables"] = {t: tr.table(t).cpu().numpy() for t in tr.local_tables}
+        cpu = lambda v: tuple(x.cpu().numpy() for x in v) if isinstance(v, tuple) \
+            else v.cpu().numpy()  # noqa: E731
+        res["tables"] = {t: cpu(tr.table(t)) for t in tr.local_tables}
         res["dense"] = [(w.cpu().numpy(), b.cpu().numpy()) for w, b in tr.dense_state()]
+        if c4:
+            res["mom"] = {t: cpu(tr.table_momentum(t)) for t in tr.local_tables}
+            res["sum"] = [(w.cpu().numpy(), b.cpu().numpy()) for w, b in tr.dense_adagrad_state()]
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, res))
@@ -239,51 +260,100 @@ def _c3_worker(rank, W, port, q, B):
         q.put((rank, traceback.format_exc()))
 
 
+def _c3_run_and_check(W, c4, lr, steps, B=64):
+    """Spawn W ranks of the C3 (or C4) table list; per step, the oracle's W-rank step runs
+    with its ReLUs aligned to the ranks' own decisions (tests/relu_align.py: every
+    disagreement must be an oracle pre-activation within rounding of 0); then every
+    rank's Z / loss per step and its final tables, dense weights (and for C4 the row-wise
+    momentum and the dense Adagrad sums) at the plain 1e-5 bound, no element exempt."""
+    import oracle as O
+    import relu_align as RA
+    from conftest import fp32_close
+    spec, alloc = _c3_spec(W)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_c3_worker, args=(r, W, port, q, B, c4, lr, steps),
+                      daemon=True) for r in range(W)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in range(W))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(W):
+        assert isinstance(res[r], dict), res[r]
+    ref = _c3_model(c4)
+    relus = RA.align(ref)
+    opt = O.RWSAdagradOracle(ref.parameters(), lr=lr) if c4 else None
+    for s, (X, lS_o, lS_i, T) in enumerate(_c3_batches(B, steps)):
+        for r in range(W):  # distributed_step runs rank 0's forward, then rank 1's, ...
+            RA.queue(relus, res[r]["masks"][s])
+        Zs, Es = O.distributed_step(ref, W, alloc, X, lS_o, lS_i, T, lr, optimizer=opt)
+        for r in range(W):
+            ok, msg = fp32_close(res[r]["Z"][s], Zs[r].numpy().ravel())
+            assert ok, (s, r, msg)
+            ok, msg = fp32_close(np.array([res[r]["E"][s]]), Es[r].numpy().reshape(1))
+            assert ok, (s, r, msg)
+    ok, msg, flips = RA.report(relus)
+    assert ok, msg
+    print(f"W={W} c4={c4}: {flips} explained ReLU flips")
+    lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
+    for r in range(W):
+        assert res[r]["local"] == [t for t in range(26) if alloc[t] == r]
+        for t, w in res[r]["tables"].items():
+            e = ref.emb_l[t]
+            if isinstance(w, tuple):  # QR: (quotient, remainder) tables + their momentum
+                assert hasattr(e, "weight_q"), t
+                parts = [(w[0], e.weight_q, res[r]["mom"][t][0]),
+                         (w[1], e.weight_r, res[r]["mom"][t][1])]
+            else:
+                parts = [(w, e.weight, res[r]["mom"][t] if c4 else None)]
+            for got, p, mom in parts:
+                ok, msg = fp32_close(got, p.detach().numpy())
+                assert ok, (r, t, msg)
+                if mom is not None:
+                    ok, msg = fp32_close(mom, opt.state[id(p)]["momentum"].numpy())
+                    assert ok, ("momentum", r, t, msg)
+        for i, (w, b) in enumerate(res[r]["dense"]):
+            ok, msg = fp32_close(w, lin[i].weight.detach().numpy())
+            assert ok, (r, "W", i, msg)
+            ok, msg = fp32_close(b, lin[i].bias.detach().numpy())
+            assert ok, (r, "b", i, msg)
+            if c4:
+                sw, sb = res[r]["sum"][i]
+                ok, msg = fp32_close(sw, opt.state[id(lin[i].weight)]["sum"].numpy())
+                assert ok, ("adagrad sum W", r, i, msg)
+                ok, msg = fp32_close(sb, opt.state[id(lin[i].bias)]["sum"].numpy())
+                assert ok, ("adagrad sum b", r, i, msg)
+
+
 @pytest.mark.parametrize("W", [4, 8])
 def test_c3_table_list_greedy_ranks_match_oracle(W):
     """The C3 table list (rows capped at 2000, D = 128, C3 MLP widths) placed as greedy
     places the TRUE Terabyte rows: W = 4 [2,13,7,4] tables per rank; W = 8 [1,2,6,5,2,3,5,2]
     (rank 2 owns 6, rank 0 one).  Uneven all-to-all splits, every rank's Z / loss / tables /
     dense weights vs oracle.distributed_step (itself pinned to the reference's gloo runs)."""
-    import oracle as O
-    from conftest import fp32_close
-    B = 64
-    spec, alloc = _c3_spec(W)
+    _, alloc = _c3_spec(W)
     per_rank = [alloc.count(r) for r in range(W)]
     assert per_rank == {4: [2, 13, 7, 4], 8: [1, 2, 6, 5, 2, 3, 5, 2]}[W]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_c3_worker, args=(r, W, port, q, B)) for r in range(W)]
-    for p in ps:
-        p.start()
-    res = dict(q.get(timeout=300) for _ in range(W))
-    for p in ps:
-        p.join(timeout=60)
-    for r in range(W):
-        assert isinstance(res[r], dict), res[r]
-    ref = _c3_model()
-    for s, (X, lS_o, lS_i, T) in enumerate(_c3_batches(B)):
-        Zs, Es = O.distributed_step(ref, W, alloc, X, lS_o, lS_i, T, 0.1)
-        for r in range(W):
-            ok, msg = fp32_close(res[r]["Z"][s], Zs[r].numpy().ravel())
-            assert ok, (s, r, msg)
-            ok, msg = fp32_close(np.array([res[r]["E"][s]]), Es[r].numpy().reshape(1))
-            assert ok, (s, r, msg)
-    lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
-    from conftest import fp32_close_relu_flips
-    for r in range(W):
-        assert res[r]["local"] == [t for t in range(26) if alloc[t] == r]
-        for t, w in res[r]["tables"].items():
-            ok, msg = fp32_close(w, ref.emb_l[t].weight.detach().numpy())
-            assert ok, (r, t, msg)
-        # 2.4 M dense weights after 2 steps through 1024-wide ReLU layers: rare ReLU
-        # boundary flips allowed (Z and loss above stay within 1e-5 everywhere)
-        for i, (w, b) in enumerate(res[r]["dense"]):
-            ok, msg = fp32_close_relu_flips(w, lin[i].weight.detach().numpy())
-            assert ok, (r, "W", i, msg)
-            ok, msg = fp32_close_relu_flips(b, lin[i].bias.detach().numpy())
-            assert ok, (r, "b", i, msg)
+    _c3_run_and_check(W, c4=False, lr=0.1, steps=2)
+
+
+def test_c4_terabyte_table_list_eight_ranks_match_oracle():
+    """BASELINE configs[4] at its own rank count: the Terabyte table list (rows capped at
+    2000) placed on 8 ranks by greedy over the TRUE rows, QR (mult, 4 collisions,
+    threshold 200: 18 of the 26 tables become quotient + remainder pairs on their owner
+    rank) and RWSAdagrad (row-wise momentum on the embedding rows, Adagrad on the
+    DDP-averaged dense gradient).  Three steps; per rank Z and loss, every quotient /
+    remainder / plain table and its momentum, the dense weights and their Adagrad sums vs
+    oracle.distributed_step with RWSAdagradOracle (pinned to the reference's QR gloo runs,
+    dist_qr.npz)."""
+    import oracle as O
+    spec, alloc = _c3_spec(8)
+    n_qr = sum(1 for n in spec["ln_emb"] if n > C4_QR["qr_threshold"])
+    assert n_qr == 18, n_qr
+    assert [alloc.count(r) for r in range(8)] == [1, 2, 6, 5, 2, 3, 5, 2]
+    _c3_run_and_check(8, c4=True, lr=1e-3, steps=3)
 
 
 def _qr_worker(rank, W, port, sharder, op, q, graph=False):
@@ -353,8 +423,8 @@ def test_c4_qr_rwsadagrad_ranks_match_reference_gloo_run(W, sharder, op, graph):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_qr_worker, args=(r, W, port, sharder, op, q, graph))
-          for r in range(W)]
+    ps = [ctx.Process(target=_qr_worker, args=(r, W, port, sharder, op, q, graph),
+                      daemon=True) for r in range(W)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(W))
@@ -460,7 +530,8 @@ def test_module_distributed_forward_matches_reference_gloo_run(W, sharder):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_module_worker, args=(r, W, port, sharder, q)) for r in range(W)]
+    ps = [ctx.Process(target=_module_worker, args=(r, W, port, sharder, q), daemon=True)
+          for r in range(W)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(W))
@@ -483,3 +554,99 @@ def test_module_distributed_forward_matches_reference_gloo_run(W, sharder):
         for name, w in res[r]["dense"].items():
             ok, msg = fp32_close(w, g[DF.rank_key(W, sharder, r, f"final_{name}")])
             assert ok, (r, name, msg)
+
+
+def _nccl_one_rank_worker(port, q, graph):
+    """One process: the single-GPU schedule and the multi-GPU schedule (force_dist: the
+    all-to-all, the gradient buckets and their all-reduces over a 1-rank RCCL group) from
+    the same weights on the same C3-width batches."""
+    try:
+        sys.path[:0] = [ROOT, os.path.join(ROOT, "dlrm-yx_amd"), HERE]
+        import torch.distributed as dist
+        from dlrm_hip.trainer import DLRMTrainer, TrainerConfig
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, device_id=dev)
+        spec, _ = _c3_spec(2)
+        cfg = TrainerConfig(**spec, loss_function="bce", learning_rate=0.1)
+        out = {}
+        for name, kw in (("single", {}),
+                         ("nccl", dict(force_dist=True, process_group=dist.group.WORLD))):
+            tr = DLRMTrainer.from_oracle(cfg, _c3_model(), device=dev, **kw)
+            assert tr.distributed == (name == "nccl")
+            bs = [tr.make_batch(*b) for b in _c3_batches(128, 3)]
+            res = {"Z": [], "E": []}
+            for i, b in enumerate(bs):
+                if graph and i > 0:
+                    tr.capture(b)()
+                else:
+                    tr.step(b)
+                bufs = tr._bufs[(128, 128)]
+                res["Z"].append(bufs["prob"].cpu().numpy())
+                res["E"].append(float(bufs["loss"].cpu()))
+            torch.cuda.synchronize()
+            tr.check_errors()
+            res["tables"] = tr.weights.cpu().numpy()
+            res["dense"] = tr.params.cpu().numpy()
+            if name == "nccl":
+                res["backend"] = dist.get_backend(tr.comm.pg)
+                res["dense_backend"] = dist.get_backend(tr.comm.dense_pg)
+            out[name] = res
+        dist.destroy_process_group()
+        q.put(out)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(traceback.format_exc())
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_multi_gpu_schedule_on_one_rank_rccl_matches_single_gpu(graph):
+    """The multi-GPU step (distributed_forward's schedule: lookup -> all-to-all || bottom
+    chain -> interaction -> top MLP -> top-bucket all-reduce -> interaction backward ->
+    reverse all-to-all || bottom backward -> bottom-bucket all-reduce -> embedding update ->
+    dense update) forced on a 1-rank nccl (RCCL) group, eager and with its kernel segments
+    replayed from hipGraphs around the collectives, against the single-GPU schedule from
+    the same weights: three C3-width steps, Z / loss / tables / dense weights within 1e-5.
+    This is the RCCL path the N > 1 bench runs."""
+    from conftest import fp32_close
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_one_rank_worker, args=(_free_port(), q, graph), daemon=True)
+    p.start()
+    out = q.get(timeout=300)
+    p.join(timeout=60)
+    assert isinstance(out, dict), out
+    a, b = out["single"], out["nccl"]
+    assert b["backend"] == "nccl" and b["dense_backend"] == "nccl"
+    for s in range(3):
+        ok, msg = fp32_close(b["Z"][s], a["Z"][s])
+        assert ok, (s, "Z", msg)
+        ok, msg = fp32_close([b["E"][s]], [a["E"][s]])
+        assert ok, (s, "loss", msg)
+    ok, msg = fp32_close(b["tables"], a["tables"])
+    assert ok, ("tables", msg)
+    ok, msg = fp32_close(b["dense"], a["dense"])
+    assert ok, ("dense", msg)
+
+
+def test_emulated_rank_runs_the_w8_shapes():
+    """bench --emulate-world 8 --emulate-rank 2: one GPU runs rank 2's kernels at the W = 8
+    shapes (its 6 Terabyte tables over the global batch, B/8 dense rows, rank-major
+    features; collectives stubbed by trainer.EmulatedComm), eager and graph-replayed."""
+    from dlrm_hip.trainer import DLRMTrainer, EmulatedComm, TrainerConfig
+    spec, alloc = _c3_spec(8)
+    cfg = TrainerConfig(**spec, loss_function="bce", learning_rate=0.1, allocation=alloc)
+    tr = DLRMTrainer(cfg, device="cuda:0", rank=2, world_size=8, comm=EmulatedComm(), seed=3)
+    assert tr.T_local == 6 and tr.distributed
+    bs = [tr.synthetic_batch(2048, 1, seed=i) for i in range(2)]
+    assert bs[0].X.shape[0] == 256 and bs[0].indices.numel() == 6 * 2048
+    tr.step(bs[0])
+    run = tr.capture(bs[1])
+    run()
+    run()
+    torch.cuda.synchronize()
+    tr.check_errors()
+    loss = float(tr._bufs[(256, 2048)]["loss"].item())
+    assert np.isfinite(loss)
+    assert bool(torch.isfinite(tr.params).all())
