@@ -682,10 +682,6 @@ def main():
                     "wgrad reduces its K split inside its own launch (no trailing REDUCE launch)")
     ap.add_argument("--head-role", type=int, default=-1, help="A/B: 1 = the head's finalize "
                     "pass rides on the top-MLP backward's first launch, 0 = own launch")
-    ap.add_argument("--sort-role", type=int, default=-1, help="A/B: 1 = the per-table sort "
-                    "rides on a top-MLP forward GEMM launch, 0 = in the lookup launch")
-    ap.add_argument("--sort-role-at", type=int, default=-1, help="A/B: which top-MLP forward "
-                    "GEMM launch carries the deferred sort")
     ap.add_argument("--bottom-parts", type=int, default=-1, help="A/B: workgroups per 16-row "
                     "block of the fused bottom MLP (1, 2, 4; 0 = auto)")
     ap.add_argument("--tbe-role-at", default="", help="A/B: bottom-backward launches "
@@ -772,10 +768,6 @@ def main():
         tr.full_last_wgrad = bool(args.full_last_wgrad)
     if args.head_role >= 0:
         tr.head_role = bool(args.head_role)
-    if args.sort_role >= 0:
-        tr.sort_role = bool(args.sort_role)
-    if args.sort_role_at >= 0:
-        tr.sort_role_at = args.sort_role_at
     if args.bottom_parts >= 0:
         tr.bottom_parts = args.bottom_parts
     if args.tbe_role_at:
@@ -975,7 +967,6 @@ def main():
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
                        "hip_graph": use_graph, "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
                        "tbe_role_at": list(tr.tbe_role_at), "bottom_parts": tr.bottom_parts,
-                       "sort_role": tr.sort_role, "sort_role_at": tr.sort_role_at,
                        "head_role": tr.head_role, "full_last_wgrad": tr.full_last_wgrad,
                        "tune": args.tune or None},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,

@@ -688,7 +688,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, 4) void gemm_role_kernel(const Gemm
                                                                       const LaunchRole r) {
   __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
   const int b = blockIdx.x;
-  static_assert(sizeof(RoleSortLds) <= sizeof(smem), "the sort role's LDS fits the tile's");
   if (b < r.blocks) return tbe_role_run<PHASE>(r, b, smem);
   group_body<BM, BN, WGM, WGN, 31>(g, b - r.blocks, smem);
 }
@@ -1001,8 +1000,6 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 1>), grid, block, 0, st, g, *role);
       else if (phase == 2)
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 2>), grid, block, 0, st, g, *role);
-      else if (phase == 3)
-        hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 3>), grid, block, 0, st, g, *role);
       else
         hipLaunchKernelGGL((gemm_role_kernel<BM, BN, WGM, WGN, 4>), grid, block, 0, st, g, *role);
       DLRM_LAUNCH_CHECK("dlrm_gemm_f32_group_role");
@@ -1221,10 +1218,10 @@ extern "C" int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* prob
     if (n == 0) return DLRM_OK;
     return dlrm_gemm_f32_group(n, probs, workspace, workspace_bytes, stream);
   }
-  DLRM_ARG(phase >= 1 && phase <= 4, "%s: phase must be 1..4", name);
+  DLRM_ARG(phase == 1 || phase == 2 || phase == 4, "%s: phase must be 1, 2 or 4", name);
   DLRM_ARG(role_kind_of_phase(phase) == r->kind,
-           "%s: phase %d does not match the role (1 / 2: dlrm_tbe_backward_defer, 3: "
-           "dlrm_tbe_sort_defer, 4: dlrm_head_step_defer)", name, (int)phase);
+           "%s: phase %d does not match the role (1 / 2: dlrm_tbe_backward_defer, 4: "
+           "dlrm_head_step_defer)", name, (int)phase);
   DLRM_ARG(n >= 0 && n <= kMaxGroup && (n == 0 || probs), "%s: 0..%d problems", name, kMaxGroup);
   Desc d[kMaxGroup];
   for (int i = 0; i < n; ++i) d[i] = desc_of(probs[i]);

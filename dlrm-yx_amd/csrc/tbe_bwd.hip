@@ -1188,56 +1188,6 @@ extern "C" int dlrm_tbe_backward_defer(
                       stream, name);
 }
 
-extern "C" int dlrm_tbe_sort_defer(const int64_t* row_base, int32_t T, int32_t B,
-                                   const void* indices, int32_t index_bits, const void* offsets,
-                                   int32_t offset_bits, int64_t num_lookups, int64_t total_rows,
-                                   int64_t D, int64_t max_lookups_per_table, void* workspace,
-                                   size_t workspace_bytes, int32_t* error_flag,
-                                   dlrm_launch_role* role, dlrm_stream_t stream) {
-  const char* name = "dlrm_tbe_sort_defer";
-  DLRM_ARG(role, "%s: null role", name);
-  auto* r = reinterpret_cast<LaunchRole*>(role);
-  *r = LaunchRole{};
-  r->magic = kRoleMagic;
-  const int64_t N = num_lookups;
-  const bool keys32 = (uint64_t)total_rows < 0xFFFFFFFFull;
-  if (!presort_applies(keys32 ? 4 : 8, max_lookups_per_table, N) || N == 0 ||
-      T * (int64_t)B >= INT32_MAX)
-    return DLRM_OK;  // no per-table sort: the backward sorts itself (presorted is ignored)
-  DLRM_ARG(row_base && offsets && indices && workspace, "%s: null pointer", name);
-  DLRM_ARG(T > 0 && B > 0 && D > 0 && total_rows > 0, "%s: bad sizes", name);
-  DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: index_bits must be 32|64", name);
-  DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: offset_bits must be 32|64", name);
-  BwdWs<uint32_t> w = carve_bwd_ws<uint32_t>(workspace, N, D, bit_width_u64((uint64_t)total_rows));
-  DLRM_REQUIRE(workspace_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
-               name, workspace_bytes, w.total);
-  if (max_lookups_per_table > kRoleSortCap || B >= (1 << (31 - kPosBits))) {
-    // tables too long for the 256-thread role: the 1024-thread sort, launched now
-    hipStream_t st = dlrm::as_stream(stream);
-#define SEG(I, O)                                                                              \
-  hipLaunchKernelGGL((tbe_bwd_segsort_kernel<I, O>), dim3(T + 1), dim3(kSegThreads), 0, st,    \
-                     static_cast<const I*>(indices), static_cast<const O*>(offsets), row_base, T, \
-                     B, N, (uint32_t)total_rows, reinterpret_cast<uint32_t*>(w.keys_out),       \
-                     w.pos_out, w.bag_of, error_flag)
-    if (index_bits == 32 && offset_bits == 32) SEG(int32_t, int32_t);
-    else if (index_bits == 32) SEG(int32_t, int64_t);
-    else if (offset_bits == 32) SEG(int64_t, int32_t);
-    else SEG(int64_t, int64_t);
-#undef SEG
-    DLRM_LAUNCH_CHECK(name);
-    return DLRM_OK;
-  }
-  r->idx = indices, r->off = offsets, r->row_base = row_base, r->err = error_flag;
-  r->T = T, r->B = B, r->N = N, r->ibits = index_bits, r->obits = offset_bits;
-  r->sentinel = (uint32_t)total_rows;
-  r->keys = reinterpret_cast<const uint32_t*>(w.keys_out);
-  r->pos = w.pos_out;
-  r->bag_of = w.bag_of;
-  r->blocks = (int32_t)(dlrm::ceil_div((int64_t)T + 1, (int64_t)8) * 8);
-  r->kind = kRoleSort;
-  return DLRM_OK;
-}
-
 extern "C" int32_t dlrm_role_blocks(const dlrm_launch_role* role) {
   const auto* r = reinterpret_cast<const LaunchRole*>(role);
   return r && r->magic == kRoleMagic ? r->blocks : 0;

@@ -504,13 +504,7 @@ struct LaunchRole {
   uint32_t sentinel, magic;
   int32_t B, ch, mode, lpb;
   int32_t blocks;  // workgroups of either pass; 0 = nothing deferred
-  // phase 3, the per-table sort (dlrm_tbe_sort_defer): writes keys / pos / bag_of
-  const void* idx;
-  const void* off;
-  const int64_t* row_base;
-  int32_t* err;
-  int32_t T, ibits, obits;
-  int32_t kind;  // kRoleUpdate (phases 1, 2), kRoleSort (3), kRoleHead (4)
+  int32_t kind;  // kRoleUpdate (phases 1, 2), kRoleHead (4)
   // phase 4, the head's finalize pass (dlrm_head_step_defer)
   struct {
     int64_t M, K, nblk;
@@ -523,10 +517,11 @@ struct LaunchRole {
     int32_t accumulate;
   } head;
 };
-enum { kRoleNone = 0, kRoleUpdate = 1, kRoleSort = 2, kRoleHead = 3 };
+// (phase 3, the per-table sort as a role, is gone: measured slower than the sort in the
+// lookup launch at C3, C2 and B = 256, profiles/r04_sort_role_ab.txt; ABI v7)
+enum { kRoleNone = 0, kRoleUpdate = 1, kRoleHead = 3 };
 inline int role_kind_of_phase(int phase) {
-  return phase == 1 || phase == 2 ? kRoleUpdate : phase == 3 ? kRoleSort : phase == 4 ? kRoleHead
-                                                                                       : kRoleNone;
+  return phase == 1 || phase == 2 ? kRoleUpdate : phase == 4 ? kRoleHead : kRoleNone;
 }
 
 inline bool tbe_role_fusable(int mode, int lpb, const float* psw, int64_t grad_extent) {
@@ -554,34 +549,12 @@ __device__ __forceinline__ void tbe_role_lpb(const LaunchRole& r, int blk) {
     tbe_role_pass<PHASE, LPB, MODE_ADAGRAD>(r, blk);
 }
 
-// Phase 3: the per-table sort, 256 threads x 8 items (tables of <= 2048 lookups), bags
-// packed into the positions; the LDS image goes in the co-launched kernel's smem.
-constexpr int kRoleSortThreads = 256, kRoleSortItems = 8;
-using RoleSortLds = SegLds<kRoleSortThreads, kRoleSortItems, true>;
-constexpr int kRoleSortCap = kRoleSortThreads * kRoleSortItems;
-
-template <typename IdxT, typename OffT>
-__device__ __forceinline__ void tbe_role_sort(const LaunchRole& r, int blk, void* lds) {
-  if (blk > r.T) return;  // blocks are rounded up to a multiple of 8
-  segsort_body<kRoleSortThreads, kRoleSortItems, true, IdxT, OffT>(
-      static_cast<const IdxT*>(r.idx), static_cast<const OffT*>(r.off), r.row_base, r.T, r.B, r.N,
-      r.sentinel, const_cast<uint32_t*>(r.keys), const_cast<int32_t*>(r.pos),
-      const_cast<int32_t*>(r.bag_of), r.err, blk, *static_cast<RoleSortLds*>(lds));
-}
-
 template <int PHASE>
 __device__ __forceinline__ void tbe_role_run(const LaunchRole& r, int blk, void* lds) {
   if constexpr (PHASE == 4) {
     head_finalize_body(r.head.M, r.head.K, r.head.nblk, r.head.part, r.head.w, r.head.lr,
                        r.head.dw, r.head.accumulate, r.head.row_loss, r.head.loss_out, blk,
                        r.blocks, static_cast<float*>(lds));
-    return;
-  }
-  if constexpr (PHASE == 3) {
-    if (r.ibits == 32 && r.obits == 32) tbe_role_sort<int32_t, int32_t>(r, blk, lds);
-    else if (r.ibits == 32) tbe_role_sort<int32_t, int64_t>(r, blk, lds);
-    else if (r.obits == 32) tbe_role_sort<int64_t, int32_t>(r, blk, lds);
-    else tbe_role_sort<int64_t, int64_t>(r, blk, lds);
     return;
   }
   switch (r.lpb) {

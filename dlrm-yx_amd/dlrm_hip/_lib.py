@@ -122,8 +122,6 @@ SIGNATURES = {
     "dlrm_head_step_defer": (c_int32, [c_int64, c_int64, P, c_int64, P, P, c_int32, c_float,
                                        c_float, P, P, P, P, c_int64, c_int32, P, c_int32,
                                        c_float, P, c_size_t, P, P]),
-    "dlrm_tbe_sort_defer": (c_int32, [P, c_int32, c_int32, P, c_int32, P, c_int32, c_int64,
-                                      c_int64, c_int64, c_int64, P, c_size_t, P, P, P]),
     "dlrm_gemm_f32_splits": (c_int32, [P]),
     "dlrm_gemm_f32_partial_bytes": (c_size_t, [c_int64, c_int64, c_int32]),
     "dlrm_colsum_workspace_size": (c_size_t, [c_int64, c_int64]),

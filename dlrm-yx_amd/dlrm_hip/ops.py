@@ -415,21 +415,6 @@ def tbe_backward_defer(mode: str, weights: torch.Tensor, row_base: torch.Tensor,
     return role if role_blocks(role) > 0 else None
 
 
-def tbe_sort_defer(row_base: torch.Tensor, T: int, B: int, indices: torch.Tensor,
-                   offsets: torch.Tensor, total_rows: int, D: int, workspace: torch.Tensor,
-                   max_lookups_per_table: int, error_flag: Optional[torch.Tensor] = None):
-    """This batch's per-table sort as pass 3 of a later gemm_group(..., role=, phase=3)
-    (dlrm_tbe_sort_defer); the backward then runs with presorted=True.  None: nothing to
-    carry (the sort already ran, or the backward sorts itself)."""
-    _check_cuda(row_base, indices, offsets, workspace, error_flag)
-    role = _lib.LaunchRole()
-    _lib.call("dlrm_tbe_sort_defer", _p(row_base), T, B, _p(indices), _bits(indices),
-              _p(offsets), _bits(offsets), indices.numel(), int(total_rows), int(D),
-              int(max_lookups_per_table), _p(workspace), workspace.numel(), _p(error_flag),
-              ctypes.byref(role), _stream(indices.device))
-    return role if role_blocks(role) > 0 else None
-
-
 def role_blocks(role) -> int:
     """Workgroups a deferred update pass adds to the launch carrying it (0: none)."""
     return 0 if role is None else _lib.query("dlrm_role_blocks", ctypes.byref(role))

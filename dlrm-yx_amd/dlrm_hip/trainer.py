@@ -248,13 +248,6 @@ class DLRMTrainer:
         # one GPU: the embedding update's passes as extra workgroups of the bottom-MLP
         # backward's GEMM launches (dlrm_gemm_f32_group_role); False: launches of their own
         self.tbe_role = True
-        # one GPU, gather-fused batches: the per-table sort as a role of a top-MLP forward
-        # GEMM launch instead of the lookup launch (dlrm_tbe_sort_defer; the bottom MLP then
-        # gets the whole chip).  Off: measured slower at C3, C2 and B = 256 - the sort's
-        # workgroups stretch the GEMM launch that carries them by more than the lookup
-        # launch saves (profiles/r04_sort_role_ab.txt)
-        self.sort_role = False
-        self.sort_role_at = 0  # which top-MLP forward GEMM launch carries it
         # one GPU: the head's finalize pass as a role of the top-MLP backward's first launch
         self.head_role = True
         # bottom-MLP forward workgroups per 16-row block in the lookup launch (0 = auto)
@@ -669,26 +662,8 @@ class DLRMTrainer:
             # first segment of the step: a launch role deferred by an aborted step (raw
             # pointers of that step) must never ride on this step's launches
             self._roles = []
-            # gather-fused one-hot batches: the per-table sort leaves the lookup launch for
-            # the first top-MLP GEMM launch (dlrm_tbe_sort_defer), so the bottom MLP has the
-            # whole chip (more workgroups per row block)
-            # (per-group timing passes, profile != None, keep every role in its own launch)
-            sort_role = gather and self.sort_role and not c_fwd and profile is None
-            chain = self._bottom_chain(batch, bufs, sort_wgs=0 if sort_role else None) \
-                if presort and not c_fwd else None
+            chain = self._bottom_chain(batch, bufs) if presort and not c_fwd else None
             self.bottom_fused = chain is not None
-            if chain is not None and sort_role:
-                with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
-                        record_function("module::forward_pass::bottom_mlp"), prof("tbe_fwd"):
-                    idx, off = st["csr"] = self._phys_csr(batch, B)
-                    ops.mlp_chain_forward(chain, self.dev)
-                    role = ops.tbe_sort_defer(self.row_base, self.T_phys, B, idx, off,
-                                              self.weights.shape[0], D,
-                                              self._ws_tbe(idx.numel()), batch.max_per_table,
-                                              error_flag=self.tbe_error_flag)
-                    if role is not None:  # rides on top-MLP forward launch sort_role_at
-                        self._roles = [None] * self.sort_role_at + [(role, 3)]
-                return
             if chain is not None:
                 # the bottom MLP forward runs as a role of the lookup launch
                 with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
@@ -898,11 +873,6 @@ class DLRMTrainer:
             # the embedding update's two HBM-bound passes ride as extra workgroups on the
             # first two (MFMA-bound) bottom-backward launches: overlap with no cross-queue
             # dependency (dlrm_tbe_backward_defer / dlrm_gemm_f32_group_role)
-            while self._roles:  # a deferred sort no forward launch carried
-                if self._roles[0] is None:
-                    self._roles.pop(0)
-                else:
-                    self._gemm([])
             deferred = (self.tbe_role and not c_bot and self.T_local > 0 and profile is None
                         and self.weights.dtype == torch.float32)
             if deferred:

@@ -103,7 +103,10 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  * 6: dlrm_tbe_backward_defer + dlrm_gemm_f32_group_role: the embedding backward's update
  *    passes (and dlrm_tbe_sort_defer: the per-table sort; dlrm_head_step_defer: the head's
  *    finalize pass) as extra workgroups of grouped GEMM launches (dlrm_launch_role); dlrm_mlp_chain gains parts /
- *    split_layer / tickets (several workgroups per 16-row block) (round 4). */
+ *    split_layer / tickets (several workgroups per 16-row block) (round 4).
+ * 7: dlrm_tbe_sort_defer and role phase 3 removed (the sort as a GEMM-launch role measured
+ *    slower than the sort in the lookup launch everywhere, profiles/r04_sort_role_ab.txt)
+ *    (round 5). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 
@@ -378,23 +381,6 @@ int dlrm_tbe_backward_defer(int32_t mode, float* weights, float* momentum, int64
 /* Workgroups a deferred pass adds to the launch that carries it (0: nothing deferred). */
 int32_t dlrm_role_blocks(const dlrm_launch_role* role);
 /*
- * This batch's per-table sort (what dlrm_tbe_forward_presort's sort role does), deferred
- * into a later grouped GEMM launch: *role becomes pass 3 for dlrm_gemm_f32_group_role,
- * which must run before the backward (then called with presorted = 1, same indices,
- * offsets and workspace).  Tables of <= 2048 lookups sort in 256-thread workgroups
- * (LDS-light: the launch's GEMM tiles keep their occupancy); with a per-table bound in
- * 2049..4096 the 1024-thread sort is launched here instead, and with none (or 64-bit row
- * keys) nothing happens and the backward sorts itself - role->blocks == 0 in both cases.
- * D: the embedding width (the workspace layout).  Bitwise the same sorted output as every
- * other sort path.
- */
-int dlrm_tbe_sort_defer(const int64_t* row_base, int32_t T, int32_t B, const void* indices,
-                        int32_t index_bits, const void* offsets, int32_t offset_bits,
-                        int64_t num_lookups, int64_t total_rows, int64_t D,
-                        int64_t max_lookups_per_table, void* workspace, size_t workspace_bytes,
-                        int32_t* error_flag, dlrm_launch_role* role, dlrm_stream_t stream);
-
-/*
  * Sparse-gradient values of an EmbeddingBag(sparse=True) backward
  * (torch _embedding_bag_sparse_backward as reached from dlrm_s_pytorch.py:1929):
  *   values[l][:] = w_l * grad_out[b*grad_batch_stride + t*D + :] for lookup l of bag (t,b)
@@ -588,8 +574,8 @@ size_t dlrm_gemm_f32_partial_bytes(int64_t M, int64_t N, int32_t splits);
 int dlrm_gemm_f32_group(int32_t n, const dlrm_gemm_problem* problems, void* workspace,
                         size_t workspace_bytes, dlrm_stream_t stream);
 /* dlrm_gemm_f32_group plus pass `phase` of a deferred role as extra workgroups of the same
- * launch: 1 / 2 the embedding update (dlrm_tbe_backward_defer), 3 the per-table sort
- * (dlrm_tbe_sort_defer), 4 the head's finalize pass (dlrm_head_step_defer); n may be 0
+ * launch: 1 / 2 the embedding update (dlrm_tbe_backward_defer), 4 the head's finalize pass
+ * (dlrm_head_step_defer); phase 3 (a deferred per-table sort) was removed in v7; n may be 0
  * (the pass alone).  role == NULL, or a role with nothing deferred: dlrm_gemm_f32_group.  The
  * problems must not touch the update's buffers (weights, momentum, grad_out, workspace). */
 int dlrm_gemm_f32_group_role(int32_t n, const dlrm_gemm_problem* problems, void* workspace,

@@ -442,7 +442,7 @@ class RWSAdagradOracle:
             st = self.state[id(p)]
             if "momentum" not in st and "sum" not in st:
                 if p.grad.is_sparse:
-                    st["momentum"] = torch.full([p.shape[0]], self.init, dtype=torch.float32)
+                    st["momentum"] = torch.full([p.shape[0]], self.init, dtype=p.dtype)
                 else:
                     st["sum"] = torch.full_like(p.data, self.init)
             st["step"] += 1

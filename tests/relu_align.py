@@ -57,7 +57,7 @@ class AlignedReLU(nn.Module):
             bad = diff & (z.detach().abs() > tau)
             self.flips += int(diff.sum())
             for i, j in bad.nonzero().tolist()[:4]:
-                self.unexplained.append(f"sample {i} unit {j}: z={float(z[i, j])!r} "
+                self.unexplained.append(f"sample {i} unit {j}: z={float(z.detach()[i, j])!r} "
                                         f"tau={float(tau[i, j])!r} engine={bool(mask[i, j])}")
         return torch.where(mask, z, torch.zeros_like(z))
 
@@ -104,3 +104,133 @@ def report(relus: List[AlignedReLU]):
     if bad or left:
         return False, f"{len(bad)} unexplained ReLU flips ({bad[:4]}), {left} masks unused", flips
     return True, "", flips
+
+
+# Conditioning of the result itself.  Some elements of a multi-step trajectory are
+# ill-conditioned at fp32: Adagrad's step lr * g / (sqrt(S) + eps) turns a gradient that has
+# cancelled down to its rounding noise into a full-size step of either sign, and a
+# saturated sigmoid turns a 1-ulp change of p into a different BCE gradient.  Two correct
+# fp32 implementations then legitimately differ there by more than 1e-5.  PermutedTwin
+# measures that per element: a second fp32 oracle runs the SAME steps with the samples of
+# each rank's batch in a different order (every sum over the batch - the loss mean, the
+# weight and embedding gradients - then rounds differently; mathematically nothing
+# changes), following the engine's ReLU / head decisions permuted alike.  The comparison
+# becomes
+#     |engine - oracle| <= 1e-5 max(1, |oracle|) + SPREAD * |oracle - twin|:
+# an element beyond 1e-5 is EXPLAINED only where the reference arithmetic itself moves that
+# much under a mere change of summation order; everywhere else the plain 1e-5 bound holds.
+SPREAD = 4.0
+
+
+class PermutedTwin:
+    def __init__(self, model, B: int, world: int = 1, seed: int = 1234):
+        """Build right after align(model) (deepcopy maps each AlignedReLU's Linear and the
+        forward hook bound to it onto the copies).  The permutation keeps every sample in
+        its rank's slice of the B-sample batch (W equal slices)."""
+        import copy
+        import numpy as np
+        self.model = copy.deepcopy(model)
+        self.relus = [m for seq in (self.model.bot_l, self.model.top_l) for m in seq
+                      if isinstance(m, AlignedReLU)]
+        self.head = None
+        rng = np.random.RandomState(seed)
+        bl = B // world
+        self.local = [torch.as_tensor(rng.permutation(bl)) for _ in range(world)]
+        self.perm = torch.cat([p + r * bl for r, p in enumerate(self.local)])
+
+    def with_head(self):
+        self.head = AlignedHead(self.model)
+        return self
+
+    def batch(self, X, lS_o, lS_i, T):
+        """The batch with its samples permuted (one lookup per bag: offsets unchanged)."""
+        p = self.perm
+        for o in lS_o:
+            if not torch.equal(torch.as_tensor(o).long(), torch.arange(len(p))):
+                raise ValueError("PermutedTwin: one-hot bags (offsets = arange) only")
+        return (torch.as_tensor(X)[p], lS_o, [torch.as_tensor(i)[p] for i in lS_i],
+                torch.as_tensor(T)[p])
+
+    def queue(self, masks, rank: int = 0):
+        """Queue one rank's engine ReLU masks, permuted like its samples."""
+        pl = self.local[rank]
+        queue(self.relus, [torch.as_tensor(m)[pl] for m in masks])
+
+    def push_head(self, dz, target, n: int, rank: int = 0):
+        pl = self.local[rank]
+        self.head.push(torch.as_tensor(dz).reshape(-1)[pl], torch.as_tensor(target).reshape(-1)[pl],
+                       n)
+
+    def close(self, got, ref, twin, what=""):
+        """(ok, message, n_explained) for the engine's value of an oracle quantity ``ref``
+        whose twin value is ``twin``."""
+        import numpy as np
+        a = np.asarray(got, dtype=np.float64)
+        b = torch.as_tensor(ref).detach().double().numpy()
+        c = torch.as_tensor(twin).detach().double().numpy()
+        base = 1e-5 * np.maximum(1.0, np.abs(b))
+        err = np.abs(a - b)
+        lim = base + SPREAD * np.abs(b - c)
+        n_expl = int(((err > base) & (err <= lim)).sum())
+        if (err > lim).any():
+            i = np.unravel_index(np.argmax(err - lim), a.shape)
+            return False, (f"{what} got {a[i]!r} oracle {b[i]!r} twin {c[i]!r} at {i}: beyond "
+                           f"1e-5 and beyond {SPREAD} x the oracle's own spread under a "
+                           f"permuted summation order"), n_expl
+        return True, "", n_expl
+
+
+# The sigmoid + BCE head has its own ill-conditioned points: the reference's BCE backward
+# divides by max(p (1 - p), 1e-12), and p rounds to exactly 1.0 for z > ~16.6, so a
+# sample's dLoss/dz jumps (to 0 at p == 1, by orders of magnitude inside the clamp) when
+# the last bit of its z moves.  AlignedHead treats those samples like ReLU flips: a hook on
+# the last Linear's output takes the engine's dz (trainer bufs["dz"]) for the samples whose
+# oracle dz is not stable under a +-tau change of z (tau as for the ReLUs), and requires
+# every OTHER sample's engine dz to match the oracle's within the fp32 bound.
+def _bce_dz(z, t, inv_m):
+    p = torch.sigmoid(z)
+    dp = (p - t) / torch.clamp((1 - p) * p, min=1e-12) * inv_m
+    return dp * (1 - p) * p
+
+
+class AlignedHead:
+    def __init__(self, model):
+        lins = [m for m in model.top_l if isinstance(m, nn.Linear)]
+        self.last = lins[-1]
+        self.queue = []  # (engine dz [n], target [n], 1 / n) per forward of the head
+        self.aligned = 0
+        self.unexplained: List[str] = []
+        self.last.register_forward_hook(self._hook)
+
+    def push(self, dz, target, n: int) -> None:
+        dt = self.last.weight.dtype
+        self.queue.append((torch.as_tensor(dz).reshape(-1, 1).to(dt),
+                           torch.as_tensor(target).reshape(-1, 1).to(dt), 1.0 / n))
+
+    def _hook(self, mod, inp, out):
+        if not self.queue:
+            raise RuntimeError("AlignedHead: no engine dz queued for this call")
+        dz_e, t, inv_m = self.queue.pop(0)
+        z = out.detach()
+        tau = TAU_REL * (inp[0].detach().abs() @ mod.weight.detach().abs().t()
+                         + mod.bias.detach().abs())
+        d0 = _bce_dz(z, t, inv_m)
+        dlo, dhi = _bce_dz(z - tau, t, inv_m), _bce_dz(z + tau, t, inv_m)
+        scale = torch.clamp(d0.abs(), min=inv_m)
+        unstable = ((dlo - d0).abs() > 1e-5 * scale) | ((dhi - d0).abs() > 1e-5 * scale)
+        agree = (dz_e - d0).abs() <= 1e-5 * scale
+        bad = ~unstable & ~agree
+        for i in bad.nonzero()[:, 0].tolist()[:4]:
+            self.unexplained.append(f"sample {i}: z={float(z[i, 0])!r} engine dz="
+                                    f"{float(dz_e[i, 0])!r} oracle dz={float(d0[i, 0])!r}")
+        take = unstable & ~agree
+        self.aligned += int(take.sum())
+        if out.requires_grad and bool(take.any()):
+            out.register_hook(lambda g: torch.where(take, dz_e, g))
+
+    def report(self):
+        left = len(self.queue)
+        if self.unexplained or left:
+            return False, (f"{len(self.unexplained)} unexplained head gradients "
+                           f"({self.unexplained[:4]}), {left} queued unused")
+        return True, ""

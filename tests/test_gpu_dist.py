@@ -284,11 +284,16 @@ def _c3_run_and_check(W, c4, lr, steps, B=64):
         assert isinstance(res[r], dict), res[r]
     ref = _c3_model(c4)
     relus = RA.align(ref)
+    tw = RA.PermutedTwin(ref, B, W)  # the oracle's own summation-order spread
     opt = O.RWSAdagradOracle(ref.parameters(), lr=lr) if c4 else None
+    opt2 = O.RWSAdagradOracle(tw.model.parameters(), lr=lr) if c4 else None
     for s, (X, lS_o, lS_i, T) in enumerate(_c3_batches(B, steps)):
         for r in range(W):  # distributed_step runs rank 0's forward, then rank 1's, ...
             RA.queue(relus, res[r]["masks"][s])
+            tw.queue(res[r]["masks"][s], rank=r)
         Zs, Es = O.distributed_step(ref, W, alloc, X, lS_o, lS_i, T, lr, optimizer=opt)
+        X2, o2, i2, T2 = tw.batch(X, lS_o, lS_i, T)
+        O.distributed_step(tw.model, W, alloc, X2, o2, i2, T2, lr, optimizer=opt2)
         for r in range(W):
             ok, msg = fp32_close(res[r]["Z"][s], Zs[r].numpy().ravel())
             assert ok, (s, r, msg)
@@ -296,35 +301,48 @@ def _c3_run_and_check(W, c4, lr, steps, B=64):
             assert ok, (s, r, msg)
     ok, msg, flips = RA.report(relus)
     assert ok, msg
-    print(f"W={W} c4={c4}: {flips} explained ReLU flips")
+    ok, msg, _ = RA.report(tw.relus)
+    assert ok, ("permuted twin", msg)
     lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
+    lin2 = [m for seq in (tw.model.bot_l, tw.model.top_l) for m in seq
+            if isinstance(m, torch.nn.Linear)]
+    n_expl = 0
     for r in range(W):
         assert res[r]["local"] == [t for t in range(26) if alloc[t] == r]
         for t, w in res[r]["tables"].items():
-            e = ref.emb_l[t]
+            e, e2 = ref.emb_l[t], tw.model.emb_l[t]
             if isinstance(w, tuple):  # QR: (quotient, remainder) tables + their momentum
                 assert hasattr(e, "weight_q"), t
-                parts = [(w[0], e.weight_q, res[r]["mom"][t][0]),
-                         (w[1], e.weight_r, res[r]["mom"][t][1])]
+                parts = [(w[0], e.weight_q, e2.weight_q, res[r]["mom"][t][0]),
+                         (w[1], e.weight_r, e2.weight_r, res[r]["mom"][t][1])]
             else:
-                parts = [(w, e.weight, res[r]["mom"][t] if c4 else None)]
-            for got, p, mom in parts:
-                ok, msg = fp32_close(got, p.detach().numpy())
-                assert ok, (r, t, msg)
+                parts = [(w, e.weight, e2.weight, res[r]["mom"][t] if c4 else None)]
+            for got, p, p2, mom in parts:
+                ok, msg, ne = tw.close(got, p, p2, f"rank {r} table {t}")
+                assert ok, msg
+                n_expl += ne
                 if mom is not None:
-                    ok, msg = fp32_close(mom, opt.state[id(p)]["momentum"].numpy())
-                    assert ok, ("momentum", r, t, msg)
+                    ok, msg, ne = tw.close(mom, opt.state[id(p)]["momentum"],
+                                           opt2.state[id(p2)]["momentum"], f"momentum {t}")
+                    assert ok, msg
+                    n_expl += ne
         for i, (w, b) in enumerate(res[r]["dense"]):
-            ok, msg = fp32_close(w, lin[i].weight.detach().numpy())
-            assert ok, (r, "W", i, msg)
-            ok, msg = fp32_close(b, lin[i].bias.detach().numpy())
-            assert ok, (r, "b", i, msg)
+            # beyond 1e-5 only where the oracle itself moves that much under a permuted
+            # summation order (relu_align.PermutedTwin)
+            for got, p, p2 in ((w, lin[i].weight, lin2[i].weight),
+                               (b, lin[i].bias, lin2[i].bias)):
+                ok, msg, ne = tw.close(got, p, p2, f"rank {r} dense {i}")
+                assert ok, msg
+                n_expl += ne
             if c4:
-                sw, sb = res[r]["sum"][i]
-                ok, msg = fp32_close(sw, opt.state[id(lin[i].weight)]["sum"].numpy())
-                assert ok, ("adagrad sum W", r, i, msg)
-                ok, msg = fp32_close(sb, opt.state[id(lin[i].bias)]["sum"].numpy())
-                assert ok, ("adagrad sum b", r, i, msg)
+                for got, p, p2 in zip(res[r]["sum"][i], (lin[i].weight, lin[i].bias),
+                                      (lin2[i].weight, lin2[i].bias)):
+                    ok, msg, ne = tw.close(got, opt.state[id(p)]["sum"],
+                                           opt2.state[id(p2)]["sum"], f"rank {r} sum {i}")
+                    assert ok, msg
+                    n_expl += ne
+    print(f"W={W} c4={c4}: {flips} explained ReLU flips, {n_expl} elements beyond 1e-5 "
+          f"explained by the oracle's own summation-order spread")
 
 
 @pytest.mark.parametrize("W", [4, 8])

@@ -1197,68 +1197,6 @@ def test_tbe_backward_deferred_into_gemm_launches(ops, mode, D, sort):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad"])
-@pytest.mark.parametrize("case", ["c3", "cap_edge", "int64", "long_tables", "no_bound",
-                                  "underestimated"])
-def test_tbe_sort_deferred_into_gemm_launch(ops, mode, case):
-    """dlrm_tbe_sort_defer + the sort as pass 3 of a grouped GEMM launch (256-thread
-    workgroups, bags packed into the positions) then the presorted backward: bitwise the
-    update of the lookup launch's 1024-thread sort (dlrm_tbe_forward_presort), error flags
-    alike.  Tables of exactly 2048 lookups (the role's cap), 64-bit indices / offsets,
-    2049..4096 lookups (sorted by the 1024-thread kernel inside the defer call: no role),
-    no per-table bound (the backward sorts itself: no role), and an underestimated bound
-    (a table past both sorts' capacity - 2048 / 4096 lookups - skipped and flagged both
-    ways; between the two capacities only the role would skip it)."""
-    torch.manual_seed(31)
-    rows, D = [3, 5000, 4, 700, 1, 90000, 17], 64
-    B, L = {"cap_edge": (1024, 2), "long_tables": (1024, 3)}.get(case, (512, 1))
-    T = len(rows)
-    lo = [torch.arange(B) * L for _ in rows]
-    li = [torch.randint(0, n, (B * L,)) for n in rows]
-    li[3][5] = 10 ** 6  # out of range
-    off, idx = O.batched_csr(lo, li)
-    if case == "underestimated":  # table 5: 9 lookups per bag, past both sorts' capacity
-        lo[5] = torch.arange(B) * 9
-        li[5] = torch.randint(0, rows[5], (B * 9,))
-        off, idx = O.batched_csr(lo, li)
-    it = torch.int64 if case == "int64" else torch.int32
-    idx, off = idx.to(it).to(dev), off.to(it).to(dev)
-    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
-    G = torch.randn(B, T, D, device=dev)
-    W0 = torch.randn(sum(rows), D, device=dev)
-    mom0 = torch.rand(sum(rows), device=dev)
-    mx = {"no_bound": 0, "underestimated": B}.get(case, B * L)
-    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), sum(rows), D),
-                     dtype=torch.uint8, device=dev)
-    A1, B1 = torch.randn(256, 260, device=dev), torch.randn(260, 512, device=dev)
-    res = []
-    for defer in (False, True):
-        flag = torch.zeros(1, dtype=torch.int32, device=dev)
-        ws.zero_()
-        p1, c1 = ops.gemm_problem(A1, B1)
-        if defer:
-            role = ops.tbe_sort_defer(row_base, T, B, idx, off, sum(rows), D, ws, mx,
-                                      error_flag=flag)
-            assert (role is not None) == (case in ("c3", "cap_edge", "int64", "underestimated"))
-            ops.gemm_group([p1], None, dev, role=role, phase=3)
-        else:
-            if mx:
-                assert ops.tbe_forward_presort(W0, row_base, T, B, idx, off, ws, mx,
-                                               error_flag=flag, lookup=False) is None
-            ops.gemm_group([p1], None, dev)
-        W, mom = W0.clone(), mom0.clone()
-        ops.tbe_backward(mode, W, row_base, T, B, idx, off, G, lr=0.3, eps=1e-8, momentum=mom,
-                         workspace=ws, max_lookups_per_table=mx, error_flag=flag,
-                         presorted=True)
-        torch.cuda.synchronize()
-        res.append((W.cpu(), mom.cpu(), flag.item(), c1.cpu()))
-    (w0, m0, f0, g0), (w1, m1, f1, g1) = res
-    assert torch.equal(w0, w1) and torch.equal(m0, m1) and torch.equal(g0, g1)
-    assert f0 == f1 and f0 & ops.TBE_ERR_INDEX
-    if case == "underestimated":
-        assert f0 & 2  # DLRM_TBE_ERR_TABLE_CAP
-
-
 def test_gemm_group_role_rejects_a_foreign_role(ops):
     """A role struct not filled by dlrm_tbe_backward_defer is refused (INVALID_ARG)."""
     import ctypes

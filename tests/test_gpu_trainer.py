@@ -535,14 +535,22 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
                         qr_operation="mult", qr_threshold=thr)
     tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
     relus = RA.align(ref)
+    tw = RA.PermutedTwin(ref, B).with_head()  # the oracle's own summation-order spread
+    head = RA.AlignedHead(ref)
     opt = O.RWSAdagradOracle(ref.parameters(), lr=lr)
+    opt2 = O.RWSAdagradOracle(tw.model.parameters(), lr=lr)
     rng = np.random.RandomState(1)
     losses = []
     n_loss_checked = 0
     for s in range(10):
         X, lS_o, lS_i, T = _rand_batch(rng, rows, B, 1, bot[0], "bce")
         Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
-        RA.queue(relus, RA.engine_masks(tr, B, B))
+        masks = RA.engine_masks(tr, B, B)
+        dz = tr._bufs[(B, B)]["dz"].cpu()
+        RA.queue(relus, masks)
+        tw.queue(masks)
+        head.push(dz, T, B)
+        tw.push_head(dz, T, B)
         Xt, ot, it, Tt = (torch.tensor(X), torch.tensor(lS_o), [torch.tensor(i) for i in lS_i],
                           torch.tensor(T))
         Zr = ref(Xt, ot, it)
@@ -550,6 +558,11 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
         opt.zero_grad()
         Er.backward()
         opt.step()
+        X2, o2, i2, T2 = tw.batch(Xt, ot, it, Tt)
+        E2 = tw.model.loss_fn(tw.model(X2, o2, i2), T2)
+        opt2.zero_grad()
+        E2.backward()
+        opt2.step()
         losses.append((round(E.item(), 5), round(Er.item(), 5)))
         ok, msg = fp32_close(Z.cpu().numpy(), Zr.detach().numpy().ravel())
         assert ok, (s, "Z", losses, msg)
@@ -567,26 +580,45 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     assert n_loss_checked == 10 if lr <= 1e-4 else n_loss_checked >= 1, n_loss_checked
     ok, msg, flips = RA.report(relus)
     assert ok, msg
-    print(f"explained ReLU flips: {flips}")
+    for r in (head, tw.head):
+        ok, msg = r.report()
+        assert ok, msg
+    ok, msg, _ = RA.report(tw.relus)
+    assert ok, ("permuted twin", msg)
+    print(f"explained ReLU flips: {flips}; saturated-head samples aligned: {head.aligned}")
     torch.cuda.synchronize()
     tr.check_errors()
-    for t, e in enumerate(ref.emb_l):
+    n_expl = 0
+    for t, (e, e2) in enumerate(zip(ref.emb_l, tw.model.emb_l)):
         got_w, got_m = tr.table(t), tr.table_momentum(t)
-        parts = [(e.weight_q, got_w[0], got_m[0]), (e.weight_r, got_w[1], got_m[1])] \
-            if hasattr(e, "weight_q") else [(e.weight, got_w, got_m)]
-        for p, gw, gm in parts:
-            ok, msg = fp32_close(gw.cpu().numpy(), p.detach().numpy())
-            assert ok, ("table", t, msg)
-            ok, msg = fp32_close(gm.cpu().numpy(), opt.state[id(p)]["momentum"].numpy())
-            assert ok, ("momentum", t, msg)
+        parts = [(e.weight_q, e2.weight_q, got_w[0], got_m[0]),
+                 (e.weight_r, e2.weight_r, got_w[1], got_m[1])] \
+            if hasattr(e, "weight_q") else [(e.weight, e2.weight, got_w, got_m)]
+        for p, p2, gw, gm in parts:
+            ok, msg, ne = tw.close(gw.cpu().numpy(), p, p2, f"table {t}")
+            assert ok, msg
+            n_expl += ne
+            ok, msg, ne = tw.close(gm.cpu().numpy(), opt.state[id(p)]["momentum"],
+                                   opt2.state[id(p2)]["momentum"], f"momentum {t}")
+            assert ok, msg
+            n_expl += ne
     lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
-    for L, (W, b), (sW, sb) in zip(lin, tr.dense_state(), tr.dense_adagrad_state()):
-        for got, p in ((W, L.weight), (b, L.bias)):
-            ok, msg = fp32_close(got.cpu().numpy(), p.detach().numpy())
-            assert ok, ("dense", msg)
-        for got, p in ((sW, L.weight), (sb, L.bias)):
-            ok, msg = fp32_close(got.cpu().numpy(), opt.state[id(p)]["sum"].numpy())
-            assert ok, ("adagrad sum", msg)
+    lin2 = [m for seq in (tw.model.bot_l, tw.model.top_l) for m in seq
+            if isinstance(m, torch.nn.Linear)]
+    for L, L2, (W, b), (sW, sb) in zip(lin, lin2, tr.dense_state(), tr.dense_adagrad_state()):
+        for got, p, p2 in ((W, L.weight, L2.weight), (b, L.bias, L2.bias)):
+            # beyond 1e-5 only where the oracle itself moves that much under a permuted
+            # summation order (relu_align.PermutedTwin)
+            ok, msg, ne = tw.close(got.cpu().numpy(), p, p2, "dense")
+            assert ok, msg
+            n_expl += ne
+        for got, p, p2 in ((sW, L.weight, L2.weight), (sb, L.bias, L2.bias)):
+            ok, msg, ne = tw.close(got.cpu().numpy(), opt.state[id(p)]["sum"],
+                                   opt2.state[id(p2)]["sum"], "adagrad sum")
+            assert ok, msg
+            n_expl += ne
+    print(f"elements beyond 1e-5 explained by the oracle's own summation-order spread: "
+          f"{n_expl}")
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -733,44 +765,6 @@ def test_bottom_parts_split_chain_matches_single(name, B):
     for other in res[1:]:
         for a, b in zip(res[0], other):
             assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("name,B", [("c3_small", 512), ("c2_small", 128)])
-@pytest.mark.parametrize("graph", [False, True])
-def test_sort_role_matches_lookup_launch_sort(name, B, graph):
-    """The per-table sort as a role of the first top-MLP GEMM launch (sort_role, with the
-    bottom MLP then split over more workgroups) vs inside the lookup launch: 3 steps leave
-    bitwise the same state, eager and replayed from a captured graph."""
-    DLRMTrainer, TrainerConfig = _trainer()
-    c = CASES[name]
-    D, rows = c["D"], c["rows"]
-    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
-                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function=c["loss"],
-                        learning_rate=c["lr"])
-    res = []
-    for role in (False, True):
-        tr = DLRMTrainer(cfg, device=dev, seed=11)
-        tr.sort_role = role
-        batches = [tr.synthetic_batch(B, 1, seed=s) for s in range(3)]
-        if graph:
-            tr.step(batches[0])
-            run = tr.capture(batches[0])
-            for b in batches[1:]:
-                for src, dst in zip((b.X, b.offsets, b.indices, b.target),
-                                    (batches[0].X, batches[0].offsets, batches[0].indices,
-                                     batches[0].target)):
-                    dst.copy_(src)
-                run()
-        else:
-            for b in batches:
-                tr.step(b)
-        torch.cuda.synchronize()
-        tr.check_errors()
-        assert tr.gather_fused and not tr._roles
-        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(),
-                    tr._bufs[(B, B)]["prob"].cpu().clone()))
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("name,B", [("c3_small", 512), ("c2_small", 128)])

@@ -81,9 +81,6 @@ def main():
         us = timeit(lambda: ops.tbe_forward_presort(W, row_base, 26, B, idx, off, ws, B,
                                                     lookup=False))
         print(f"{name} B={B} sort-only presort: {us:7.2f} us", flush=True)
-        role = ops.tbe_sort_defer(row_base, 26, B, idx, off, W.shape[0], D, ws, B)
-        us = timeit(lambda: ops.gemm_group([], None, dev, role=role, phase=3))
-        print(f"{name} B={B} sort as a role (256 threads, alone): {us:7.2f} us", flush=True)
         for parts in (1, 2, 4):
             chain = ops.mlp_chain(X, layers, parts=parts)
             us = timeit(lambda: ops.mlp_chain_forward(chain))
