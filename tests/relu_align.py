@@ -180,6 +180,102 @@ class PermutedTwin:
         return True, "", n_expl
 
 
+# Adagrad's step lr * g / (sqrt(S) + eps) is ill-conditioned where g is small against the
+# error it can carry: its derivative in g is up to lr / (sqrt(S) + eps).  AdagradBound
+# bounds the error of every dense weight gradient g = dY^T X of every step by running
+# error analysis (u = ROUND_REL, the relative error allowed per dot product, which also
+# covers the <= 1e-5 weight and state differences carried from earlier steps):
+#  * forward, per MLP: dX_0 = 0 (bottom: the exact dense input) or u |R| (top: the
+#    interaction output); dY_k = u (|X_k| |W_k|^T + |b_k|) + dX_k |W_k|^T, masked by the
+#    ReLU to give dX_{k+1}: a pre-activation that cancels to almost nothing is relatively
+#    inaccurate, and so is everything computed from it;
+#  * backward magnitudes E_k of the terms dY_k is summed from: |dLoss/dz| at the head, then
+#    E_k = E_{k+1} |W_{k+1}| masked (top MLP; bottom MLP: E = |dY|);
+#  * |error of g_k| <= u E_k^T |X_k| + |dY_k|^T dX_k.
+# It accumulates lr * scale * that / (sqrt(S_t) + eps) per element over the steps; close()
+# then explains an element by EITHER the permuted twin's spread or this bound.
+ROUND_REL = 64 * 2.0 ** -24
+
+
+class AdagradBound:
+    def __init__(self, model, lr: float, eps: float = 1e-10, scale: float = 1.0):
+        self.lr, self.eps, self.scale = lr, eps, scale
+        self.mlps = {"bot": [m for m in model.bot_l if isinstance(m, nn.Linear)],
+                     "top": [m for m in model.top_l if isinstance(m, nn.Linear)]}
+        self.bound = {id(p): torch.zeros_like(p, dtype=torch.float64)
+                      for Ls in self.mlps.values() for L in Ls for p in (L.weight, L.bias)}
+        self.grad = {id(p): torch.zeros_like(p, dtype=torch.float64)
+                     for Ls in self.mlps.values() for L in Ls for p in (L.weight, L.bias)}
+        self.calls = []  # per forward of an MLP: (which, {k: |X_k|}, {k: |dY_k|})
+        for which, Ls in self.mlps.items():
+            for k, L in enumerate(Ls):
+                L.register_forward_hook(lambda m, i, o, w=which, k=k: self._hook(w, k, i, o))
+
+    def _hook(self, which, k, inp, out):
+        if k == 0:
+            self.calls.append((which, {}, {}))
+        _, xs, dys = self.calls[-1]
+        xs[k] = inp[0].detach().abs().double()
+        if out.requires_grad:
+            out.register_hook(lambda g: dys.__setitem__(k, g.detach().abs().double()))
+
+    def after_step(self, opt) -> None:
+        """Call after the oracle optimizer's step (its state holds the new sums)."""
+        u = ROUND_REL
+        for which, xs, dys in self.calls:
+            Ls = self.mlps[which]
+            n = len(Ls)
+            Wa = [L.weight.detach().abs().double() for L in Ls]
+            ba = [L.bias.detach().abs().double() for L in Ls]
+            dX = torch.zeros_like(xs[0]) if which == "bot" else u * xs[0]
+            dXs = []
+            for k in range(n):  # forward error bounds
+                dXs.append(dX)
+                dY = u * (xs[k] @ Wa[k].t() + ba[k]) + dX @ Wa[k].t()
+                dX = dY * (xs[k + 1] > 0) if k + 1 < n else None
+            E = dys[n - 1]
+            for k in range(n - 1, -1, -1):  # backward magnitudes + the gradient bound
+                if which == "bot":
+                    E = dys[k]
+                gw = u * (E.t() @ xs[k]) + dys[k].t() @ dXs[k]
+                gb = u * E.sum(0)
+                self.grad[id(Ls[k].weight)].add_(gw)
+                self.grad[id(Ls[k].bias)].add_(gb)
+                if which == "top" and k > 0:
+                    E = (E @ Wa[k]) * (xs[k] > 0)
+        self.calls = []
+        for Ls in self.mlps.values():
+            for L in Ls:
+                for p in (L.weight, L.bias):
+                    S = opt.state[id(p)]["sum"].double()
+                    g = self.grad[id(p)]
+                    self.bound[id(p)].add_(self.lr * self.scale * g / (S.sqrt() + self.eps))
+                    g.zero_()
+
+
+def close_explained(got, ref, twin, bound=None, what=""):
+    """(ok, message, n_explained): |got - ref| <= 1e-5 max(1, |ref|) + max(SPREAD |ref -
+    twin|, bound) element-wise (bound: an AdagradBound allowance, or None)."""
+    import numpy as np
+    a = np.asarray(got, dtype=np.float64)
+    b = torch.as_tensor(ref).detach().double().numpy()
+    c = torch.as_tensor(twin).detach().double().numpy()
+    base = 1e-5 * np.maximum(1.0, np.abs(b))
+    extra = SPREAD * np.abs(b - c)
+    if bound is not None:
+        extra = np.maximum(extra, bound.numpy())
+    err = np.abs(a - b)
+    lim = base + extra
+    n_expl = int(((err > base) & (err <= lim)).sum())
+    if (err > lim).any():
+        i = np.unravel_index(np.argmax(err - lim), a.shape)
+        bd = float(bound.numpy()[i]) if bound is not None else 0.0
+        return False, (f"{what} got {a[i]!r} oracle {b[i]!r} twin {c[i]!r} at {i}: beyond 1e-5, "
+                       f"{SPREAD} x the permuted twin's spread and the Adagrad conditioning "
+                       f"allowance {bd!r}"), n_expl
+    return True, "", n_expl
+
+
 # The sigmoid + BCE head has its own ill-conditioned points: the reference's BCE backward
 # divides by max(p (1 - p), 1e-12), and p rounds to exactly 1.0 for z > ~16.6, so a
 # sample's dLoss/dz jumps (to 0 at p == 1, by orders of magnitude inside the clamp) when

@@ -285,6 +285,7 @@ def _c3_run_and_check(W, c4, lr, steps, B=64):
     ref = _c3_model(c4)
     relus = RA.align(ref)
     tw = RA.PermutedTwin(ref, B, W)  # the oracle's own summation-order spread
+    ab = RA.AdagradBound(ref, lr, scale=1.0 / W) if c4 else None
     opt = O.RWSAdagradOracle(ref.parameters(), lr=lr) if c4 else None
     opt2 = O.RWSAdagradOracle(tw.model.parameters(), lr=lr) if c4 else None
     for s, (X, lS_o, lS_i, T) in enumerate(_c3_batches(B, steps)):
@@ -292,6 +293,8 @@ def _c3_run_and_check(W, c4, lr, steps, B=64):
             RA.queue(relus, res[r]["masks"][s])
             tw.queue(res[r]["masks"][s], rank=r)
         Zs, Es = O.distributed_step(ref, W, alloc, X, lS_o, lS_i, T, lr, optimizer=opt)
+        if ab is not None:
+            ab.after_step(opt)
         X2, o2, i2, T2 = tw.batch(X, lS_o, lS_i, T)
         O.distributed_step(tw.model, W, alloc, X2, o2, i2, T2, lr, optimizer=opt2)
         for r in range(W):
@@ -331,7 +334,9 @@ def _c3_run_and_check(W, c4, lr, steps, B=64):
             # summation order (relu_align.PermutedTwin)
             for got, p, p2 in ((w, lin[i].weight, lin2[i].weight),
                                (b, lin[i].bias, lin2[i].bias)):
-                ok, msg, ne = tw.close(got, p, p2, f"rank {r} dense {i}")
+                ok, msg, ne = RA.close_explained(got, p, p2,
+                                                 ab.bound[id(p)] if ab is not None else None,
+                                                 f"rank {r} dense {i}")
                 assert ok, msg
                 n_expl += ne
             if c4:

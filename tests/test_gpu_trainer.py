@@ -537,6 +537,7 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     relus = RA.align(ref)
     tw = RA.PermutedTwin(ref, B).with_head()  # the oracle's own summation-order spread
     head = RA.AlignedHead(ref)
+    ab = RA.AdagradBound(ref, lr)  # after the head: its hooks see the aligned dz
     opt = O.RWSAdagradOracle(ref.parameters(), lr=lr)
     opt2 = O.RWSAdagradOracle(tw.model.parameters(), lr=lr)
     rng = np.random.RandomState(1)
@@ -558,6 +559,7 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
         opt.zero_grad()
         Er.backward()
         opt.step()
+        ab.after_step(opt)
         X2, o2, i2, T2 = tw.batch(Xt, ot, it, Tt)
         E2 = tw.model.loss_fn(tw.model(X2, o2, i2), T2)
         opt2.zero_grad()
@@ -608,8 +610,9 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     for L, L2, (W, b), (sW, sb) in zip(lin, lin2, tr.dense_state(), tr.dense_adagrad_state()):
         for got, p, p2 in ((W, L.weight, L2.weight), (b, L.bias, L2.bias)):
             # beyond 1e-5 only where the oracle itself moves that much under a permuted
-            # summation order (relu_align.PermutedTwin)
-            ok, msg, ne = tw.close(got.cpu().numpy(), p, p2, "dense")
+            # summation order, or where Adagrad's conditioning allows it
+            # (relu_align.PermutedTwin, AdagradBound)
+            ok, msg, ne = RA.close_explained(got.cpu().numpy(), p, p2, ab.bound[id(p)], "dense")
             assert ok, msg
             n_expl += ne
         for got, p, p2 in ((sW, L.weight, L2.weight), (sb, L.bias, L2.bias)):
@@ -617,7 +620,7 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
                                    opt2.state[id(p2)]["sum"], "adagrad sum")
             assert ok, msg
             n_expl += ne
-    print(f"elements beyond 1e-5 explained by the oracle's own summation-order spread: "
+    print(f"elements beyond 1e-5 explained (permuted-order spread or Adagrad conditioning): "
           f"{n_expl}")
 
 

@@ -138,6 +138,7 @@ def test_two_fp32_summation_orders_of_c4_w8_are_explained_by_the_twin():
     ref = TD._c3_model(True)
     relus = RA.align(ref)
     tw = RA.PermutedTwin(ref, B, W)
+    ab = RA.AdagradBound(ref, lr, scale=1.0 / W)
     opt = O.RWSAdagradOracle(ref.parameters(), lr=lr)
     opt2 = O.RWSAdagradOracle(tw.model.parameters(), lr=lr)
     eperm = RA.PermutedTwin(eng, B, W, seed=99)
@@ -154,6 +155,7 @@ def test_two_fp32_summation_orders_of_c4_w8_are_explained_by_the_twin():
             RA.queue(relus, ms)
             tw.queue(ms, rank=r)
         O.distributed_step(ref, W, alloc, X, lS_o, lS_i, T, lr, optimizer=opt)
+        ab.after_step(opt)
         O.distributed_step(tw.model, W, alloc, *tw.batch(X, lS_o, lS_i, T), lr, optimizer=opt2)
     assert RA.report(relus)[0] and RA.report(tw.relus)[0]
     lin = lambda m: [x for seq in (m.bot_l, m.top_l) for x in seq  # noqa: E731
@@ -161,7 +163,10 @@ def test_two_fp32_summation_orders_of_c4_w8_are_explained_by_the_twin():
     n_expl = 0
     for L, L2, Le in zip(lin(ref), lin(tw.model), lin(eng)):
         for p, p2, pe in ((L.weight, L2.weight, Le.weight), (L.bias, L2.bias, Le.bias)):
-            ok, msg, n = tw.close(pe.detach().numpy(), p, p2)
+            ok, msg, n = RA.close_explained(pe.detach().numpy(), p, p2, ab.bound[id(p)])
             assert ok, msg
             n_expl += n
+            # the conditioning allowance alone explains it too
+            ok, msg, _ = RA.close_explained(pe.detach().numpy(), p, p, ab.bound[id(p)])
+            assert ok, ("Adagrad bound alone", msg)
     print(f"elements beyond 1e-5 between two fp32 orders, all explained: {n_expl}")
