@@ -953,7 +953,7 @@ def main():
 
     if (rank == 0 and not emulated) or (emulated and local_rank == 0):
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": procs,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1000.0, 4),
             "ms_per_step_p10_p50_p90": [pct[10], pct[50], pct[90]],
@@ -965,7 +965,8 @@ def main():
                        "lookups_per_bag": c["L"], "bot": c["bot"], "top": ln_top,
                        "optimizer": c["optimizer"], "qr": c.get("qr"),
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
-                       "hip_graph": use_graph, "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
+                       "hip_graph": use_graph, "capture": tr.capture_mode,
+                       "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
                        "tbe_role_at": list(tr.tbe_role_at), "bottom_parts": tr.bottom_parts,
                        "head_role": tr.head_role, "full_last_wgrad": tr.full_last_wgrad,
                        "tune": args.tune or None},

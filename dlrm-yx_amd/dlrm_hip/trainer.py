@@ -264,6 +264,7 @@ class DLRMTrainer:
         self._colsum_ws: Optional[torch.Tensor] = None
         self._head_ws: Optional[torch.Tensor] = None
         self.step_count = 0
+        self.capture_mode = None  # "whole" | "segments": how the last capture() was built
         if init:
             self.init_random(seed)
 
@@ -574,11 +575,13 @@ class DLRMTrainer:
         return self._cur["prob"], self._cur["loss"]
 
     def segments(self, batch: Batch, profile=None):
-        """The step as an ordered list of ("gpu", fn) / ("comm", fn) items.  "gpu" items only
-        enqueue HIP kernels on the current stream (no host sync, no allocation after the
-        first step of a batch size): each one can be captured in its own hipGraph.  "comm"
-        items issue or wait for the RCCL collectives between them (multi GPU only), so a
-        multi-GPU step replays a few graphs around its three collectives.
+        """The step as an ordered list of ("gpu", fn) / ("comm", fn) / ("host", fn) items.
+        "gpu" items only enqueue HIP kernels on the current stream (no host sync, no
+        allocation after the first step of a batch size): each one can be captured in a
+        hipGraph.  "comm" items issue or wait for the collectives between them (multi GPU
+        only); on RCCL they are stream-ordered too, so the whole multi-GPU step captures as
+        ONE graph (capture); on gloo they run eagerly between segment graphs.  "host" items
+        are host bookkeeping, run on every replay.
 
         MLP backward: each layer's weight gradient is split-K into a per-layer partial
         buffer and its reduction (+ fused SGD on one GPU) is a REDUCE job inside the NEXT
@@ -911,7 +914,7 @@ class DLRMTrainer:
             segs = [("gpu", fwd_single), ("gpu", middle), ("gpu", backward_single)]
             if not fused_opt:
                 segs.append(("gpu", dense_update))
-            return segs + [("comm", done)]
+            return segs + [("host", done)]
         # multi GPU (distributed_forward, dlrm_s_pytorch.py:686-730; DDP :1626-1633):
         #  * the pooled-embedding all-to-all overlaps the bottom MLP (one chain launch);
         #  * the top MLP's gradient bucket is all-reduced as soon as the top backward is
@@ -946,7 +949,7 @@ class DLRMTrainer:
             ("comm", wait("ar_top")),
             ("comm", wait("ar_bot")),
             ("gpu", dense_update),
-            ("comm", done),
+            ("host", done),
         ]
 
 
@@ -999,11 +1002,42 @@ class DLRMTrainer:
         ops.qr_pool_combine_forward(self.cfg.qr_operation, self.T_local, B, self.D, self._qr_pq,
                                     self._qr_pr, bufs["P"], bufs["E"])
 
-    def capture(self, batch: Batch, pool=None):
-        """A replayable step for ``batch``: its "gpu" segments captured as hipGraphs (one
-        graph on one GPU; a few graphs around the collectives on several), "comm" items run
-        eagerly between them.  Run one eager step of this batch size first (allocations).
-        Returns a callable; each call is one full training step on the captured buffers."""
+    def capture(self, batch: Batch, pool=None, whole: Optional[bool] = None):
+        """A replayable step for ``batch``.  whole (default: one GPU, or collectives that
+        capture - the emulated rank's device copies): the step's kernels AND its
+        collectives in ONE hipGraph (a graph-to-graph boundary costs ~9 us of idle GPU,
+        profiles/r05_step_timeline_emul8_r2.txt); else (RCCL, gloo) the "gpu" segments
+        captured as graphs with the "comm" items run eagerly between them.  Run one eager step of this
+        batch size first (allocations).  Returns a callable; each call is one full training
+        step on the captured buffers."""
+        auto = whole is None
+        if auto:
+            whole = not self.distributed or bool(getattr(self.comm, "capturable", False))
+        if whole:
+            segs = self.segments(batch)
+            host = [fn for kind, fn in segs if kind == "host"]
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=pool):
+                    for kind, fn in segs:
+                        if kind != "host":
+                            fn()
+            except Exception as e:  # noqa: BLE001
+                if not (auto and self.distributed):
+                    raise
+                import warnings
+                warnings.warn(f"whole-step capture with the collectives failed ({e!r}); "
+                              "capturing the kernel segments between eager collectives")
+                torch.cuda.synchronize()
+                return self.capture(batch, pool=pool, whole=False)
+            self.capture_mode = "whole"
+
+            def run_whole():
+                g.replay()
+                for fn in host:
+                    fn()
+            return run_whole
+        self.capture_mode = "segments"
         items = []
         pending = []
         segs = self.segments(batch)
@@ -1021,6 +1055,8 @@ class DLRMTrainer:
         for kind, fn in segs:
             if kind == "gpu":
                 pending.append(fn)
+            elif kind == "host":
+                items.append(fn)
             else:
                 flush()
                 items.append(fn)
@@ -1232,6 +1268,10 @@ class TorchComm:
             dense_pg = dist.new_group(ranks=list(range(dist.get_world_size(pg))),
                                       backend=dist.get_backend(pg))
         self.dense_pg = dense_pg
+        # collectives are not captured into the step's hipGraph: a capture of RCCL
+        # collectives issued through torch.distributed hung on this stack (1-rank nccl,
+        # gpurun_out r05 pytest_cap); the kernel segments between them are graphs instead
+        self.capturable = False
 
     def a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
         import torch.distributed as dist
@@ -1260,6 +1300,7 @@ class EmulatedComm:
     of min(send, recv) bytes on the current stream (the rest of the receive buffer keeps
     whatever it holds); the all-reduce does nothing.  Times the rank's own work, not the
     fabric."""
+    capturable = True
 
     def a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
         n = min(int(sum(out_splits)), int(sum(in_splits)))

@@ -612,6 +612,7 @@ def _nccl_one_rank_worker(port, q, graph):
             tr.check_errors()
             res["tables"] = tr.weights.cpu().numpy()
             res["dense"] = tr.params.cpu().numpy()
+            res["capture"] = tr.capture_mode
             if name == "nccl":
                 res["backend"] = dist.get_backend(tr.comm.pg)
                 res["dense_backend"] = dist.get_backend(tr.comm.dense_pg)
@@ -642,6 +643,8 @@ def test_multi_gpu_schedule_on_one_rank_rccl_matches_single_gpu(graph):
     assert isinstance(out, dict), out
     a, b = out["single"], out["nccl"]
     assert b["backend"] == "nccl" and b["dense_backend"] == "nccl"
+    if graph:  # RCCL: kernel segments as graphs, the collectives eager between them
+        assert b["capture"] == "segments", b["capture"]
     for s in range(3):
         ok, msg = fp32_close(b["Z"][s], a["Z"][s])
         assert ok, (s, "Z", msg)
@@ -666,6 +669,7 @@ def test_emulated_rank_runs_the_w8_shapes():
     assert bs[0].X.shape[0] == 256 and bs[0].indices.numel() == 6 * 2048
     tr.step(bs[0])
     run = tr.capture(bs[1])
+    assert tr.capture_mode == "whole"  # the emulated collectives are device copies
     run()
     run()
     torch.cuda.synchronize()
