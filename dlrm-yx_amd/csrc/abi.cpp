@@ -26,7 +26,7 @@ extern "C" int dlrm_abi_version(void) { return 7; }
 extern "C" const char* dlrm_last_error(void) { return dlrm::g_last_error; }
 
 extern "C" int dlrm_set_tuning(int32_t key, int64_t value) {
-  DLRM_ARG(key >= DLRM_TUNE_GEMM_TILE && key <= DLRM_TUNE_INTERACT_BWD,
+  DLRM_ARG(key >= DLRM_TUNE_GEMM_TILE && key <= DLRM_TUNE_INTERACT_FWD,
            "dlrm_set_tuning: unknown key %d", (int)key);
   DLRM_ARG(value >= 0, "dlrm_set_tuning: negative value");
   dlrm::g_tuning[key] = value;

@@ -477,10 +477,21 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArg
 // (D 16) 8.5 -> 6.8 us, but C3 (D 128) 20.6 -> 29.8 us - each of a sample's four waves
 // rebuilds S and re-reads dR - so it is the default only for D <= 32 (one wave per sample);
 // tuning INTERACT_BWD = 3 / 4 forces v3 / v4.
-inline bool use_v4(int D) {
-  const int t = dlrm::tuning(DLRM_TUNE_INTERACT_BWD);
-  return t == 4 || (t != 3 && D <= 32);
+// Backward kernel for the compile-time D (tuning INTERACT_BWD: 3 / 4 / 5 forces v3 / v4 /
+// v5; default v4 for D <= 32, v5 above); forward (INTERACT_FWD: 4 / 5; default v5 for
+// D >= 64).
+inline int bwd_version(int D) {
+  const int t = (int)dlrm::tuning(DLRM_TUNE_INTERACT_BWD);
+  if (t == 3 || t == 4) return t;
+  if (t == 5) return D >= 64 ? 5 : 4;
+  return D <= 32 ? 4 : 5;
 }
+inline int fwd_version(int D) {
+  const int t = (int)dlrm::tuning(DLRM_TUNE_INTERACT_FWD);
+  if (t == 4) return 4;
+  return D >= 64 ? 5 : 4;
+}
+inline int v5_grid(int64_t B) { return (int)std::min<int64_t>(B, 16384); }
 
 template <int RPI>
 __device__ __forceinline__ const float* row_ptr_n(const FeatArgs& fa, int F, int64_t b, int i0,
@@ -608,6 +619,212 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_v4(int B, int F, FeatArg
             dst[n] = x;
           }
         }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------ v5: a workgroup per sample --
+// D = 64 / 128: one sample per workgroup of D / 32 waves, each wave owning a 32-column
+// block of T (F <= 32 rows staged once in LDS by the whole workgroup).  v4 ran one wave per
+// sample, so a C3 batch of 2048 samples put 8 waves on a CU and every wave walked the
+// whole sample (gather latency, 64 dependent MFMAs, the output row) alone; here the batch
+// is D / 32 times as many waves with a quarter of the chain each.
+//   forward: wave w multiplies its column block (Z_w = T_w T_w^T, 16 MFMAs); the partial
+//            Grams meet in LDS and are added in block order for the lower triangle;
+//   backward: wave w computes dT_w = S T_w (S = G + G^T from the staged dR, v3's products
+//            in v3's k order: bitwise v3), writes it over its columns of T, and the
+//            workgroup stores every gradient row as whole float4 rows.
+template <int D>
+__device__ __forceinline__ const float* row_ptr_w(const FeatArgs& fa, int F, int64_t b, int i0,
+                                                  int sub) {
+  constexpr int RPW = 64 / (D / 4);  // rows per wave-instruction
+  const float* p = fa.ptr[0];
+  int64_t bs = 0;
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int f = i0 + j;
+    const float* pj = f < F ? fa.ptr[f] : fa.ptr[0];
+    const int64_t bj = f < F ? fa.bs[f] : 0;
+    if (sub == j) p = pj, bs = bj;
+  }
+  return p + b * bs;
+}
+
+template <int D>
+__device__ __forceinline__ float* grad_ptr_w(const GradArgs& ga, int F, int64_t b, int i0,
+                                             int sub) {
+  constexpr int RPW = 64 / (D / 4);
+  float* p = ga.ptr[0];
+  int64_t bs = 0;
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int f = i0 + j;
+    float* pj = f < F ? ga.ptr[f] : ga.ptr[0];
+    const int64_t bj = f < F ? ga.bs[f] : 0;
+    if (sub == j) p = pj, bs = bj;
+  }
+  return p + b * bs;
+}
+
+// T (F <= 32 rows, rows >= F zero) of sample b -> Tl (pitch DP), the whole workgroup.
+template <int D, bool GATHER>
+__device__ __forceinline__ void v5_load_t(int B, int F, const FeatArgs& fa, const GatherArgs& gt,
+                                          int64_t b, float* Tl, bool flag) {
+  constexpr int NT = 2 * D, C4 = D / 4, RPW = 64 / C4, RPB = NT / C4, NI = 32 / RPB;
+  constexpr int DP = D + 4;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int sw = lane / C4, c = lane - sw * C4;
+  float4 v[NI];
+#pragma unroll
+  for (int q = 0; q < NI; ++q) {
+    const int i0 = q * RPB + wave * RPW, f = i0 + sw;
+    if constexpr (GATHER) {
+      const float* src = fa.ptr[0] + b * fa.bs[0];
+      bool zero = false;
+      if (f >= 1 && f < F) {
+        const int64_t lo = gt.row_base[f - 1], n = gt.row_base[f] - lo;
+        const int64_t r = gt.idx[(int64_t)(f - 1) * B + b];
+        if (r >= 0 && r < n) {
+          src = gt.W + (lo + r) * D;
+        } else {
+          zero = true;
+          if (flag && c == 0 && gt.err) atomicOr(gt.err, DLRM_TBE_ERR_INDEX);
+        }
+      }
+      v[q] = *reinterpret_cast<const float4*>(src + 4 * c);
+      if (zero) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      v[q] = *reinterpret_cast<const float4*>(row_ptr_w<D>(fa, F, b, i0, sw) + 4 * c);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NI; ++q) {
+    const int f = q * RPB + wave * RPW + sw;
+    *reinterpret_cast<float4*>(Tl + f * DP + 4 * c) =
+        f < F ? v[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int D, bool GATHER>
+__global__ __launch_bounds__(2 * D) void interact_dot_fwd_v5(int B, int F, FeatArgs fa, int self,
+                                                             float* __restrict__ out,
+                                                             int64_t ld_out, int width,
+                                                             GatherArgs gt) {
+  constexpr int NW = D / 32, DP = D + 4, PP = 33;
+  __shared__ __attribute__((aligned(16))) float Tl[32 * DP];
+  __shared__ float Pl[NW * 32 * PP];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int h = lane >> 5, l32 = lane & 31;
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    v5_load_t<D, GATHER>(B, F, fa, gt, b, Tl, true);
+    __syncthreads();
+    {
+      const float* trow = Tl + l32 * DP + 32 * wave + 16 * h;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(trow + 4 * q);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, v.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, v.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, v.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, v.w, acc, 0, 0, 0);
+      }
+      float* P = Pl + wave * 32 * PP;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) P[((r & 3) + 8 * (r >> 2) + 4 * h) * PP + l32] = acc[r];
+    }
+    __syncthreads();
+    float* orow = out + b * ld_out;
+    for (int e = tid; e < width; e += 2 * D) {
+      float v;
+      if (e < D) {
+        v = Tl[e];
+      } else {
+        int i, j;
+        pair_of(e - D, self, i, j);
+        v = Pl[i * PP + j];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v += Pl[w * 32 * PP + i * PP + j];
+      }
+      orow[e] = v;
+    }
+    __syncthreads();
+  }
+}
+
+template <int D, bool GATHER>
+__global__ __launch_bounds__(2 * D) void interact_dot_bwd_v5(int B, int F, FeatArgs fa, int self,
+                                                             const float* __restrict__ gout,
+                                                             int64_t ld_g, GradArgs ga,
+                                                             int relu_x, int vec_g,
+                                                             GatherArgs gt) {
+  constexpr int NT = 2 * D, DP = D + 4, C4 = D / 4, RPW = 64 / C4, RPB = NT / C4;
+  constexpr int GP = D + 32 * 33 / 2 + 4;
+  __shared__ __attribute__((aligned(16))) float Tl[32 * DP];
+  __shared__ __attribute__((aligned(16))) float Gl[GP];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  const int width = D + npairs;
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    {
+      const float* gsrc = gout + b * ld_g;
+      const int w4 = vec_g ? width / 4 : 0;
+      for (int q = tid; q < w4; q += NT)
+        *reinterpret_cast<float4*>(Gl + 4 * q) = *reinterpret_cast<const float4*>(gsrc + 4 * q);
+      for (int q = 4 * w4 + tid; q < width; q += NT) Gl[q] = gsrc[q];
+    }
+    v5_load_t<D, GATHER>(B, F, fa, gt, b, Tl, false);
+    __syncthreads();
+    {
+      // v3's S row l32 (columns k = 16h + s) and T block column n: same products, same order
+      const int n = 32 * wave + l32;
+      float sv[16], bv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = 16 * h + s, i = l32;
+        float v = 0.f;
+        if (i < F && k < F) {
+          if (i == k)
+            v = self ? 2.f * Gl[D + pair_index(i, i, true)] : 0.f;
+          else
+            v = Gl[D + (i > k ? pair_index(i, k, self) : pair_index(k, i, self))];
+        }
+        sv[s] = v;
+        bv[s] = Tl[(16 * h + s) * DP + n];
+      }
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sv[s], bv[s], acc, 0, 0, 0);
+      const bool xpos = Tl[n] > 0.f;  // row 0 of this column, read before it is overwritten
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (i < F) {
+          float v = acc[r];
+          if (i == 0) {
+            v += Gl[n];
+            if (relu_x && !xpos) v = 0.f;
+          }
+          Tl[i * DP + n] = v;
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int sw = lane / C4, c = lane - sw * C4;
+      for (int q = 0; q * RPB < F; ++q) {
+        const int i0 = q * RPB + wave * RPW, f = i0 + sw;
+        float* dst = grad_ptr_w<D>(ga, F, b, i0, sw);
+        if (f < F)
+          *reinterpret_cast<float4*>(dst + 4 * c) = *reinterpret_cast<const float4*>(Tl + f * DP + 4 * c);
       }
     }
     __syncthreads();
@@ -751,6 +968,17 @@ extern "C" int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D,
   // the elementwise one otherwise
   const bool fast = F <= 32 && (D == 16 || D == 32 || D == 64 || D == 128) &&
                     aligned_feats(fa, F);
+  if (fast && fwd_version(D) == 5) {
+    const int width = D + npairs;
+    if (D == 64)
+      hipLaunchKernelGGL((interact_dot_fwd_v5<64, false>), dim3(v5_grid(B)), dim3(128), 0, st, B, F,
+                         fa, self_interaction ? 1 : 0, out, ld_out, width, GatherArgs{});
+    else
+      hipLaunchKernelGGL((interact_dot_fwd_v5<128, false>), dim3(v5_grid(B)), dim3(256), 0, st, B,
+                         F, fa, self_interaction ? 1 : 0, out, ld_out, width, GatherArgs{});
+    DLRM_LAUNCH_CHECK(name);
+    return DLRM_OK;
+  }
   if (fast) {
     const int width = D + npairs;
     const int vec_out = ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 4 == 0) ? 1 : 0;
@@ -807,7 +1035,20 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
     if ((reinterpret_cast<uintptr_t>(ga.ptr[f]) & 15) || (ga.bs[f] & 3)) grads_aligned = false;
   if (fast && grads_aligned) {
     const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
-    if (use_v4(D)) {
+    const int ver = bwd_version(D);
+    if (ver == 5) {
+      if (D == 64)
+        hipLaunchKernelGGL((interact_dot_bwd_v5<64, false>), dim3(v5_grid(B)), dim3(128), 0, st, B,
+                           F, fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0,
+                           vec_g, GatherArgs{});
+      else
+        hipLaunchKernelGGL((interact_dot_bwd_v5<128, false>), dim3(v5_grid(B)), dim3(256), 0, st, B,
+                           F, fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0,
+                           vec_g, GatherArgs{});
+      DLRM_LAUNCH_CHECK(name);
+      return DLRM_OK;
+    }
+    if (ver == 4) {
       const int nblk = D > 32 ? D / 32 : 1, cb = D < 32 ? D : 32;
       const size_t lds = 4 * (32 * (size_t)(cb + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
       const int grid = (int)std::min<int64_t>(dlrm::ceil_div((int64_t)B * nblk, 4), 8192);
@@ -911,10 +1152,20 @@ extern "C" int dlrm_interact_dot_forward_gather(int32_t B, int32_t F, int32_t D,
   for (int f = 0; f < F; ++f) fa.ptr[f] = x, fa.bs[f] = x_bstride;
   const GatherArgs gt{weights, row_base, indices, error_flag};
   const int width = D + npairs;
+  hipStream_t st = dlrm::as_stream(stream);
+  if (fwd_version(D) == 5) {
+    if (D == 64)
+      hipLaunchKernelGGL((interact_dot_fwd_v5<64, true>), dim3(v5_grid(B)), dim3(128), 0, st, B, F,
+                         fa, self_interaction ? 1 : 0, out, ld_out, width, gt);
+    else
+      hipLaunchKernelGGL((interact_dot_fwd_v5<128, true>), dim3(v5_grid(B)), dim3(256), 0, st, B,
+                         F, fa, self_interaction ? 1 : 0, out, ld_out, width, gt);
+    DLRM_LAUNCH_CHECK(name);
+    return DLRM_OK;
+  }
   const int vec_out = ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 4 == 0) ? 1 : 0;
   const size_t lds = 4 * (32 * (size_t)(D + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
   const int grid = (int)std::min<int64_t>(dlrm::ceil_div(B, 4), 8192);
-  hipStream_t st = dlrm::as_stream(stream);
 #define L4G(DD)                                                                              \
   hipLaunchKernelGGL((interact_dot_fwd_v4<DD, true>), dim3(grid), dim3(256), lds, st, B, F, fa, \
                      self_interaction ? 1 : 0, out, ld_out, width, vec_out, gt)
@@ -954,7 +1205,20 @@ extern "C" int dlrm_interact_dot_backward_gather(
   const GatherArgs gt{weights, row_base, indices, nullptr};
   const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
   hipStream_t st = dlrm::as_stream(stream);
-  if (use_v4(D)) {
+  const int ver = bwd_version(D);
+  if (ver == 5) {
+    if (D == 64)
+      hipLaunchKernelGGL((interact_dot_bwd_v5<64, true>), dim3(v5_grid(B)), dim3(128), 0, st, B, F,
+                         fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g,
+                         gt);
+    else
+      hipLaunchKernelGGL((interact_dot_bwd_v5<128, true>), dim3(v5_grid(B)), dim3(256), 0, st, B, F,
+                         fa, self_interaction ? 1 : 0, grad_out, ld_gout, ga, relu_x ? 1 : 0, vec_g,
+                         gt);
+    DLRM_LAUNCH_CHECK(name);
+    return DLRM_OK;
+  }
+  if (ver == 4) {
     const int nblk = D > 32 ? D / 32 : 1, cb = D < 32 ? D : 32;
     const size_t lds4 = 4 * (32 * (size_t)(cb + 4) + D + 32 * 33 / 2 + 4) * sizeof(float);
     const int grid4 = (int)std::min<int64_t>(dlrm::ceil_div((int64_t)B * nblk, 4), 8192);

@@ -79,7 +79,7 @@ class DeferredErrorCheck:
 
 # dlrm_tune_key (include/dlrm_hip.h): plan overrides for sweeps and coverage tests
 TUNE_KEYS = {"gemm_tile": 1, "gemm_split": 2, "tbe_block": 3, "tbe_sort": 4, "tbe_lean": 5,
-             "interact_bwd": 6}
+             "interact_bwd": 6, "interact_fwd": 7}
 
 
 class tuning:

@@ -124,15 +124,20 @@ const char* dlrm_last_error(void);
  *   DLRM_TUNE_TBE_LEAN   : 1 = the non-deferred backward's update passes as the
  *                          16-rows-in-flight kernels even where the lean ones apply (ABI v6)
  *   DLRM_TUNE_INTERACT_BWD : the dot-interaction backward's kernel: 3 = one wave per sample
- *                          (v3), 4 = one wave per sample x 32-column block (v4); default v4
- *                          for D <= 32, v3 above (ABI v6) */
+ *                          (v3), 4 = one wave per sample x 32-column block (v4), 5 = one
+ *                          workgroup per sample, a wave per 32-column block (v5, D >= 64);
+ *                          default v4 for D <= 32, v5 above (ABI v6; v5 in v7)
+ *   DLRM_TUNE_INTERACT_FWD : the dot-interaction forward's kernel: 4 = one wave per sample
+ *                          (v4), 5 = one workgroup per sample (v5, D >= 64; default there)
+ *                          (ABI v7) */
 enum dlrm_tune_key {
   DLRM_TUNE_GEMM_TILE = 1,
   DLRM_TUNE_GEMM_SPLIT = 2,
   DLRM_TUNE_TBE_BLOCK = 3,
   DLRM_TUNE_TBE_SORT = 4,
   DLRM_TUNE_TBE_LEAN = 5,
-  DLRM_TUNE_INTERACT_BWD = 6
+  DLRM_TUNE_INTERACT_BWD = 6,
+  DLRM_TUNE_INTERACT_FWD = 7
 };
 int dlrm_set_tuning(int32_t key, int64_t value);
 int64_t dlrm_get_tuning(int32_t key);

@@ -880,8 +880,9 @@ def test_interact_backward_relu_x_and_paths(ops, path, D):
 @pytest.mark.parametrize("gather", [False, True])
 def test_interact_backward_v4_matches_v3(ops, D, F, self_int, gather):
     """The interaction backward as one wave per sample x 32-column block (v4, forced by
-    DLRM_TUNE_INTERACT_BWD = 4; the default for D <= 32) vs one wave per sample (v3, forced
-    by 3; the default above) and the default pick: bitwise the same gradients -
+    DLRM_TUNE_INTERACT_BWD = 4; the default for D <= 32), one wave per sample (v3, forced
+    by 3), one workgroup per sample with a wave per column block (v5, forced by 5; the
+    default for D >= 64) and the default pick: bitwise the same gradients -
     every element is the same 32-deep MFMA sum - pooled and gather-fused, ReLU' of x fused,
     a ragged batch (B = 203) and strided x."""
     torch.manual_seed(D * 10 + F)
@@ -896,7 +897,7 @@ def test_interact_backward_v4_matches_v3(ops, D, F, self_int, gather):
     npairs = F * (F + 1) // 2 if self_int else F * (F - 1) // 2
     gR = torch.randn(B, D + npairs, device=dev)
     res = []
-    for v in (4, 3, 0):
+    for v in (4, 3, 5, 0):
         with ops.tuning(interact_bwd=v):
             if gather:
                 g = ops.interact_backward_gather(x, W, row_base, idx, gR, self_int, relu_x=True)
@@ -907,6 +908,40 @@ def test_interact_backward_v4_matches_v3(ops, D, F, self_int, gather):
     for other in res[1:]:
         for a, b in zip(res[0], other):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("F,self_int", [(2, False), (9, True), (27, False), (32, False)])
+@pytest.mark.parametrize("gather", [False, True])
+def test_interact_forward_v5_matches_v4_and_reference(ops, D, F, self_int, gather):
+    """The interaction forward as one workgroup per sample (v5: a wave per 32-column block,
+    the partial Gram matrices added in LDS; the default for D >= 64) vs one wave per sample
+    (v4, forced by DLRM_TUNE_INTERACT_FWD = 4) and a torch fp64 bmm + tril reference:
+    within the fp32 bound (the k sum is split into blocks), pooled and gather-fused, a
+    ragged batch (B = 203) and strided x."""
+    torch.manual_seed(D * 7 + F)
+    T, B = F - 1, 203
+    rows = [int(r) for r in torch.randint(1, 500, (T,))]
+    row_base = torch.tensor([0] + list(np.cumsum(rows)), dtype=torch.int64, device=dev)
+    W = torch.randn(int(row_base[-1]), D, device=dev)
+    idx = torch.cat([torch.randint(0, n, (B,)) for n in rows]).to(torch.int32).to(dev)
+    off = torch.arange(T * B + 1, dtype=torch.int32, device=dev)
+    x = torch.randn(B, D + 4, device=dev)[:, :D]
+    E = ops.tbe_forward(W, row_base, T, B, idx, off)
+    Tm = torch.cat([x[:, None, :], E], 1).double()
+    Z = torch.bmm(Tm, Tm.transpose(1, 2))
+    li, lj = torch.tril_indices(F, F, 0 if self_int else -1)
+    ref = torch.cat([x.double(), Z[:, li, lj]], 1).cpu().numpy()
+    outs = []
+    for v in (4, 5, 0):
+        with ops.tuning(interact_fwd=v):
+            R = ops.interact_forward_gather(x, W, row_base, idx, self_int) if gather else \
+                ops.interact_forward("dot", x, E, self_int)
+        torch.cuda.synchronize()
+        outs.append(R.cpu())
+        ok, msg = fp32_close(R.cpu().numpy(), ref)
+        assert ok, (v, msg)
+    assert torch.equal(outs[1], outs[2])  # v5 is the default
 
 
 def _mlp_ref(X, layers):
