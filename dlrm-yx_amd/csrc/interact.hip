@@ -478,18 +478,25 @@ __global__ __launch_bounds__(256) void interact_dot_bwd_v3(int B, int F, FeatArg
 // rebuilds S and re-reads dR - so it is the default only for D <= 32 (one wave per sample);
 // tuning INTERACT_BWD = 3 / 4 forces v3 / v4.
 // Backward kernel for the compile-time D (tuning INTERACT_BWD: 3 / 4 / 5 forces v3 / v4 /
-// v5; default v4 for D <= 32, v5 above); forward (INTERACT_FWD: 4 / 5; default v5 for
-// D >= 64).
-inline int bwd_version(int D) {
+// v5; default v4 for D <= 32, above v5 for short batches, v3 for long ones); forward
+// (INTERACT_FWD: 4 / 5; default v5 for D >= 64 and short batches).
+// v5 pays where the batch is short against the chip (<= kV5MaxBatch samples: B = 256 C3
+// step 181.4 -> 172.8 us, forward 9.7 -> 5.9 us, backward 15.2 -> 10.0 us); at B = 2048 its
+// four times as many waves lose (forward 14.3 -> 16.2 us, backward 21.0 -> 26.3 us), so v4 /
+// v3 keep the long batches (profiles/r05_interact_v5_ab.txt).
+constexpr int64_t kV5MaxBatch = 1024;
+inline int bwd_version(int D, int64_t B) {
   const int t = (int)dlrm::tuning(DLRM_TUNE_INTERACT_BWD);
   if (t == 3 || t == 4) return t;
   if (t == 5) return D >= 64 ? 5 : 4;
-  return D <= 32 ? 4 : 5;
+  if (D <= 32) return 4;
+  return B <= kV5MaxBatch ? 5 : 3;
 }
-inline int fwd_version(int D) {
+inline int fwd_version(int D, int64_t B) {
   const int t = (int)dlrm::tuning(DLRM_TUNE_INTERACT_FWD);
   if (t == 4) return 4;
-  return D >= 64 ? 5 : 4;
+  if (t == 5) return D >= 64 ? 5 : 4;
+  return D >= 64 && B <= kV5MaxBatch ? 5 : 4;
 }
 inline int v5_grid(int64_t B) { return (int)std::min<int64_t>(B, 16384); }
 
@@ -968,7 +975,7 @@ extern "C" int dlrm_interact_dot_forward(int32_t B, int32_t F, int32_t D,
   // the elementwise one otherwise
   const bool fast = F <= 32 && (D == 16 || D == 32 || D == 64 || D == 128) &&
                     aligned_feats(fa, F);
-  if (fast && fwd_version(D) == 5) {
+  if (fast && fwd_version(D, B) == 5) {
     const int width = D + npairs;
     if (D == 64)
       hipLaunchKernelGGL((interact_dot_fwd_v5<64, false>), dim3(v5_grid(B)), dim3(128), 0, st, B, F,
@@ -1035,7 +1042,7 @@ extern "C" int dlrm_interact_dot_backward(int32_t B, int32_t F, int32_t D,
     if ((reinterpret_cast<uintptr_t>(ga.ptr[f]) & 15) || (ga.bs[f] & 3)) grads_aligned = false;
   if (fast && grads_aligned) {
     const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
-    const int ver = bwd_version(D);
+    const int ver = bwd_version(D, B);
     if (ver == 5) {
       if (D == 64)
         hipLaunchKernelGGL((interact_dot_bwd_v5<64, false>), dim3(v5_grid(B)), dim3(128), 0, st, B,
@@ -1153,7 +1160,7 @@ extern "C" int dlrm_interact_dot_forward_gather(int32_t B, int32_t F, int32_t D,
   const GatherArgs gt{weights, row_base, indices, error_flag};
   const int width = D + npairs;
   hipStream_t st = dlrm::as_stream(stream);
-  if (fwd_version(D) == 5) {
+  if (fwd_version(D, B) == 5) {
     if (D == 64)
       hipLaunchKernelGGL((interact_dot_fwd_v5<64, true>), dim3(v5_grid(B)), dim3(128), 0, st, B, F,
                          fa, self_interaction ? 1 : 0, out, ld_out, width, gt);
@@ -1205,7 +1212,7 @@ extern "C" int dlrm_interact_dot_backward_gather(
   const GatherArgs gt{weights, row_base, indices, nullptr};
   const int vec_g = ((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_gout % 4 == 0) ? 1 : 0;
   hipStream_t st = dlrm::as_stream(stream);
-  const int ver = bwd_version(D);
+  const int ver = bwd_version(D, B);
   if (ver == 5) {
     if (D == 64)
       hipLaunchKernelGGL((interact_dot_bwd_v5<64, true>), dim3(v5_grid(B)), dim3(128), 0, st, B, F,

@@ -242,6 +242,11 @@ class DLRMTrainer:
         self.bot_sched = "auto"
         # one GPU: the bottom MLP forward as a role of the lookup launch (mlp_rows.hpp)
         self.fuse_bottom = True
+        # several GPUs: the bottom MLP forward as a role of the lookup launch too (True), or
+        # as its own chain launch beside the in-flight all-to-all (False).  The emulated
+        # W = 8 rank 2 step: 16.3 us of chain launch -> a few us inside the lookup launch;
+        # the cost is the all-to-all starting after the (longer) fused launch
+        self.dist_bottom_in_lookup = True
         # one GPU, one-hot batches: the dot interaction gathers the embedding rows itself
         # (dlrm_interact_dot_forward_gather); the lookup launch keeps only its sort role
         self.fuse_gather = True
@@ -636,11 +641,16 @@ class DLRMTrainer:
                     out = bufs["P"] if self.qr_active else bufs["E"]
                 if self.T_local > 0 and presort:
                     # the backward's per-table sort runs inside the lookup launch (alone,
-                    # when the interaction gathers the rows itself)
+                    # when the interaction gathers the rows itself); several GPUs: with the
+                    # bottom MLP forward as a third role (dist_bottom_in_lookup)
+                    chain = self._bottom_chain(batch, bufs) if dist and profile is None and \
+                        self.dist_bottom_in_lookup else None
+                    st["bottom_done"] = chain is not None
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
                                             batch.max_per_table, out=None if gather else out,
-                                            error_flag=self.tbe_error_flag, lookup=not gather)
+                                            error_flag=self.tbe_error_flag, bottom=chain,
+                                            lookup=not gather)
                 elif self.T_local > 0:
                     ops.tbe_forward(self.weights, self.row_base, self.T_phys, B, idx, off,
                                     out=out, error_flag=self.tbe_error_flag)
@@ -649,6 +659,8 @@ class DLRMTrainer:
 
         def bottom_fwd():
             h = batch.X
+            if st.pop("bottom_done", False):  # ran inside the lookup launch
+                return
             with record_function("module::forward_pass::bottom_mlp"):
                 if dist and profile is None:
                     # several GPUs: the bottom MLP as one row-block chain launch (activations

@@ -126,9 +126,11 @@ const char* dlrm_last_error(void);
  *   DLRM_TUNE_INTERACT_BWD : the dot-interaction backward's kernel: 3 = one wave per sample
  *                          (v3), 4 = one wave per sample x 32-column block (v4), 5 = one
  *                          workgroup per sample, a wave per 32-column block (v5, D >= 64);
- *                          default v4 for D <= 32, v5 above (ABI v6; v5 in v7)
+ *                          default v4 for D <= 32; above, v5 for batches <= 1024, else v3
+ *                          (ABI v6; v5 in v7)
  *   DLRM_TUNE_INTERACT_FWD : the dot-interaction forward's kernel: 4 = one wave per sample
- *                          (v4), 5 = one workgroup per sample (v5, D >= 64; default there)
+ *                          (v4), 5 = one workgroup per sample (v5, D >= 64; default there
+ *                          for batches <= 1024)
  *                          (ABI v7) */
 enum dlrm_tune_key {
   DLRM_TUNE_GEMM_TILE = 1,

@@ -579,7 +579,7 @@ def test_module_distributed_forward_matches_reference_gloo_run(W, sharder):
             assert ok, (r, name, msg)
 
 
-def _nccl_one_rank_worker(port, q, graph):
+def _nccl_one_rank_worker(port, q, graph, in_lookup=True):
     """One process: the single-GPU schedule and the multi-GPU schedule (force_dist: the
     all-to-all, the gradient buckets and their all-reduces over a 1-rank RCCL group) from
     the same weights on the same C3-width batches."""
@@ -597,6 +597,7 @@ def _nccl_one_rank_worker(port, q, graph):
         for name, kw in (("single", {}),
                          ("nccl", dict(force_dist=True, process_group=dist.group.WORLD))):
             tr = DLRMTrainer.from_oracle(cfg, _c3_model(), device=dev, **kw)
+            tr.dist_bottom_in_lookup = in_lookup
             assert tr.distributed == (name == "nccl")
             bs = [tr.make_batch(*b) for b in _c3_batches(128, 3)]
             res = {"Z": [], "E": []}
@@ -624,10 +625,11 @@ def _nccl_one_rank_worker(port, q, graph):
         q.put(traceback.format_exc())
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_multi_gpu_schedule_on_one_rank_rccl_matches_single_gpu(graph):
-    """The multi-GPU step (distributed_forward's schedule: lookup -> all-to-all || bottom
-    chain -> interaction -> top MLP -> top-bucket all-reduce -> interaction backward ->
+@pytest.mark.parametrize("graph,in_lookup", [(False, True), (True, True), (True, False)])
+def test_multi_gpu_schedule_on_one_rank_rccl_matches_single_gpu(graph, in_lookup):
+    """The multi-GPU step (distributed_forward's schedule: lookup (+ the bottom MLP as a role
+    of its launch, or as a chain launch beside the all-to-all) -> all-to-all -> interaction
+    -> top MLP -> top-bucket all-reduce -> interaction backward ->
     reverse all-to-all || bottom backward -> bottom-bucket all-reduce -> embedding update ->
     dense update) forced on a 1-rank nccl (RCCL) group, eager and with its kernel segments
     replayed from hipGraphs around the collectives, against the single-GPU schedule from
@@ -636,7 +638,8 @@ def test_multi_gpu_schedule_on_one_rank_rccl_matches_single_gpu(graph):
     from conftest import fp32_close
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_nccl_one_rank_worker, args=(_free_port(), q, graph), daemon=True)
+    p = ctx.Process(target=_nccl_one_rank_worker, args=(_free_port(), q, graph, in_lookup),
+                    daemon=True)
     p.start()
     out = q.get(timeout=300)
     p.join(timeout=60)

@@ -917,8 +917,8 @@ def test_interact_forward_v5_matches_v4_and_reference(ops, D, F, self_int, gathe
     """The interaction forward as one workgroup per sample (v5: a wave per 32-column block,
     the partial Gram matrices added in LDS; the default for D >= 64) vs one wave per sample
     (v4, forced by DLRM_TUNE_INTERACT_FWD = 4) and a torch fp64 bmm + tril reference:
-    within the fp32 bound (the k sum is split into blocks), pooled and gather-fused, a
-    ragged batch (B = 203) and strided x."""
+    within 1e-5 plus the D-term accumulation bound (the k sum is split into blocks), pooled
+    and gather-fused, a ragged batch (B = 203) and strided x."""
     torch.manual_seed(D * 7 + F)
     T, B = F - 1, 203
     rows = [int(r) for r in torch.randint(1, 500, (T,))]
@@ -930,8 +930,12 @@ def test_interact_forward_v5_matches_v4_and_reference(ops, D, F, self_int, gathe
     E = ops.tbe_forward(W, row_base, T, B, idx, off)
     Tm = torch.cat([x[:, None, :], E], 1).double()
     Z = torch.bmm(Tm, Tm.transpose(1, 2))
+    Za = torch.bmm(Tm.abs(), Tm.abs().transpose(1, 2))
     li, lj = torch.tril_indices(F, F, 0 if self_int else -1)
     ref = torch.cat([x.double(), Z[:, li, lj]], 1).cpu().numpy()
+    # fp32 vs fp64: 1e-5 plus the standard D-term accumulation bound 2 D u |T| |T|^T
+    acc = torch.cat([torch.zeros_like(x.double()), Za[:, li, lj]], 1).cpu().numpy()
+    lim = 1e-5 * np.maximum(1.0, np.abs(ref)) + 2 * D * 2.0 ** -24 * acc
     outs = []
     for v in (4, 5, 0):
         with ops.tuning(interact_fwd=v):
@@ -939,8 +943,8 @@ def test_interact_forward_v5_matches_v4_and_reference(ops, D, F, self_int, gathe
                 ops.interact_forward("dot", x, E, self_int)
         torch.cuda.synchronize()
         outs.append(R.cpu())
-        ok, msg = fp32_close(R.cpu().numpy(), ref)
-        assert ok, (v, msg)
+        err = np.abs(R.cpu().numpy() - ref)
+        assert (err <= lim).all(), (v, float((err - lim).max()))
     assert torch.equal(outs[1], outs[2])  # v5 is the default
 
 
