@@ -13,8 +13,9 @@
 //    them with wave shuffles (ds_bpermute), four row fetches in flight per lane;
 //  * 64-bit row bases (a 54 M x 128 table set is 6.9e9 elements);
 //  * backward (tbe_bwd.hip): stable radix sort of (global row, lookup) pairs, fixed
-//    64-lookup blocks summed per run of equal rows, partials combined in block order;
-//    every weight row read and written once — bitwise reproducible.
+//    blocks of 16 lookups (64 from 2^18 lookups per call) summed per run of equal rows,
+//    partials combined in block order; every weight row read and written once — bitwise
+//    reproducible.
 #include "tbe_common.hpp"
 
 namespace {

@@ -8,7 +8,8 @@
 //  1. keys:    per lookup l, global row row_base[t] + idx[l] (or a sentinel) and its bag;
 //  2. sort:    stable LSD radix sort of (row, l) pairs on ceil(log2 rows) bits (hand-written:
 //              per-table LDS sort, tiled per-table passes, or device-wide passes; below);
-//  3. blocks:  the sorted lookups are cut into fixed blocks of 64.  One lane-group per
+//  3. blocks:  the sorted lookups are cut into fixed blocks (16 lookups; 64 from 2^18
+//              lookups per call, tbe_bwd_roles.hpp CH / kLongCH).  One lane-group per
 //              block walks them in order (row ids / grad-row offsets loaded coalesced and
 //              broadcast by wave shuffles, four gradient rows in flight), summing the
 //              gradient of each run of equal rows.  A run that starts and ends inside
