@@ -82,13 +82,32 @@ struct GemmGroup {
   int total;  // blocks in the launch
 };
 
+// Row swizzle of a k-contiguous [mn][32] LDS image (16-B chunk c of row r stored at chunk
+// c ^ swz_kc(r)): the 16-lane groups of a fragment's ds_read_b128 (lanes l16 x k-quarter kq,
+// chunks 2kq + h) then cover all 64 banks.  An mn-contiguous [32][MN] image flips bit 4 of
+// mn on k-rows 8..15 and 24..31 instead (the two k-quarters of a ds_read_b32 half-wave land
+// on opposite 16-bank halves).
+__device__ __forceinline__ int swz_kc(int r) {
+  return ((r >> 1) & 7) ^ (((unsigned)((r & 15) - 4) < 8u) ? 2 : 0);
+}
+
 // One operand's (MN x BKT) panel, staged global -> registers -> LDS.
 //   KC  : X(mn, k) = X[mn*ld + k]  -> LDS [mn][BKT + 4]   (fragments: ds_read_b128)
 //   !KC : X(mn, k) = X[k*ld + mn]  -> LDS [BKT][MN + 4]   (fragments: ds_read_b32)
-template <int MN, int BKT, bool KC, bool VEC, int NT>
+// SWZ (BKT = 32, MN >= 32): unpadded and swizzled as above - no bank conflicts in the
+// fragment reads of the pipelined body (the padded images read 2-way conflicted: +4 % on
+// the C3 step, profiles/r05_gemm_swizzle_ab.txt).
+template <int MN, int BKT, bool KC, bool VEC, int NT, bool SWZ = false>
 struct Stage {
-  static constexpr int PITCH = KC ? BKT + 4 : MN + 4;
+  static_assert(!SWZ || (BKT == 32 && MN >= 32), "swizzled images: BKT 32, MN >= 32");
+  static constexpr int PITCH = SWZ ? (KC ? BKT : MN) : (KC ? BKT + 4 : MN + 4);
   static constexpr int SIZE = KC ? MN * PITCH : BKT * PITCH;  // floats per LDS buffer
+  // float offset of element (mn, k) in the image (KC: k % 4 == 0 addresses a whole chunk)
+  __device__ __forceinline__ static int at(int mn, int k) {
+    if constexpr (!SWZ) return KC ? mn * PITCH + k : k * PITCH + mn;
+    else if constexpr (KC) return mn * PITCH + 4 * ((k >> 2) ^ swz_kc(mn)) + (k & 3);
+    else return k * PITCH + (mn ^ (((k >> 3) & 1) << 4));
+  }
   static constexpr int NV = MN * BKT / 4 / NT;               // float4 per thread
   static_assert(NV >= 1 && MN * BKT % (4 * NT) == 0, "panel / thread mismatch");
   float4 regs[NV];
@@ -203,21 +222,16 @@ struct Stage {
     regs[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
   }
 
+  // (!KC: a float4 is a 4-aligned mn run, which the bit-4 flip keeps contiguous)
   __device__ __forceinline__ void store_one(int v, float* __restrict__ lds, int tid) const {
     int mn, k;
     coords(tid + v * NT, mn, k);
-    float* dst = KC ? lds + mn * PITCH + k : lds + k * PITCH + mn;
-    *reinterpret_cast<float4*>(dst) = regs[v];
+    *reinterpret_cast<float4*>(lds + at(mn, k)) = regs[v];
   }
 
   __device__ __forceinline__ void store(float* __restrict__ lds, int tid) const {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      int mn, k;
-      coords(tid + v * NT, mn, k);
-      float* dst = KC ? lds + mn * PITCH + k : lds + k * PITCH + mn;
-      *reinterpret_cast<float4*>(dst) = regs[v];
-    }
+    for (int v = 0; v < NV; ++v) store_one(v, lds, tid);
   }
 
   // NS consecutive k-steps (k = kbase .. kbase+NS-1) of the 32-wide sub-tile at `off`
@@ -227,10 +241,9 @@ struct Stage {
                                        float (&f)[NS]) const {
     static_assert(NS % 4 == 0, "fragment length");
     if constexpr (KC) {
-      const float* p = lds + (off + l32) * PITCH + kbase;
 #pragma unroll
       for (int c = 0; c < NS / 4; ++c) {
-        const float4 v = *reinterpret_cast<const float4*>(p + 4 * c);
+        const float4 v = *reinterpret_cast<const float4*>(lds + at(off + l32, kbase + 4 * c));
         f[4 * c + 0] = v.x;
         f[4 * c + 1] = v.y;
         f[4 * c + 2] = v.z;
@@ -238,7 +251,7 @@ struct Stage {
       }
     } else {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) f[s] = lds[(kbase + s) * PITCH + off + l32];
+      for (int s = 0; s < NS; ++s) f[s] = lds[at(off + l32, kbase + s)];
     }
   }
 };
@@ -458,8 +471,8 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(FM >= 1 && FN >= 1, "wave sub-tile");
   constexpr int KL = kBK / 4;  // k-steps per K-tile (each lane group owns KL consecutive k)
-  using SA = Stage<BM, kBK, A_KC, true, NT>;
-  using SB = Stage<BN, kBK, B_KC, true, NT>;
+  using SA = Stage<BM, kBK, A_KC, true, NT, true>;
+  using SB = Stage<BN, kBK, B_KC, true, NT, true>;
   constexpr int NS = SA::NV + SB::NV;  // staged float4 per thread per K-tile
   static_assert(NS <= KL - 1, "staging must finish before the barrier step");
 
@@ -634,9 +647,9 @@ __device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
 
 template <int BM, int BN>
 constexpr int group_smem_floats() {
-  // the largest LDS image over the four operand layouts (double-buffered A and B panels)
-  return 2 * ((BM * (kBK + 4) > kBK * (BM + 4) ? BM * (kBK + 4) : kBK * (BM + 4)) +
-              (BN * (kBK + 4) > kBK * (BN + 4) ? BN * (kBK + 4) : kBK * (BN + 4)));
+  // double-buffered A and B panels (unpadded swizzled images: the same size for every
+  // operand layout)
+  return 2 * (BM + BN) * kBK;
 }
 
 // Body kinds: the four operand layouts, plus 4 = layout 2 (wgrad) with the row sums.
