@@ -674,7 +674,7 @@ def main():
                          "steps, so the clocks have left their idle state (tools/ramp_probe.py)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraphs")
     ap.add_argument("--bot-sched", default="", help="A/B: bottom-MLP backward schedule "
-                    "(partial | full | chain | auto; default: the trainer's)")
+                    "(partial | full | auto; default: the trainer's)")
     ap.add_argument("--tbe-role", type=int, default=-1, help="A/B: 1 = the embedding update's "
                     "passes ride on the bottom-backward GEMM launches, 0 = own launches "
                     "(default: the trainer's)")

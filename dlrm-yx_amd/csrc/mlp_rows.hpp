@@ -57,10 +57,8 @@ struct MlpChain {
 // reads as zeros, so a fetched register is never touched before its MFMA.
 constexpr int kMlpRing = 8;
 
-// TW (the backward's data gradient): B[k][col] = W[k][col] (W used transposed: the k of
-// the product is W's row), four dword loads per chunk instead of one float4.
 // Tiles tb + wave + j * kMlpWaves (j < NTW).
-template <int NTW, bool TW = false>
+template <int NTW>
 __device__ __forceinline__ void mlp_kloop(mlp_f32x4 (&acc)[kMlpTiles], const float* in,
                                           __amdgpu_buffer_rsrc_t rw, int tb, int wave, int n,
                                           int kp, int64_t ldw, int nch, int l16, int kq) {
@@ -69,18 +67,8 @@ __device__ __forceinline__ void mlp_kloop(mlp_f32x4 (&acc)[kMlpTiles], const flo
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int col = (tb + wave + j * NW) * 16 + l16, k = c * 16 + 4 * kq;
-      if constexpr (TW) {
-        float e[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int off = (col < n && k + u < kp) ? (int)(((k + u) * ldw + col) * 4) : 0x7ffffff0;
-          e[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, off, 0, 0));
-        }
-        bv[j] = make_float4(e[0], e[1], e[2], e[3]);
-      } else {
-        const int off = (col < n && k < kp) ? (int)((col * ldw + k) * 4) : 0x7ffffff0;
-        bv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0));
-      }
+      const int off = (col < n && k < kp) ? (int)((col * ldw + k) * 4) : 0x7ffffff0;
+      bv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0));
     }
   };
   auto lda = [&](int c) {
@@ -227,88 +215,6 @@ __device__ __forceinline__ void mlp_rows_body(const MlpChain& mc, int64_t blk, f
       for (int e = tid; e < RB * extra; e += NT) {
         const int r = e / extra, c = n + (e - r * extra);
         nx[r * P + c] = c == n ? 1.f : 0.f;
-      }
-    }
-    __syncthreads();
-    float* t = in;
-    in = nx;
-    nx = t;
-  }
-}
-
-// Row-block data-gradient chain: the bottom MLP backward's dgrads (the autograd of
-// apply_mlp's Linear+ReLU stack, dlrm_s_pytorch.py:518-524) for 16 samples per workgroup,
-// every layer in one pass with the gradients kept in LDS.  G_{L-1} (dLoss/d the last
-// layer's pre-activation, already masked by its ReLU') comes in; for l = L-1 .. 1,
-// G_{l-1} = (G_l . W_l[:, :out_width[l-1]]) * (Y_{l-1} > 0) goes to the caller's buffer
-// (the weight-gradient GEMMs read it) and to LDS as the next layer's input.  The weights
-// are read transposed (mlp_kloop<TW>): k runs over W_l's rows.
-struct MlpGrad {
-  const float* Glast;
-  int64_t ldgl;
-  float* G[DLRM_MLP_MAX_LAYERS];
-  int64_t ldg[DLRM_MLP_MAX_LAYERS];
-};
-
-__device__ __forceinline__ void mlp_rows_bwd_body(const MlpChain& mc, const MlpGrad& mg,
-                                                  int64_t blk, float* lds) {
-  constexpr int RB = kMlpRows, P = kMlpPitch, NW = kMlpWaves, MT = kMlpTiles;
-  constexpr int NT = NW * 64;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kq = lane >> 4, l16 = lane & 15;
-  const int64_t r0 = blk * RB;
-  const int L = mc.layers;
-  float* in = lds;
-  float* nx = lds + RB * P;
-  {  // G_{L-1} rows, zero-padded to a multiple of 16 columns
-    const int n = mc.nout[L - 1], kr = (n + 15) & ~15;
-    for (int e = tid; e < RB * kr; e += NT) {
-      const int r = e / kr, c = e - r * kr;
-      in[r * P + c] = (r0 + r < mc.rows && c < n) ? mg.Glast[(r0 + r) * mg.ldgl + c] : 0.f;
-    }
-  }
-  __syncthreads();
-  for (int l = L - 1; l >= 1; --l) {
-    const int kdim = mc.nout[l], ncols = mc.nout[l - 1];
-    const int nch = (kdim + 15) / 16, ntile = (ncols + 15) / 16;
-    const float* W = mc.W[l];
-    const int64_t ldw = mc.ldw[l];
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)W, (short)0, (int)(((int64_t)(kdim - 1) * ldw + ncols) * 4), 0x00020000);
-    mlp_f32x4 acc[MT];
-#pragma unroll
-    for (int j = 0; j < MT; ++j) acc[j] = mlp_f32x4{0.f, 0.f, 0.f, 0.f};
-    const int nt_w = ntile > wave ? (ntile - wave + NW - 1) / NW : 0;
-    switch (nt_w) {
-      case 1: mlp_kloop<1, true>(acc, in, rw, 0, wave, ncols, kdim, ldw, nch, l16, kq); break;
-      case 2: mlp_kloop<2, true>(acc, in, rw, 0, wave, ncols, kdim, ldw, nch, l16, kq); break;
-      default: break;
-    }
-    // epilogue: ReLU' of layer l-1's output (its forward activation Y_{l-1})
-    const float* Y = mc.Y[l - 1];
-    const int64_t ldy = mc.ldy[l - 1];
-    float* G = mg.G[l - 1];
-    const int64_t ldg = mg.ldg[l - 1];
-#pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      const int col = (wave + j * NW) * 16 + l16;
-      if (col < ncols) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 4 * kq + r;
-          const bool ok = r0 + row < mc.rows;
-          const float v = (ok && Y[(r0 + row) * ldy + col] > 0.f) ? acc[j][r] : 0.f;
-          nx[row * P + col] = v;
-          if (ok) G[(r0 + row) * ldg + col] = v;
-        }
-      }
-    }
-    if (l > 1) {  // zeros to the 16-column boundary (the next layer's k chunks)
-      const int kr = (ncols + 15) & ~15, extra = kr - ncols;
-      for (int e = tid; e < RB * extra; e += NT) {
-        const int r = e / extra, c = ncols + (e - r * extra);
-        nx[r * P + c] = 0.f;
       }
     }
     __syncthreads();

@@ -166,11 +166,6 @@ __global__ __launch_bounds__(kMlpWaves * 64) void mlp_chain_kernel(const MlpChai
   mlp_rows_body(mc, blockIdx.x, lds);
 }
 
-__global__ __launch_bounds__(kMlpWaves * 64) void mlp_chain_bwd_kernel(const MlpChain mc,
-                                                                       const MlpGrad mg) {
-  __shared__ __attribute__((aligned(16))) float lds[kMlpLdsFloats];
-  mlp_rows_bwd_body(mc, mg, blockIdx.x, lds);
-}
 
 
 // The per-table LDS sort applies (and dlrm_tbe_forward_presort can run it early).
@@ -1303,30 +1298,6 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
 extern "C" int dlrm_mlp_chain_supported(const dlrm_mlp_chain* chain) {
   MlpChain mc{};
   return mlp_chain_prepare(chain, mc);
-}
-
-extern "C" int dlrm_mlp_chain_backward(const dlrm_mlp_chain* chain, const float* g_last,
-                                       int64_t ld_g_last, float* const* g, const int64_t* ld_g,
-                                       dlrm_stream_t stream) {
-  const char* name = "dlrm_mlp_chain_backward";
-  MlpChain mc{};
-  DLRM_ARG(mlp_chain_prepare(chain, mc), "%s: unsupported chain", name);
-  if (chain->rows == 0 || chain->layers < 2) return DLRM_OK;
-  DLRM_ARG(g_last && ld_g_last >= chain->out_width[chain->layers - 1], "%s: bad g_last", name);
-  DLRM_ARG(g && ld_g, "%s: null gradient arrays", name);
-  MlpGrad mg{};
-  mg.Glast = g_last;
-  mg.ldgl = ld_g_last;
-  for (int l = 0; l + 1 < chain->layers; ++l) {
-    DLRM_ARG(g[l] && ld_g[l] >= chain->out_width[l], "%s: bad gradient buffer %d", name, l);
-    DLRM_ARG(g[l] != g_last, "%s: gradient buffer %d aliases g_last", name, l);
-    mg.G[l] = g[l];
-    mg.ldg[l] = ld_g[l];
-  }
-  hipLaunchKernelGGL(mlp_chain_bwd_kernel, dim3((unsigned)dlrm::ceil_div(chain->rows, kMlpRows)),
-                     dim3(kMlpWaves * 64), 0, dlrm::as_stream(stream), mc, mg);
-  DLRM_LAUNCH_CHECK(name);
-  return DLRM_OK;
 }
 
 extern "C" int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream) {

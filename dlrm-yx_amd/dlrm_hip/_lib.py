@@ -86,7 +86,6 @@ SIGNATURES = {
     "dlrm_tbe_forward_rows": (c_int32, [P, c_int32, c_int64, c_int64, P, c_int32, c_int32, P,
                                         c_int32, P, c_int32, P, P, c_int64, P, P]),
     "dlrm_mlp_chain_forward": (c_int32, [P, P]),
-    "dlrm_mlp_chain_backward": (c_int32, [P, P, c_int64, P, P, P]),
     "dlrm_tbe_expand_grad": (c_int32, [c_int64, c_int32, c_int32, P, c_int32, c_int64, P, P,
                                        c_int64, P, P]),
     "dlrm_qr_split_indices": (c_int32, [P, c_int32, c_int64, c_int64, P, P, P]),

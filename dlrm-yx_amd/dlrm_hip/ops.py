@@ -218,22 +218,6 @@ def mlp_chain_forward(chain, device=None) -> None:
               _stream(dev))
 
 
-def mlp_chain_backward(chain, g_last: torch.Tensor, grads, device=None) -> None:
-    """dlrm_mlp_chain_backward: the chain's data gradients in one launch.  ``g_last``:
-    dLoss/d(pre-activation of the last layer) [rows, >= out_width[-1]]; ``grads``: L-1
-    output tensors [rows, >= out_width[l]] (g_0 .. g_{L-2})."""
-    _check_cuda(g_last, *grads)
-    L = int(chain.layers)
-    if len(grads) != L - 1:
-        raise ValueError(f"mlp_chain_backward: {L - 1} gradient buffers expected")
-    ptrs = (ctypes.c_void_p * max(L - 1, 1))(*[g.data_ptr() for g in grads])
-    lds = (ctypes.c_int64 * max(L - 1, 1))(*[g.stride(0) for g in grads])
-    dev = device if device is not None else g_last.device
-    _lib.call("dlrm_mlp_chain_backward", ctypes.cast(ctypes.byref(chain), ctypes.c_void_p),
-              _p(g_last), g_last.stride(0), ctypes.cast(ptrs, ctypes.c_void_p),
-              ctypes.cast(lds, ctypes.c_void_p), _stream(dev))
-
-
 # the TBE backward's sort keys are 32-bit global rows (ABI v4): a table set that one
 # backward call serves must hold fewer rows (checked where tables are built, so a forward
 # is never accepted for a configuration the backward would refuse)

@@ -233,12 +233,12 @@ class DLRMTrainer:
         self.group_wgrad = True
         self.full_last_wgrad = False
         # bottom-MLP backward schedule: "partial" (split wgrads reduced in the next launch),
-        # "full" (in-launch split-K, n_bot launches; bottom_bwd_full), "chain" (the data
-        # gradients in one row-block launch, then every wgrad in one grouped launch) or
-        # "auto": full at <= 128 rows per GPU, else partial (measured, one MI355X: full
-        # 0.976 vs partial 0.857 M samples/s at the Kaggle shape, B = 128; partial ahead at
-        # C3 B = 2048, 4.67 vs 4.54 M, and at B = 256, 1.21 vs 1.19 M;
-        # profiles/r04_bot_sched_ab.txt)
+        # "full" (in-launch split-K, n_bot launches; bottom_bwd_full) or "auto": full at
+        # <= 128 rows per GPU, else partial (measured, one MI355X: full 0.976 vs partial
+        # 0.857 M samples/s at the Kaggle shape, B = 128; partial ahead at C3 B = 2048, 4.67
+        # vs 4.54 M, and at B = 256, 1.21 vs 1.19 M; profiles/r04_bot_sched_ab.txt.  A third
+        # schedule - the data gradients as one row-block launch - lost at every shape and
+        # was removed in ABI v8)
         self.bot_sched = "auto"
         # one GPU: the bottom MLP forward as a role of the lookup launch (mlp_rows.hpp)
         self.fuse_bottom = True
@@ -807,27 +807,7 @@ class DLRMTrainer:
                 else:
                     self._gemm(pending + [w] + rq)
 
-        def bottom_bwd_chain(chain):
-            """Bottom-MLP backward in two launches: the data gradients of every layer in one
-            row-block launch (dlrm_mlp_chain_backward, gradients kept in LDS between layers),
-            then every layer's weight gradient (in-launch split-K, SGD fused on one GPU)
-            in one grouped GEMM launch together with the top MLP's pending reduce job."""
-            rq = st.pop("rq")
-            gs = [bufs["gb"][li][:, :self.bot[li].N] for li in range(self.n_bot - 1)]
-            ops.mlp_chain_backward(chain, bufs["gx"], gs)
-            probs = []
-            for li in range(self.n_bot):
-                g = gs[li] if li < self.n_bot - 1 else bufs["gx"]
-                inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
-                probs.append(self._wgrad(self.bot[li], g, inp, fused_opt, lr))
-            self._gemm(probs + rq)
-
         def bottom_bwd(s1=None):
-            if self.bot_sched == "chain" and not c_bot and len(self.bot) + len(st["rq"]) <= 6:
-                chain = self._bottom_chain(batch, bufs, backward=True)
-                if chain is not None and self.n_bot >= 2:
-                    with prof("gemm"):
-                        return bottom_bwd_chain(chain)
             sched = self.bot_sched
             if sched == "auto":
                 sched = "full" if Bl <= 128 else "partial"
@@ -1163,36 +1143,34 @@ class DLRMTrainer:
             self._colsum(hin[:, :last.Kp], scale=dz, out=last.gW[0],
                          workspace=self._ws_colsum(Bl, last.Kp))
 
-    def _bottom_chain(self, batch: Batch, bufs, backward: bool = False,
-                      sort_wgs: Optional[int] = None, standalone: bool = False):
-        """The bottom MLP as a dlrm_mlp_chain (None when unsupported; for the forward also
-        when disabled or, unless it runs as its own launch (standalone), when there are no
-        local tables to share the lookup launch with)."""
-        if not backward and (not self.fuse_bottom or (self.T_local == 0 and not standalone)):
+    def _bottom_chain(self, batch: Batch, bufs, sort_wgs: Optional[int] = None,
+                      standalone: bool = False):
+        """The bottom MLP forward as a dlrm_mlp_chain (None when unsupported or disabled or,
+        unless it runs as its own launch (standalone), when there are no local tables to
+        share the lookup launch with)."""
+        if not self.fuse_bottom or (self.T_local == 0 and not standalone):
             return None
         layers = [(L.W, out, L.Kp) for L, out in zip(self.bot, bufs["bot_act"])]
-        parts = 1
-        if not backward:
-            # several workgroups per 16-row block while the lookup launch still fits the
-            # chip in one wave (its T_local + 1 sort workgroups beside them): small batches
-            # then run the bottom MLP on 2-4x the CUs (mlp_rows.hpp, split chains)
-            nrb = (batch.X.shape[0] + 15) // 16
-            parts = self.bottom_parts
-            others = self.T_local + 1 if sort_wgs is None else sort_wgs
-            if parts <= 0:
-                parts = next((p for p in (4, 2) if nrb * p + others <= self._cus), 1)
-            widest = max(range(len(layers)), key=lambda i: layers[i][2] * layers[i][0].shape[0])
-            if (layers[widest][0].shape[0] + 15) // 16 < parts:
-                parts = 1
-            if parts > 1:
-                tk = bufs.get("mlp_tickets")
-                if tk is None or tk.numel() < nrb:
-                    tk = bufs["mlp_tickets"] = torch.zeros(nrb, dtype=torch.int32,
-                                                           device=self.dev)
-                chain = ops.mlp_chain(batch.X, layers, parts=parts, split_layer=widest,
-                                      tickets=tk)
-                if ops.mlp_chain_supported(chain):
-                    return chain
+        # several workgroups per 16-row block while the lookup launch still fits the
+        # chip in one wave (its T_local + 1 sort workgroups beside them): small batches
+        # then run the bottom MLP on 2-4x the CUs (mlp_rows.hpp, split chains)
+        nrb = (batch.X.shape[0] + 15) // 16
+        parts = self.bottom_parts
+        others = self.T_local + 1 if sort_wgs is None else sort_wgs
+        if parts <= 0:
+            parts = next((p for p in (4, 2) if nrb * p + others <= self._cus), 1)
+        widest = max(range(len(layers)), key=lambda i: layers[i][2] * layers[i][0].shape[0])
+        if (layers[widest][0].shape[0] + 15) // 16 < parts:
+            parts = 1
+        if parts > 1:
+            tk = bufs.get("mlp_tickets")
+            if tk is None or tk.numel() < nrb:
+                tk = bufs["mlp_tickets"] = torch.zeros(nrb, dtype=torch.int32,
+                                                       device=self.dev)
+            chain = ops.mlp_chain(batch.X, layers, parts=parts, split_layer=widest,
+                                  tickets=tk)
+            if ops.mlp_chain_supported(chain):
+                return chain
         chain = ops.mlp_chain(batch.X, layers)
         return chain if ops.mlp_chain_supported(chain) else None
 

@@ -106,7 +106,10 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  *    split_layer / tickets (several workgroups per 16-row block) (round 4).
  * 7: dlrm_tbe_sort_defer and role phase 3 removed (the sort as a GEMM-launch role measured
  *    slower than the sort in the lookup launch everywhere, profiles/r04_sort_role_ab.txt)
- *    (round 5). */
+ *    (round 5).
+ * 8: dlrm_mlp_chain_backward removed (the bottom MLP's data gradients as one row-block
+ *    launch lost to the grouped GEMM schedules at every batch size,
+ *    profiles/r04_bot_sched_ab.txt) (round 5). */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 
@@ -203,18 +206,6 @@ int dlrm_mlp_chain_supported(const dlrm_mlp_chain* chain);
 
 /* The chain on its own: 16 rows per workgroup, every layer in one launch. */
 int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream);
-
-/* The data gradients of the chain's backward (round 4; the autograd of apply_mlp's
- * Linear+ReLU stack, dlrm_s_pytorch.py:518-524, without the weight gradients, which the
- * caller runs as one grouped GEMM launch): given g_last = dLoss/d(pre-activation of the
- * last layer) [rows][>= out_width[L-1]], for l = L-1 .. 1
- *   g[l-1] = (g_l . W_l[:, :out_width[l-1]]) * (Y_{l-1} > 0)   (columns < out_width[l-1])
- * with g_{L-1} = g_last; W_l and Y_{l-1} are the chain's (the forward's weights and
- * outputs).  16 rows per workgroup, every layer in one launch, gradients kept in LDS
- * between layers.  g / ld_g: L-1 buffers and row pitches, none aliasing g_last.  Same
- * support rules as the forward (dlrm_mlp_chain_supported). */
-int dlrm_mlp_chain_backward(const dlrm_mlp_chain* chain, const float* g_last, int64_t ld_g_last,
-                            float* const* g, const int64_t* ld_g, dlrm_stream_t stream);
 
 /*
  * dlrm_tbe_forward + the per-table sort of the backward (which depends only on the

@@ -26,7 +26,7 @@ def test_abi_library_exports_every_header_symbol():
         assert hasattr(lib, n), f"{n} declared in include/dlrm_hip.h but not exported"
         assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
     assert set(_lib.SIGNATURES) == set(names)
-    assert lib.dlrm_abi_version() == 7
+    assert lib.dlrm_abi_version() == 8
 
 
 def test_abi_rejects_bad_arguments_without_gpu():

@@ -660,42 +660,9 @@ def test_c3_zipf_hot_rows_vs_oracle(graph):
     _compare_state(tr, ref)
 
 
-@pytest.mark.parametrize("name", ["c3_small", "c2_small"])
-@pytest.mark.parametrize("graph", [False, True])
-def test_bottom_backward_chain_schedule_vs_oracle(name, graph):
-    """bot_sched="chain": the bottom MLP's data gradients in one row-block launch
-    (dlrm_mlp_chain_backward) and every bottom wgrad (in-launch split-K, SGD fused) plus the
-    top MLP's pending reduce job in one grouped launch; C3 (3 bottom layers) and C2 (4
-    layers: 5 problems in the group) widths, 2 steps vs the oracle, eager and replayed."""
-    DLRMTrainer, TrainerConfig = _trainer()
-    c = CASES[name]
-    D, rows = c["D"], c["rows"]
-    ln_top = [_num_int(len(rows), D)] + c["top"]
-    np.random.seed(7)
-    ref = O.OracleDLRM(D, rows, c["bot"], ln_top, loss_function=c["loss"])
-    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"], ln_top=ln_top,
-                        loss_function=c["loss"], learning_rate=c["lr"])
-    tr = DLRMTrainer.from_oracle(cfg, ref, device=dev)
-    tr.bot_sched = "chain"
-    rng = np.random.RandomState(3)
-    for s in range(2):
-        X, lS_o, lS_i, T = _rand_batch(rng, rows, c["B"], c["L"], c["bot"][0], c["loss"])
-        Zr, Er = ref.train_step(torch.tensor(X), torch.tensor(lS_o),
-                                [torch.tensor(i) for i in lS_i], torch.tensor(T), c["lr"])
-        b = tr.make_batch(X, lS_o, lS_i, T)
-        if graph and s > 0:
-            tr.capture(b)()
-            Z = tr._cur["prob"]
-        else:
-            Z, _ = tr.step(b)
-        ok, msg = fp32_close(Z.cpu().numpy(), Zr.numpy().ravel())
-        assert ok, (s, msg)
-    _compare_state(tr, ref)
-
-
 @pytest.mark.parametrize("name,sched,optimizer,at", [
     ("c3_small", "partial", "sgd", (0, 1)), ("c3_small", "full", "sgd", (0, 1)),
-    ("c3_small", "chain", "sgd", (0, 1)), ("c2_small", "full", "sgd", (0, 1)),
+    ("c2_small", "full", "sgd", (0, 1)),
     ("c2_small", "partial", "rwsadagrad", (0, 1)), ("c3_small", "partial", "rwsadagrad", (0, 1)),
     ("c3_small", "partial", "sgd", (0, 3)), ("c3_small", "partial", "sgd", (1, 2)),
     ("c2_small", "full", "sgd", (2, 9))])
