@@ -9,13 +9,16 @@
 namespace {
 
 constexpr int kDigitBits = 8;
+// Tables of at most this many lookups take the rank sort (n broadcast LDS keys per element,
+// n^2 / 32 VALU lane-operations in all) instead of the radix passes (segsort_body).
+constexpr int kRankSortMax = 512;
 
 // TH threads x IT items per thread; PACKED: each item's local bag rides in the high bits of
 // its position (pos < 2^kPosBits), so no per-position bag table is needed (the 256-thread
 // role then fits in 21 KB of LDS, under the 64x32 GEMM tile's 27.6 KB).
 constexpr int kPosBits = 11;
 template <int TH, int IT, bool PACKED>
-struct SegLds {
+struct alignas(16) SegLds {
   static constexpr int kCap = TH * IT, kWaves = TH / 64;
   uint32_t key[kCap];
   int32_t pos[kCap];
@@ -198,6 +201,50 @@ __device__ __forceinline__ void segsort_body(
       if (key[u] == (uint32_t)nrows && err) atomicOr(err, DLRM_TBE_ERR_INDEX);
       if constexpr (PACKED) pos[u] = i | (bags[i] << kPosBits);
     }
+  }
+  if (n <= TH && n <= kRankSortMax) {
+    // Short tables (small batches: <= 512 lookups per table): a stable rank sort instead of
+    // bits / 8 radix passes of five barriers each.  Element i's destination is
+    // #{j : key_j < key_i or (key_j == key_i and j < i)} - the (key, element) order the
+    // stable radix sort produces, so the output is bitwise the radix path's.  One element
+    // per thread; every lane walks the same LDS keys (broadcast reads): before its wave's
+    // own elements j < i for every lane (count key_j <= k), after them j > i (key_j < k),
+    // the 64 in between per element - two VALU operations per key outside the diagonal.
+    __syncthreads();  // (PACKED: bags in sm.pos were read above; sm.key is free)
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int i = w * (IT * 64) + u * 64 + l;
+      if (i < n) {
+        sm.key[i] = key[u];
+        if constexpr (PACKED) sm.pos[i] = pos[u];  // pos[u] = i | (bag << kPosBits)
+      }
+    }
+    if (tid < 4) sm.key[n + tid] = 0xffffffffu;  // pad: never < a key (keys <= nrows)
+    __syncthreads();
+    if (tid < n) {
+      const uint32_t k = sm.key[tid];
+      const int wb = tid & ~63, we = wb + 64 < n ? wb + 64 : n;
+      uint32_t rank = 0;
+      for (int j = 0; j < wb; j += 4) {
+        const uint4 q = *reinterpret_cast<const uint4*>(sm.key + j);
+        rank += (q.x <= k) + (q.y <= k) + (q.z <= k) + (q.w <= k);
+      }
+      for (int j = wb; j < we; ++j) {
+        const uint32_t q = sm.key[j];
+        rank += (q < k) | ((q == k) & (j < tid));
+      }
+      for (int j = we; j < n; j += 4) {
+        const uint4 q = *reinterpret_cast<const uint4*>(sm.key + j);
+        rank += (q.x < k) + (q.y < k) + (q.z < k) + (q.w < k);
+      }
+      keys_out[s0 + rank] = k < (uint32_t)nrows ? (uint32_t)(rb + k) : sentinel;
+      pos_out[s0 + rank] = (int32_t)(s0 + tid);
+      if constexpr (PACKED)
+        bag_of[s0 + rank] = t * B + (sm.pos[tid] >> kPosBits);
+      else
+        bag_of[s0 + rank] = sm.bag[tid];
+    }
+    return;
   }
   // (PACKED: the sort's first scatter into sm.pos comes after three barriers)
   seg_radix_sort<TH, IT, PACKED>(key, pos, bits, sm);

@@ -105,14 +105,16 @@ def test_tbe_weighted_and_dense_grad(ops):
 
 @pytest.mark.parametrize("mode", ["sgd", "rowwise_adagrad", "dense"])
 @pytest.mark.parametrize("invalid", [False, True])
-def test_tbe_backward_per_table_sort_vs_global_sort(ops, mode, invalid):
+@pytest.mark.parametrize("B,L", [(512, 2), (100, 1), (256, 2)])
+def test_tbe_backward_per_table_sort_vs_global_sort(ops, mode, invalid, B, L):
     """The per-table LDS sort and the device-wide radix sort order lookups by (row, position)
     alike: with all indices valid the updates are bitwise identical.  Out-of-range indices
     (skipped) sit at a different place in the two sorted arrays, which shifts the fixed
     16-lookup reduction blocks; both then still match the reference within fp32 tolerance.
-    Skewed tables (3 rows, ~340 lookups per row) exercise runs spanning many blocks."""
+    Skewed tables (3 rows, ~340 lookups per row) exercise runs spanning many blocks.  100
+    and 512 lookups per table take the per-table rank sort (<= 512), 1024 the radix passes."""
     torch.manual_seed(7)
-    rows, D, B, L = [3, 5000, 4, 700, 1], 64, 512, 2
+    rows, D = [3, 5000, 4, 700, 1], 64
     T = len(rows)
     lo = [torch.arange(B) * L for _ in rows]
     li = [torch.randint(0, n, (B * L,)) for n in rows]
