@@ -855,13 +855,15 @@ constexpr PlanEntry kPlans[] = {
     {0, 0, 0, 0, 64, 64, 1},  // sentinel (never matches: M = 0)
 };
 
-// Compiled tiles (BM x BN on 2x2 waves): 64x64, 128x64, 64x128, 32x64, 64x32.  (Other
+// Compiled tiles (BM x BN on 2x2 waves): 64x64, 128x64, 64x128, 32x64, 64x32, 32x32 (the
+// latency-bound small-batch shapes: twice the workgroups of 64x32 without a K split,
+// profiles/r05_gemm_plans_resweep.txt).  (Other
 // wave layouts of pipe_body - 64x32 on 2x1, 32x64 on 1x2, 128x32 on 4x1 - measured slower
 // on every DLRM shape: tools/gemm_cfg_ab.py, profiles/r02_gemm_cfg_ab.txt.)
 bool tile_ok(int bm, int bn, int wm, int wn) {
   return wm == 2 && wn == 2 &&
          ((bm == 64 && bn == 64) || (bm == 128 && bn == 64) || (bm == 64 && bn == 128) ||
-          (bm == 32 && bn == 64) || (bm == 64 && bn == 32));
+          (bm == 32 && bn == 64) || (bm == 64 && bn == 32) || (bm == 32 && bn == 32));
 }
 
 struct Tile {
@@ -1163,6 +1165,8 @@ int run(int n, const Desc* d, void* ws, size_t ws_bytes, hipStream_t st,
   }
   if (t.bm == 128) return launch_group<128, 64>(m, q, pl, ws, ws_bytes, role, phase, st);
   if (t.bn == 128) return launch_group<64, 128>(m, q, pl, ws, ws_bytes, role, phase, st);
+  if (t.bm == 32 && t.bn == 32)
+    return launch_group<32, 32>(m, q, pl, ws, ws_bytes, role, phase, st);
   if (t.bm == 32) return launch_group<32, 64>(m, q, pl, ws, ws_bytes, role, phase, st);
   if (t.bn == 32) return launch_group<64, 32>(m, q, pl, ws, ws_bytes, role, phase, st);
   return launch_group<64, 64>(m, q, pl, ws, ws_bytes, role, phase, st);

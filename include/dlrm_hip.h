@@ -118,7 +118,7 @@ const char* dlrm_last_error(void);
  * value 0 restores the planner's choice.  Results stay exact under any override (the
  * tests compare every path with the reference), only speed changes.
  *   DLRM_TUNE_GEMM_TILE  : BM * 1000 + BN of the pipelined GEMM's workgroup tile (64064,
- *                          128064, 64128, 32064, 64032); the measured plan table is skipped
+ *                          128064, 64128, 32064, 64032, 32032); the measured plan table is skipped
  *   DLRM_TUNE_GEMM_SPLIT : K splits of every FULL problem (with DLRM_TUNE_GEMM_TILE)
  *   DLRM_TUNE_TBE_BLOCK  : sorted lookups per TBE-backward block (16 or 64)
  *   DLRM_TUNE_TBE_SORT   : 1 = the device-wide radix sort even where the tiled per-table

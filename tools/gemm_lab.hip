@@ -513,6 +513,7 @@ extern "C" int lab_gemm(int32_t cfg, int32_t split, int32_t n, const dlrm_gemm_p
   hipStream_t st = dlrm::as_stream(stream);
   switch (cfg) {
     case 100: return lab_launch<64, 32, 2, 2, 2, 0, true>(n, d, pl, ws, ws_bytes, st);
+    case 110: return lab_launch<32, 32, 2, 2, 4, 0, true>(n, d, pl, ws, ws_bytes, st);
     case 101: return lab_launch<64, 64, 2, 2, 2, 0, true>(n, d, pl, ws, ws_bytes, st);
     case 102: return lab_launch<128, 64, 2, 2, 2, 0, true>(n, d, pl, ws, ws_bytes, st);
     case 103: return lab_launch<128, 128, 4, 2, 1, 0, true>(n, d, pl, ws, ws_bytes, st);

@@ -15,7 +15,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dlrm-yx_amd"))
 from dlrm_hip import ops  # noqa: E402
 
-CFGS = ["64x64", "32x64", "64x32", "128x64", "64x128"]
+CFGS = ["64x64", "32x64", "64x32", "128x64", "64x128", "32x32"]
 LAYERS = {  # (K, N) of the C3 (terabyte) layers
     "terabyte": [(13, 512), (512, 256), (256, 128), (479, 1024), (1024, 1024), (1024, 512),
                  (512, 256)],
