@@ -21,7 +21,7 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace dlrm
 
-extern "C" int dlrm_abi_version(void) { return 8; }
+extern "C" int dlrm_abi_version(void) { return DLRM_ABI_VERSION; }
 
 extern "C" const char* dlrm_last_error(void) { return dlrm::g_last_error; }
 

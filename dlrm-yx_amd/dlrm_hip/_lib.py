@@ -11,6 +11,9 @@ import os
 from ctypes import c_float, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# DLRM_ABI_VERSION of include/dlrm_hip.h that these signatures mirror; load() refuses a
+# library built from any other header (tests/test_cpu_host.py checks header == this).
+ABI_VERSION = 8
 LIB_PATH = os.environ.get("DLRM_HIP_LIB", os.path.join(_HERE, "libdlrm_hip.so"))
 
 
@@ -162,6 +165,12 @@ def load() -> ctypes.CDLL:
             f"libdlrm_hip.so not found at {LIB_PATH}; build it with "
             f"`make -C dlrm-yx_amd/csrc` (or __graft_entry__.build())")
     lib = ctypes.CDLL(LIB_PATH)
+    lib.dlrm_abi_version.restype = c_int32
+    got = int(lib.dlrm_abi_version())
+    if got != ABI_VERSION:
+        raise DLRMHipUnavailable(
+            f"{LIB_PATH} has ABI version {got}, the bindings expect {ABI_VERSION}; rebuild it "
+            f"with `make -C dlrm-yx_amd/csrc`")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

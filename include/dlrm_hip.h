@@ -110,6 +110,8 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  * 8: dlrm_mlp_chain_backward removed (the bottom MLP's data gradients as one row-block
  *    launch lost to the grouped GEMM schedules at every batch size,
  *    profiles/r04_bot_sched_ab.txt) (round 5). */
+#define DLRM_ABI_VERSION 8 /* the one source of truth: abi.cpp returns it, dlrm_hip/_lib.py
+                             pins it (tests/test_cpu_host.py checks all of them agree) */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
 

@@ -26,7 +26,19 @@ def test_abi_library_exports_every_header_symbol():
         assert hasattr(lib, n), f"{n} declared in include/dlrm_hip.h but not exported"
         assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
     assert set(_lib.SIGNATURES) == set(names)
-    assert lib.dlrm_abi_version() == 8
+    hdr = open(os.path.join(ROOT, "include", "dlrm_hip.h")).read()
+    want = int(re.search(r"#define\s+DLRM_ABI_VERSION\s+(\d+)", hdr).group(1))
+    assert lib.dlrm_abi_version() == _lib.ABI_VERSION == want
+    src = open(os.path.join(ROOT, "dlrm-yx_amd", "csrc", "abi.cpp")).read()
+    assert "return DLRM_ABI_VERSION;" in src  # no literal that can drift from the header
+
+
+def test_graft_entry_build_runs_here():
+    """__graft_entry__.build(): make (up to date, or rebuilds) + import + ABI check. The
+    driver's build step; it broke silently in round 5 when the ABI moved."""
+    import __graft_entry__ as g
+    g.build()
+    assert g._header_abi_version() == __import__("dlrm_hip")._lib.ABI_VERSION
 
 
 def test_abi_rejects_bad_arguments_without_gpu():
