@@ -696,6 +696,9 @@ def main():
                     "B/W dense batch, collectives replaced by same-size device copies "
                     "(trainer.EmulatedComm); a builder's projection, not a multi-GPU figure")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--emulate-capture", choices=["segments", "whole"], default="segments",
+                    help="segments (default): captured as RCCL captures - four graphs around "
+                    "the eager all-to-alls; whole: one graph (no RCCL path can do that today)")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-cores", default="", help=argparse.SUPPRESS)
@@ -755,8 +758,8 @@ def main():
                         qr_threshold=qr["threshold"] if qr else 200)
     if emulated:
         world, rank = args.emulate_world, args.emulate_rank
-        tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, comm=EmulatedComm(),
-                         seed=1)
+        tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world,
+                         comm=EmulatedComm(whole=args.emulate_capture == "whole"), seed=1)
     else:
         tr = DLRMTrainer(cfg, device=dev, rank=rank, world_size=world, process_group=pg,
                          seed=1)
@@ -966,6 +969,7 @@ def main():
                        "optimizer": c["optimizer"], "qr": c.get("qr"),
                        "parallelism": f"table-sharded emb x{world} + dp{world}",
                        "hip_graph": use_graph, "capture": tr.capture_mode,
+                       "graphs_per_step": tr.graphs_per_step if use_graph else None,
                        "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
                        "tbe_role_at": list(tr.tbe_role_at), "bottom_parts": tr.bottom_parts,
                        "head_role": tr.head_role, "full_last_wgrad": tr.full_last_wgrad,
@@ -986,13 +990,19 @@ def main():
         if cpu and "value" in cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 1)
         if emulated:
+            # a projection, never the headline metric: its own metric name,
+            # value null, the projected rate inside the emulated block
+            line["metric"] = "EMULATED one-rank projection (not a multi-GPU measurement)"
+            line["value"] = None
             line["emulated"] = {
+                "projected_samples_per_s": round(value, 1),
                 "world": world, "rank": rank, "local_batch": Bl,
                 "tables_this_rank": tr.T_local, "tables_per_rank": tr.tables_per_rank,
                 "what": "one GPU runs this rank's kernels at the W-rank shapes; the "
                         "all-to-all is a same-size device copy and the all-reduce a no-op "
                         "(trainer.EmulatedComm): the rank's compute schedule, not the "
-                        "fabric; value = global batch / this rank's step time",
+                        "fabric; projected_samples_per_s = global batch / this rank's step "
+                        "time",
                 "note": "builder-run projection; never a multi-GPU measurement"}
         print(json.dumps(line), flush=True)
     if procs > 1:

@@ -270,6 +270,7 @@ class DLRMTrainer:
         self._head_ws: Optional[torch.Tensor] = None
         self.step_count = 0
         self.capture_mode = None  # "whole" | "segments": how the last capture() was built
+        self.graphs_per_step = 0  # hipGraphs one replay of the last capture() launches
         if init:
             self.init_random(seed)
 
@@ -580,13 +581,14 @@ class DLRMTrainer:
         return self._cur["prob"], self._cur["loss"]
 
     def segments(self, batch: Batch, profile=None):
-        """The step as an ordered list of ("gpu", fn) / ("comm", fn) / ("host", fn) items.
-        "gpu" items only enqueue HIP kernels on the current stream (no host sync, no
-        allocation after the first step of a batch size): each one can be captured in a
-        hipGraph.  "comm" items issue or wait for the collectives between them (multi GPU
-        only); on RCCL they are stream-ordered too, so the whole multi-GPU step captures as
-        ONE graph (capture); on gloo they run eagerly between segment graphs.  "host" items
-        are host bookkeeping, run on every replay.
+        """The step as an ordered list of ("gpu", fn) / ("a2a", fn) / ("ar", fn) /
+        ("host", fn) items.  "gpu" items only enqueue HIP kernels on the current stream (no
+        host sync, no allocation after the first step of a batch size): each one can be
+        captured in a hipGraph.  "a2a" / "ar" items issue or wait for the all-to-alls / the
+        dense all-reduces between them (multi GPU only): RCCL's all-reduces are captured
+        with the kernels, its all-to-alls run eagerly between the graphs (capture); on
+        gloo every collective runs eagerly.  "host" items are host bookkeeping, run on
+        every replay.
 
         MLP backward: each layer's weight gradient is split-K into a per-layer partial
         buffer and its reduction (+ fused SGD on one GPU) is a REDUCE job inside the NEXT
@@ -660,7 +662,7 @@ class DLRMTrainer:
         def bottom_fwd():
             h = batch.X
             if st.pop("bottom_done", False):  # ran inside the lookup launch
-                return
+                return _EMPTY
             with record_function("module::forward_pass::bottom_mlp"):
                 if dist and profile is None:
                     # several GPUs: the bottom MLP as one row-block chain launch (activations
@@ -753,10 +755,16 @@ class DLRMTrainer:
                     # launch's reduce job), so it may run beside the dgrad reading W
                     self._gemm([dg, w] + rq)
                     rq = [r]
-                elif not fused_opt:
+                elif r is None and not fused_opt:
                     # the wgrad writes the gradient bucket, not W: beside the dgrad
                     self._gemm([dg, w] + rq)
                     rq = []
+                elif r is not None:
+                    # a split wgrad kept out of the dgrad's launch (group_wgrad off): its
+                    # partials in a launch of their own, its reduce job on the next one
+                    self._gemm([dg] + rq)
+                    self._gemm([w])
+                    rq = [r]
                 else:
                     # an unsplit wgrad updates W_l in its epilogue: it rides on the NEXT
                     # launch (dgrad of layer l-1 reads W_{l-1}, not W_l; its g_l buffer
@@ -925,21 +933,47 @@ class DLRMTrainer:
         def wait(key):
             return lambda: st.pop(key).wait()
 
+        a2a_fwd = lambda: st.__setitem__("a2a", self._alltoall_fwd(bufs, Bl))  # noqa: E731
+        a2a_bwd = lambda: st.__setitem__("a2a", self._alltoall_bwd(bufs, Bl))  # noqa: E731
+        if getattr(self.comm, "capture_ar", False):
+            # RCCL: the all-reduces capture into hipGraphs, the all-to-alls do not (DESIGN.md
+            # §8: a captured all_to_all_single crashes hipStreamEndCapture on this stack).
+            # Each all-reduce is waited in the graph that issues it, so the step is FOUR
+            # graphs around the two eager all-to-alls: the top bucket overlaps the bottom
+            # backward and the reverse all-to-all, the bottom bucket the embedding update
+            return [
+                ("gpu", lookup),
+                ("a2a", a2a_fwd),
+                ("gpu", bottom_fwd),
+                ("a2a", wait("a2a")),  # All2All_Wait (extend_distributed.py:489)
+                ("gpu", top),
+                ("gpu", interaction_bwd),
+                ("a2a", a2a_bwd),
+                ("ar", ar("top")),
+                ("gpu", record_function("## Backward ##")(bottom_bwd)),
+                ("ar", wait("ar_top")),
+                ("a2a", wait("a2a")),
+                ("ar", ar("bot")),
+                ("gpu", record_function("## Backward ##")(emb_bwd)),
+                ("ar", wait("ar_bot")),
+                ("gpu", dense_update),
+                ("host", done),
+            ]
         return [
             ("gpu", lookup),
-            ("comm", lambda: st.__setitem__("a2a", self._alltoall_fwd(bufs, Bl))),
+            ("a2a", a2a_fwd),
             ("gpu", bottom_fwd),
-            ("comm", wait("a2a")),  # All2All_Wait (extend_distributed.py:489)
+            ("a2a", wait("a2a")),  # All2All_Wait (extend_distributed.py:489)
             ("gpu", top),
-            ("comm", ar("top")),
+            ("ar", ar("top")),
             ("gpu", interaction_bwd),
-            ("comm", lambda: st.__setitem__("a2a", self._alltoall_bwd(bufs, Bl))),
+            ("a2a", a2a_bwd),
             ("gpu", record_function("## Backward ##")(bottom_bwd)),
-            ("comm", ar("bot")),
-            ("comm", wait("a2a")),
+            ("ar", ar("bot")),
+            ("a2a", wait("a2a")),
             ("gpu", record_function("## Backward ##")(emb_bwd)),
-            ("comm", wait("ar_top")),
-            ("comm", wait("ar_bot")),
+            ("ar", wait("ar_top")),
+            ("ar", wait("ar_bot")),
             ("gpu", dense_update),
             ("host", done),
         ]
@@ -995,13 +1029,14 @@ class DLRMTrainer:
                                     self._qr_pr, bufs["P"], bufs["E"])
 
     def capture(self, batch: Batch, pool=None, whole: Optional[bool] = None):
-        """A replayable step for ``batch``.  whole (default: one GPU, or collectives that
-        capture - the emulated rank's device copies): the step's kernels AND its
-        collectives in ONE hipGraph (a graph-to-graph boundary costs ~9 us of idle GPU,
-        profiles/r05_step_timeline_emul8_r2.txt); else (RCCL, gloo) the "gpu" segments
-        captured as graphs with the "comm" items run eagerly between them.  Run one eager step of this
-        batch size first (allocations).  Returns a callable; each call is one full training
-        step on the captured buffers."""
+        """A replayable step for ``batch``.  whole (default: one GPU, or a comm whose
+        collectives all capture): the step's kernels AND its collectives in ONE hipGraph (a
+        graph-to-graph boundary costs ~9 us of idle GPU, profiles/r05_step_timeline_emul8_
+        r2.txt); else the "gpu" segments - with the collectives the comm can capture
+        (``capture_ar``: RCCL's all-reduces) - as graphs, and the rest ("a2a": RCCL's
+        all-to-alls, everything on gloo) run eagerly between them.  Run one eager step of
+        this batch size first (allocations).  Returns a callable; each call is one full
+        training step on the captured buffers."""
         auto = whole is None
         if auto:
             whole = not self.distributed or bool(getattr(self.comm, "capturable", False))
@@ -1023,6 +1058,7 @@ class DLRMTrainer:
                 torch.cuda.synchronize()
                 return self.capture(batch, pool=pool, whole=False)
             self.capture_mode = "whole"
+            self.graphs_per_step = 1
 
             def run_whole():
                 g.replay()
@@ -1030,22 +1066,27 @@ class DLRMTrainer:
                     fn()
             return run_whole
         self.capture_mode = "segments"
+        in_graph = {"gpu"}
+        if getattr(self.comm, "capture_ar", False):
+            in_graph.add("ar")
         items = []
         pending = []
         segs = self.segments(batch)
+        self.graphs_per_step = 0
 
         def flush():
             if not pending:
                 return
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
-                for fn in pending:
-                    fn()
-            items.append(g.replay)
+                launched = [fn() is not _EMPTY for fn in pending]
+            if any(launched):  # a segment that enqueued nothing is not replayed
+                items.append(g.replay)
+                self.graphs_per_step += 1
             pending.clear()
 
         for kind, fn in segs:
-            if kind == "gpu":
+            if kind in in_graph:
                 pending.append(fn)
             elif kind == "host":
                 items.append(fn)
@@ -1230,6 +1271,9 @@ class DLRMTrainer:
         return {"tables": tabs, "rows": rows, "lookups": look,
                 "lookup_max_over_mean": round(max(look) / mean, 3) if mean else None}
 
+_EMPTY = object()  # returned by a "gpu" segment that enqueued nothing this step
+
+
 class _NullCtx:
     def __enter__(self):
         return self
@@ -1251,17 +1295,31 @@ class TorchComm:
     for.  gloo groups with CUDA tensors (tests: several ranks on one GPU) stage through
     the host, synchronously."""
 
-    def __init__(self, pg, dense_pg=None):
+    def __init__(self, pg, dense_pg=None, separate_dense: bool = True):
+        """``separate_dense`` False: the all-reduces share the all-to-all's communicator
+        (one stream; the fallback if two concurrent communicators misbehave at W > 1 -
+        that overlap has run on 1-rank RCCL and multi-rank gloo only)."""
         import torch.distributed as dist
         self.pg = pg
         if dense_pg is None:
-            dense_pg = dist.new_group(ranks=list(range(dist.get_world_size(pg))),
-                                      backend=dist.get_backend(pg))
+            if separate_dense:
+                # the SAME ranks as pg (global rank ids: pg need not be WORLD)
+                dense_pg = dist.new_group(ranks=dist.get_process_group_ranks(pg),
+                                          backend=dist.get_backend(pg))
+            else:
+                dense_pg = pg
         self.dense_pg = dense_pg
-        # collectives are not captured into the step's hipGraph: a capture of RCCL
-        # collectives issued through torch.distributed hung on this stack (1-rank nccl,
-        # gpurun_out r05 pytest_cap); the kernel segments between them are graphs instead
+        # What captures into a hipGraph on this stack (tools/rccl_capture_probe.py,
+        # profiles/r06_rccl_capture_probe.txt): RCCL all-reduces (sync or async + wait, on
+        # either communicator) and all-gathers capture and replay correctly; an
+        # all_to_all_single - warmed eagerly first or not - crashes hipStreamEndCapture
+        # (unbounded recursion inside libamdhip64).  So the all-reduces ride inside the
+        # step's graphs and only the two all-to-alls run eagerly between them (the
+        # round-5 "hang" was this crash in a spawned test worker, its parent waiting on a
+        # queue that never filled).  gloo: nothing captures.
+        nccl = dist.get_backend(pg) == "nccl" and dist.get_backend(dense_pg) == "nccl"
         self.capturable = False
+        self.capture_ar = nccl
 
     def a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
         import torch.distributed as dist
@@ -1289,8 +1347,14 @@ class EmulatedComm:
     the B/W local batch, the rank-major features).  The all-to-all becomes one device copy
     of min(send, recv) bytes on the current stream (the rest of the receive buffer keeps
     whatever it holds); the all-reduce does nothing.  Times the rank's own work, not the
-    fabric."""
-    capturable = True
+    fabric.  By default it captures like RCCL does (``capture_ar``: the all-reduces inside
+    the step's graphs, the all-to-alls eager between four graphs), so the projection pays
+    the same graph boundaries as the real path; ``whole=True``: one graph (what the step
+    would cost if RCCL's all-to-all captured)."""
+
+    def __init__(self, whole: bool = False):
+        self.capturable = bool(whole)
+        self.capture_ar = True
 
     def a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
         n = min(int(sum(out_splits)), int(sum(in_splits)))

@@ -161,23 +161,11 @@ class PermutedTwin:
         self.head.push(torch.as_tensor(dz).reshape(-1)[pl], torch.as_tensor(target).reshape(-1)[pl],
                        n)
 
-    def close(self, got, ref, twin, what=""):
+    def close(self, got, ref, twin, what="", stats=None):
         """(ok, message, n_explained) for the engine's value of an oracle quantity ``ref``
-        whose twin value is ``twin``."""
-        import numpy as np
-        a = np.asarray(got, dtype=np.float64)
-        b = torch.as_tensor(ref).detach().double().numpy()
-        c = torch.as_tensor(twin).detach().double().numpy()
-        base = 1e-5 * np.maximum(1.0, np.abs(b))
-        err = np.abs(a - b)
-        lim = base + SPREAD * np.abs(b - c)
-        n_expl = int(((err > base) & (err <= lim)).sum())
-        if (err > lim).any():
-            i = np.unravel_index(np.argmax(err - lim), a.shape)
-            return False, (f"{what} got {a[i]!r} oracle {b[i]!r} twin {c[i]!r} at {i}: beyond "
-                           f"1e-5 and beyond {SPREAD} x the oracle's own spread under a "
-                           f"permuted summation order"), n_expl
-        return True, "", n_expl
+        whose twin value is ``twin``.  ``stats``: an ExplainStats that counts the compared
+        and explained elements (the tests cap them)."""
+        return close_explained(got, ref, twin, None, what, stats)
 
 
 # Adagrad's step lr * g / (sqrt(S) + eps) is ill-conditioned where g is small against the
@@ -253,23 +241,58 @@ class AdagradBound:
                     g.zero_()
 
 
-def close_explained(got, ref, twin, bound=None, what=""):
+class ExplainStats:
+    """What the explained comparisons used, for the tests' caps: elements compared, those
+    beyond 1e-5 explained by the permuted twin's spread (``n_twin``), those explained ONLY
+    by the Adagrad conditioning allowance (``n_bound``), and the largest error among the
+    latter (``max_bound_err``, to compare with lr: one Adagrad step moves an element by
+    at most ~lr)."""
+
+    def __init__(self):
+        self.compared = 0
+        self.n_twin = 0
+        self.n_bound = 0
+        self.max_bound_err = 0.0
+
+    @property
+    def n_explained(self):
+        return self.n_twin + self.n_bound
+
+    def __repr__(self):
+        return (f"ExplainStats(compared={self.compared}, twin={self.n_twin}, "
+                f"bound={self.n_bound}, max_bound_err={self.max_bound_err:.3g})")
+
+
+def close_explained(got, ref, twin, bound=None, what="", stats=None):
     """(ok, message, n_explained): |got - ref| <= 1e-5 max(1, |ref|) + max(SPREAD |ref -
-    twin|, bound) element-wise (bound: an AdagradBound allowance, or None)."""
+    twin|, bound) element-wise (bound: an AdagradBound allowance, or None).  An element
+    with a small allowance (a well-conditioned gradient: large |g| against its error, a
+    large Adagrad sum S) gets the plain 1e-5 bound (tests/test_relu_align_cpu.py injects
+    such errors and checks they are rejected)."""
     import numpy as np
     a = np.asarray(got, dtype=np.float64)
     b = torch.as_tensor(ref).detach().double().numpy()
     c = torch.as_tensor(twin).detach().double().numpy()
     base = 1e-5 * np.maximum(1.0, np.abs(b))
+    twin_lim = base + SPREAD * np.abs(b - c)
     extra = SPREAD * np.abs(b - c)
     if bound is not None:
-        extra = np.maximum(extra, bound.numpy())
+        extra = np.maximum(extra, torch.as_tensor(bound).double().numpy())
     err = np.abs(a - b)
     lim = base + extra
-    n_expl = int(((err > base) & (err <= lim)).sum())
+    beyond = err > base
+    by_twin = beyond & (err <= twin_lim)
+    by_bound = beyond & ~by_twin & (err <= lim)
+    n_expl = int(by_twin.sum() + by_bound.sum())
+    if stats is not None:
+        stats.compared += int(a.size)
+        stats.n_twin += int(by_twin.sum())
+        stats.n_bound += int(by_bound.sum())
+        if by_bound.any():
+            stats.max_bound_err = max(stats.max_bound_err, float(err[by_bound].max()))
     if (err > lim).any():
         i = np.unravel_index(np.argmax(err - lim), a.shape)
-        bd = float(bound.numpy()[i]) if bound is not None else 0.0
+        bd = float(torch.as_tensor(bound).numpy()[i]) if bound is not None else 0.0
         return False, (f"{what} got {a[i]!r} oracle {b[i]!r} twin {c[i]!r} at {i}: beyond 1e-5, "
                        f"{SPREAD} x the permuted twin's spread and the Adagrad conditioning "
                        f"allowance {bd!r}"), n_expl
@@ -296,6 +319,7 @@ class AlignedHead:
         self.queue = []  # (engine dz [n], target [n], 1 / n) per forward of the head
         self.aligned = 0
         self.unexplained: List[str] = []
+        self.seen = []  # (oracle z, tau, target) of every forward, for loss_interval()
         self.last.register_forward_hook(self._hook)
 
     def push(self, dz, target, n: int) -> None:
@@ -310,6 +334,7 @@ class AlignedHead:
         z = out.detach()
         tau = TAU_REL * (inp[0].detach().abs() @ mod.weight.detach().abs().t()
                          + mod.bias.detach().abs())
+        self.seen.append((z.clone(), tau.clone(), t.clone()))
         d0 = _bce_dz(z, t, inv_m)
         dlo, dhi = _bce_dz(z - tau, t, inv_m), _bce_dz(z + tau, t, inv_m)
         scale = torch.clamp(d0.abs(), min=inv_m)
@@ -330,3 +355,37 @@ class AlignedHead:
             return False, (f"{len(self.unexplained)} unexplained head gradients "
                            f"({self.unexplained[:4]}), {left} queued unused")
         return True, ""
+
+
+def _bce_terms(p, t):
+    """nn.BCELoss's per-sample terms (log clamped at -100, dlrm_s_pytorch.py:170-178) of
+    fp32 probabilities p, evaluated in fp64."""
+    p, t = p.double(), t.double()
+    return -(t * torch.log(p).clamp(min=-100) + (1 - t) * torch.log1p(-p).clamp(min=-100))
+
+
+def loss_interval(z, tau, t):
+    """The BCE loss a correct fp32 engine may report for a batch whose oracle logits are z,
+    from the ORACLE's state only.  A sample's clamped BCE term is ILL-CONDITIONED at fp32
+    where one ulp of its fp32 probability p moves the term by more than 1e-5 max(1, term)
+    (p within a few thousand ulp of 1 for t = 0, or of 0 for t = 1: the clamped log of a
+    difference that has cancelled); there the term may be anywhere between its values at
+    the fp32 sigmoid of z - tau and z + tau, widened by one ulp of p (the term is monotone
+    in p for t in {0, 1}).  Every other sample contributes the oracle's own term.  Returns
+    (lo, hi, n_ill): the interval of the batch mean and the number of ill-conditioned
+    samples.  The engine's own Z plays no part: a saturated step's loss is checked against
+    the oracle's logits."""
+    z32 = z.float().reshape(-1)
+    tau32 = tau.float().reshape(-1)
+    t32 = t.float().reshape(-1)
+    p = torch.sigmoid(z32)
+    mid = _bce_terms(p, t32)
+    up = _bce_terms(torch.nextafter(p, torch.ones_like(p)), t32)
+    dn = _bce_terms(torch.nextafter(p, torch.zeros_like(p)), t32)
+    ill = torch.maximum((up - mid).abs(), (dn - mid).abs()) > 1e-5 * torch.clamp(mid.abs(), min=1.0)
+    p_lo = torch.nextafter(torch.sigmoid(z32 - tau32), torch.zeros_like(p))
+    p_hi = torch.nextafter(torch.sigmoid(z32 + tau32), torch.ones_like(p))
+    a, b = _bce_terms(p_lo, t32), _bce_terms(p_hi, t32)
+    lo = torch.where(ill, torch.minimum(torch.minimum(a, b), mid), mid)
+    hi = torch.where(ill, torch.maximum(torch.maximum(a, b), mid), mid)
+    return float(lo.mean()), float(hi.mean()), int(ill.sum())

@@ -260,12 +260,20 @@ def _c3_worker(rank, W, port, q, B, c4=False, lr=0.1, steps=2):
         q.put((rank, traceback.format_exc()))
 
 
+DIST_CAPS = {"flips": 4, "bound": 16}
+
+
 def _c3_run_and_check(W, c4, lr, steps, B=64):
     """Spawn W ranks of the C3 (or C4) table list; per step, the oracle's W-rank step runs
     with its ReLUs aligned to the ranks' own decisions (tests/relu_align.py: every
     disagreement must be an oracle pre-activation within rounding of 0); then every
-    rank's Z / loss per step and its final tables, dense weights (and for C4 the row-wise
-    momentum and the dense Adagrad sums) at the plain 1e-5 bound, no element exempt."""
+    rank's Z / loss per step at the plain 1e-5 bound, and its final tables, dense weights
+    (and for C4 the row-wise momentum and the dense Adagrad sums) at 1e-5 except where a
+    difference is EXPLAINED: by the permuted twin's spread (tables, momentum, sums, dense)
+    or, for C4's dense weights, by AdagradBound.  Caps (DIST_CAPS; logged r05 runs: W=8 C4
+    0 flips and 16 explained elements = 2 dense elements x 8 ranks): flips, elements
+    explained <= 1e-5 of those compared, elements explained ONLY by AdagradBound, each
+    with an error <= 0.1 lr."""
     import oracle as O
     import relu_align as RA
     from conftest import fp32_close
@@ -309,7 +317,7 @@ def _c3_run_and_check(W, c4, lr, steps, B=64):
     lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
     lin2 = [m for seq in (tw.model.bot_l, tw.model.top_l) for m in seq
             if isinstance(m, torch.nn.Linear)]
-    n_expl = 0
+    st = RA.ExplainStats()
     for r in range(W):
         assert res[r]["local"] == [t for t in range(26) if alloc[t] == r]
         for t, w in res[r]["tables"].items():
@@ -321,33 +329,32 @@ def _c3_run_and_check(W, c4, lr, steps, B=64):
             else:
                 parts = [(w, e.weight, e2.weight, res[r]["mom"][t] if c4 else None)]
             for got, p, p2, mom in parts:
-                ok, msg, ne = tw.close(got, p, p2, f"rank {r} table {t}")
+                ok, msg, _ = tw.close(got, p, p2, f"rank {r} table {t}", st)
                 assert ok, msg
-                n_expl += ne
                 if mom is not None:
-                    ok, msg, ne = tw.close(mom, opt.state[id(p)]["momentum"],
-                                           opt2.state[id(p2)]["momentum"], f"momentum {t}")
+                    ok, msg, _ = tw.close(mom, opt.state[id(p)]["momentum"],
+                                          opt2.state[id(p2)]["momentum"], f"momentum {t}", st)
                     assert ok, msg
-                    n_expl += ne
         for i, (w, b) in enumerate(res[r]["dense"]):
             # beyond 1e-5 only where the oracle itself moves that much under a permuted
-            # summation order (relu_align.PermutedTwin)
+            # summation order (relu_align.PermutedTwin) or Adagrad's conditioning allows it
             for got, p, p2 in ((w, lin[i].weight, lin2[i].weight),
                                (b, lin[i].bias, lin2[i].bias)):
-                ok, msg, ne = RA.close_explained(got, p, p2,
-                                                 ab.bound[id(p)] if ab is not None else None,
-                                                 f"rank {r} dense {i}")
+                ok, msg, _ = RA.close_explained(got, p, p2,
+                                                ab.bound[id(p)] if ab is not None else None,
+                                                f"rank {r} dense {i}", st)
                 assert ok, msg
-                n_expl += ne
             if c4:
                 for got, p, p2 in zip(res[r]["sum"][i], (lin[i].weight, lin[i].bias),
                                       (lin2[i].weight, lin2[i].bias)):
-                    ok, msg, ne = tw.close(got, opt.state[id(p)]["sum"],
-                                           opt2.state[id(p2)]["sum"], f"rank {r} sum {i}")
+                    ok, msg, _ = tw.close(got, opt.state[id(p)]["sum"],
+                                          opt2.state[id(p2)]["sum"], f"rank {r} sum {i}", st)
                     assert ok, msg
-                    n_expl += ne
-    print(f"W={W} c4={c4}: {flips} explained ReLU flips, {n_expl} elements beyond 1e-5 "
-          f"explained by the oracle's own summation-order spread")
+    print(f"W={W} c4={c4}: {flips} explained ReLU flips; {st}")
+    assert flips <= DIST_CAPS["flips"], flips
+    assert st.n_explained <= 1e-5 * st.compared, st
+    assert st.n_bound <= DIST_CAPS["bound"], st
+    assert st.max_bound_err <= 0.1 * lr, st
 
 
 @pytest.mark.parametrize("W", [4, 8])
@@ -614,6 +621,7 @@ def _nccl_one_rank_worker(port, q, graph, in_lookup=True):
             res["tables"] = tr.weights.cpu().numpy()
             res["dense"] = tr.params.cpu().numpy()
             res["capture"] = tr.capture_mode
+            res["graphs"] = tr.graphs_per_step
             if name == "nccl":
                 res["backend"] = dist.get_backend(tr.comm.pg)
                 res["dense_backend"] = dist.get_backend(tr.comm.dense_pg)
@@ -646,8 +654,11 @@ def test_multi_gpu_schedule_on_one_rank_rccl_matches_single_gpu(graph, in_lookup
     assert isinstance(out, dict), out
     a, b = out["single"], out["nccl"]
     assert b["backend"] == "nccl" and b["dense_backend"] == "nccl"
-    if graph:  # RCCL: kernel segments as graphs, the collectives eager between them
+    if graph:  # RCCL: the all-reduces inside the graphs, the all-to-alls eager between
         assert b["capture"] == "segments", b["capture"]
+        # lookup (+ bottom MLP) | a2a | top + interaction bwd | a2a | top bucket all-reduce
+        # + bottom bwd | wait | bottom bucket all-reduce + embedding update + dense update
+        assert b["graphs"] == (4 if in_lookup else 5), b["graphs"]
     for s in range(3):
         ok, msg = fp32_close(b["Z"][s], a["Z"][s])
         assert ok, (s, "Z", msg)
@@ -659,24 +670,38 @@ def test_multi_gpu_schedule_on_one_rank_rccl_matches_single_gpu(graph, in_lookup
     assert ok, ("dense", msg)
 
 
-def test_emulated_rank_runs_the_w8_shapes():
+@pytest.mark.parametrize("whole", [False, True])
+def test_emulated_rank_runs_the_w8_shapes(whole):
     """bench --emulate-world 8 --emulate-rank 2: one GPU runs rank 2's kernels at the W = 8
     shapes (its 6 Terabyte tables over the global batch, B/8 dense rows, rank-major
-    features; collectives stubbed by trainer.EmulatedComm), eager and graph-replayed."""
+    features; collectives stubbed by trainer.EmulatedComm), eager and graph-replayed:
+    by default captured the way RCCL captures (four graphs around the eager all-to-alls),
+    with whole=True as one graph.  Both replays give bitwise the same state."""
     from dlrm_hip.trainer import DLRMTrainer, EmulatedComm, TrainerConfig
     spec, alloc = _c3_spec(8)
     cfg = TrainerConfig(**spec, loss_function="bce", learning_rate=0.1, allocation=alloc)
-    tr = DLRMTrainer(cfg, device="cuda:0", rank=2, world_size=8, comm=EmulatedComm(), seed=3)
-    assert tr.T_local == 6 and tr.distributed
-    bs = [tr.synthetic_batch(2048, 1, seed=i) for i in range(2)]
-    assert bs[0].X.shape[0] == 256 and bs[0].indices.numel() == 6 * 2048
-    tr.step(bs[0])
-    run = tr.capture(bs[1])
-    assert tr.capture_mode == "whole"  # the emulated collectives are device copies
-    run()
-    run()
-    torch.cuda.synchronize()
-    tr.check_errors()
-    loss = float(tr._bufs[(256, 2048)]["loss"].item())
-    assert np.isfinite(loss)
-    assert bool(torch.isfinite(tr.params).all())
+    out = []
+    for mode in ("eager", "graph"):
+        tr = DLRMTrainer(cfg, device="cuda:0", rank=2, world_size=8,
+                         comm=EmulatedComm(whole=whole), seed=3)
+        assert tr.T_local == 6 and tr.distributed
+        bs = [tr.synthetic_batch(2048, 1, seed=i) for i in range(2)]
+        assert bs[0].X.shape[0] == 256 and bs[0].indices.numel() == 6 * 2048
+        tr.step(bs[0])
+        if mode == "graph":
+            run = tr.capture(bs[1])
+            assert tr.capture_mode == ("whole" if whole else "segments")
+            assert tr.graphs_per_step == (1 if whole else 4), tr.graphs_per_step
+            run()
+            run()
+        else:
+            tr.step(bs[1])
+            tr.step(bs[1])
+        torch.cuda.synchronize()
+        tr.check_errors()
+        loss = float(tr._bufs[(256, 2048)]["loss"].item())
+        assert np.isfinite(loss)
+        assert bool(torch.isfinite(tr.params).all())
+        out.append((tr.params.clone(), tr.weights.clone(), loss))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2]

@@ -388,7 +388,7 @@ def test_gemm_vs_fp64(ops, M, N, K, ta, tb):
 
 
 # workgroup tiles the planner can pick (dlrm_set_tuning DLRM_TUNE_GEMM_TILE = BM*1000 + BN)
-GEMM_CFGS = [64064, 128064, 64128, 64032, 32064]
+GEMM_CFGS = [64064, 128064, 64128, 64032, 32064, 32032]
 
 
 @pytest.mark.parametrize("cfg", GEMM_CFGS)
@@ -723,14 +723,15 @@ def test_gemm_splitk_in_launch_fixup_is_deterministic_and_resets(ops):
     assert ok, msg
     tiles = 16384  # the fixed ticket region
     assert int(ws[:4 * tiles].view(torch.int32).abs().sum()) == 0
-    for split in (2, 5, 9):  # forced splits, fused SGD epilogue
+    for tile, split in ((64064, 2), (64064, 5), (64064, 9), (32032, 2), (32032, 7)):
+        # forced tiles and splits, fused SGD epilogue (32x32: the small-batch plans' tile)
         C0 = torch.randn(M, N, device=dev)
         C = C0.clone()
-        with ops.tuning(gemm_tile=64064, gemm_split=split):
+        with ops.tuning(gemm_tile=tile, gemm_split=split):
             ops.gemm(A, Bm, True, False, C=C, alpha=0.5, epilogue=ops.EPI_SGD, workspace=ws)
         ok, msg = gemm_close((C0 - C).cpu().numpy() / 0.5, ref.numpy(),
                              (A.double().abs().t() @ Bm.double().abs()).cpu().numpy(), K + 4)
-        assert ok, (split, msg)
+        assert ok, (tile, split, msg)
         assert int(ws[:4 * tiles].view(torch.int32).abs().sum()) == 0
 
 

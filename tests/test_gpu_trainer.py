@@ -501,6 +501,9 @@ def test_gather_fused_step_matches_pooled_path(graph):
         assert torch.equal(a, b)
 
 
+C4_TRAJ_CAPS = {"flips": 4, "aligned": 4, "ill_loss": 64, "bound": 4}
+
+
 @pytest.mark.parametrize("lr", [1e-4, 1e-3])
 def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     """C4 (QR mult, 4 collisions, threshold 200 + RWSAdagrad) at the Terabyte widths (D = 128,
@@ -514,8 +517,19 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     pre-activation within rounding of 0 (tests/relu_align.py), and the oracle then follows
     the engine's decision.  lr 1e-4 is the bench's C4 lr (no saturation); at 1e-3 the
     reference's own trajectory swings through saturation (tools/c4_lr_probe.py) and the
-    engine must follow it; on saturated steps the engine's loss is checked against the
-    clamped BCE of its own Z (nn.BCELoss clamps log at -100)."""
+    engine must follow it.  On saturated steps the engine's loss must lie in the interval
+    the ORACLE's logits allow (relu_align.loss_interval: every sample's clamped BCE term at
+    z -+ tau, widened by one ulp of p); the engine's own Z plays no part there.
+
+    Caps (VERDICT r05 "What's weak" #1; the logged runs of r05/r06 are in the comments):
+      * explained ReLU flips <= C4_TRAJ_CAPS["flips"] (logged: 0 at lr 1e-4, 1 at 1e-3);
+      * saturated-head samples aligned <= C4_TRAJ_CAPS["aligned"] (logged: 0, 0);
+      * samples with an ill-conditioned loss term <= C4_TRAJ_CAPS["ill_loss"] over the 10
+        steps;
+      * elements explained beyond 1e-5 <= 1e-5 of the elements compared (logged: 0 and 4 of
+        ~7.6 M), of which those explained ONLY by AdagradBound <= C4_TRAJ_CAPS["bound"],
+        each with an error <= 0.1 lr (one Adagrad step moves an element by ~lr at most;
+        logged: 3.1e-5 and 3.3e-5 at lr 1e-3, profiles/r05_c4_explain_probe.txt)."""
     import bench
     import relu_align as RA
     DLRMTrainer, TrainerConfig = _trainer()
@@ -543,6 +557,7 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     rng = np.random.RandomState(1)
     losses = []
     n_loss_checked = 0
+    n_ill_loss = 0
     for s in range(10):
         X, lS_o, lS_i, T = _rand_batch(rng, rows, B, 1, bot[0], "bce")
         Z, E = tr.step(tr.make_batch(X, lS_o, lS_i, T))
@@ -573,11 +588,12 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
             n_loss_checked += 1
             ok, msg = fp32_close(E.cpu().numpy(), [Er.item()])
             assert ok, (s, "loss", losses, msg)
-        else:  # the engine's loss from its own Z, clamped as nn.BCELoss clamps log
-            p, t = Z.double().cpu(), torch.tensor(T, dtype=torch.float64).view(-1)
-            bce = -(t * torch.log(p).clamp(min=-100) + (1 - t) * torch.log1p(-p).clamp(min=-100))
-            ok, msg = fp32_close(E.cpu().numpy(), [float(bce.mean())], atol=1e-4)
-            assert ok, (s, "saturated loss", losses, msg)
+        else:  # saturated: the interval the oracle's own logits allow (loss_interval)
+            lo, hi, n_ill = RA.loss_interval(*head.seen[s])
+            n_ill_loss += n_ill
+            tol = 1e-5 * max(1.0, abs(Er.item()))
+            assert lo - tol <= E.item() <= hi + tol, (s, "saturated loss", E.item(), lo, hi,
+                                                      Er.item(), n_ill)
     print("C4 losses (engine, oracle):", losses)
     assert n_loss_checked == 10 if lr <= 1e-4 else n_loss_checked >= 1, n_loss_checked
     ok, msg, flips = RA.report(relus)
@@ -587,23 +603,20 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
         assert ok, msg
     ok, msg, _ = RA.report(tw.relus)
     assert ok, ("permuted twin", msg)
-    print(f"explained ReLU flips: {flips}; saturated-head samples aligned: {head.aligned}")
     torch.cuda.synchronize()
     tr.check_errors()
-    n_expl = 0
+    st = RA.ExplainStats()
     for t, (e, e2) in enumerate(zip(ref.emb_l, tw.model.emb_l)):
         got_w, got_m = tr.table(t), tr.table_momentum(t)
         parts = [(e.weight_q, e2.weight_q, got_w[0], got_m[0]),
                  (e.weight_r, e2.weight_r, got_w[1], got_m[1])] \
             if hasattr(e, "weight_q") else [(e.weight, e2.weight, got_w, got_m)]
         for p, p2, gw, gm in parts:
-            ok, msg, ne = tw.close(gw.cpu().numpy(), p, p2, f"table {t}")
+            ok, msg, _ = tw.close(gw.cpu().numpy(), p, p2, f"table {t}", st)
             assert ok, msg
-            n_expl += ne
-            ok, msg, ne = tw.close(gm.cpu().numpy(), opt.state[id(p)]["momentum"],
-                                   opt2.state[id(p2)]["momentum"], f"momentum {t}")
+            ok, msg, _ = tw.close(gm.cpu().numpy(), opt.state[id(p)]["momentum"],
+                                  opt2.state[id(p2)]["momentum"], f"momentum {t}", st)
             assert ok, msg
-            n_expl += ne
     lin = [m for seq in (ref.bot_l, ref.top_l) for m in seq if isinstance(m, torch.nn.Linear)]
     lin2 = [m for seq in (tw.model.bot_l, tw.model.top_l) for m in seq
             if isinstance(m, torch.nn.Linear)]
@@ -612,16 +625,22 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
             # beyond 1e-5 only where the oracle itself moves that much under a permuted
             # summation order, or where Adagrad's conditioning allows it
             # (relu_align.PermutedTwin, AdagradBound)
-            ok, msg, ne = RA.close_explained(got.cpu().numpy(), p, p2, ab.bound[id(p)], "dense")
+            ok, msg, _ = RA.close_explained(got.cpu().numpy(), p, p2, ab.bound[id(p)], "dense",
+                                            st)
             assert ok, msg
-            n_expl += ne
         for got, p, p2 in ((sW, L.weight, L2.weight), (sb, L.bias, L2.bias)):
-            ok, msg, ne = tw.close(got.cpu().numpy(), opt.state[id(p)]["sum"],
-                                   opt2.state[id(p2)]["sum"], "adagrad sum")
+            ok, msg, _ = tw.close(got.cpu().numpy(), opt.state[id(p)]["sum"],
+                                  opt2.state[id(p2)]["sum"], "adagrad sum", st)
             assert ok, msg
-            n_expl += ne
-    print(f"elements beyond 1e-5 explained (permuted-order spread or Adagrad conditioning): "
-          f"{n_expl}")
+    print(f"lr {lr}: explained ReLU flips {flips}; saturated-head samples aligned "
+          f"{head.aligned}; ill-conditioned loss terms {n_ill_loss}; {st}")
+    caps = C4_TRAJ_CAPS
+    assert flips <= caps["flips"], flips
+    assert head.aligned <= caps["aligned"], head.aligned
+    assert n_ill_loss <= caps["ill_loss"], n_ill_loss
+    assert st.n_explained <= 1e-5 * st.compared, st
+    assert st.n_bound <= caps["bound"], st
+    assert st.max_bound_err <= 0.1 * lr, st
 
 
 @pytest.mark.parametrize("graph", [False, True])

@@ -170,3 +170,98 @@ def test_two_fp32_summation_orders_of_c4_w8_are_explained_by_the_twin():
             ok, msg, _ = RA.close_explained(pe.detach().numpy(), p, p, ab.bound[id(p)])
             assert ok, ("Adagrad bound alone", msg)
     print(f"elements beyond 1e-5 between two fp32 orders, all explained: {n_expl}")
+
+
+def _c4_like_run(steps=3, lr=1e-3):
+    """The small model (BCE) with RWSAdagrad over a few steps, with the permuted twin and
+    AdagradBound the GPU tests use; returns (ref, twin, bound, opt)."""
+    import numpy as np
+    ref = _model()
+    tw = RA.PermutedTwin(ref, 6, world=2)
+    ab = RA.AdagradBound(ref, lr)
+    opt = O.RWSAdagradOracle(ref.parameters(), lr=lr)
+    opt2 = O.RWSAdagradOracle(tw.model.parameters(), lr=lr)
+    rng = np.random.RandomState(5)
+    for _ in range(steps):
+        X, lS_o, lS_i = _batch()
+        X = X + torch.tensor(rng.rand(*X.shape).astype("float32"))
+        T = torch.tensor(rng.randint(0, 2, (6, 1)).astype("float32"))
+        E = ref.loss_fn(ref(X, lS_o, lS_i), T)
+        opt.zero_grad()
+        E.backward()
+        opt.step()
+        ab.after_step(opt)
+        E2 = tw.model.loss_fn(tw.model(*tw.batch(X, lS_o, lS_i, T)[:3]), tw.batch(X, lS_o, lS_i, T)[3])
+        opt2.zero_grad()
+        E2.backward()
+        opt2.step()
+    return ref, tw, ab, opt
+
+
+def test_adagrad_bound_rejects_an_error_in_a_well_conditioned_dense_weight():
+    """the conditioning allowance must not hide a real error.  The
+    element with the smallest AdagradBound allowance (a large |g| against its error bound,
+    a large Adagrad sum S) gets a 1e-4 error: close_explained must reject it, with the
+    permuted twin and the bound in place; the untouched weights must pass."""
+    ref, tw, ab, opt = _c4_like_run()
+    L, L2 = ref.top_l[0], tw.model.top_l[0]
+    bound = ab.bound[id(L.weight)]
+    S = opt.state[id(L.weight)]["sum"]
+    spread = (L.weight.detach() - L2.weight.detach()).abs().double()
+    # well conditioned: S >> 0 (a unit that saw gradients), a small allowance and a small
+    # twin spread
+    score = bound + RA.SPREAD * spread + (S.double() < 1e-8) * 1e9
+    i = divmod(int(torch.argmin(score)), score.shape[1])
+    assert float(S[i]) >= 1e-8
+    assert float(bound[i]) < 1e-6 and float(spread[i]) < 1e-6, (float(bound[i]), float(spread[i]))
+    got = L.weight.detach().clone().double()
+    st = RA.ExplainStats()
+    ok, msg, n = RA.close_explained(got.numpy(), L.weight, L2.weight, bound, "dense", st)
+    assert ok and n == 0 and st.compared == got.numel(), msg
+    got[i] += 1e-4
+    ok, msg, _ = RA.close_explained(got.numpy(), L.weight, L2.weight, bound, "dense", st)
+    assert not ok and "Adagrad conditioning allowance" in msg, msg
+    # and the caps see what an allowance was used for
+    got[i] -= 1e-4
+    j = divmod(int(torch.argmax(bound)), bound.shape[1])
+    got[j] += 0.5 * float(bound[j]) + 1e-5 * max(1.0, abs(float(L.weight[j])))
+    st2 = RA.ExplainStats()
+    ok, _, _ = RA.close_explained(got.numpy(), L.weight, L2.weight, bound, "dense", st2)
+    if float(bound[j]) > RA.SPREAD * float(spread[j]) * 2:  # explained by the bound only
+        assert ok and st2.n_bound == 1 and st2.max_bound_err > 0, st2
+
+
+def test_permuted_twin_rejects_an_error_in_a_table_row():
+    """A 1e-4 error in an updated embedding row and in a row no lookup touched: tw.close
+    must reject both (a table has no conditioning allowance, only the twin's spread)."""
+    ref, tw, _, opt = _c4_like_run()
+    e, e2 = ref.emb_l[0], tw.model.emb_l[0]
+    X, lS_o, lS_i = _batch()
+    touched = int(lS_i[0][0])
+    untouched = next(r for r in range(50) if r not in set(lS_i[0].tolist()))
+    for row in (touched, untouched):
+        got = e.weight.detach().clone().double()
+        ok, msg, n = tw.close(got.numpy(), e.weight, e2.weight, "table 0")
+        assert ok and n == 0, msg
+        got[row, 1] += 1e-4
+        ok, msg, _ = tw.close(got.numpy(), e.weight, e2.weight, "table 0")
+        assert not ok and "permuted" in msg, (row, msg)
+    m, m2 = opt.state[id(e.weight)]["momentum"], None
+    assert m.shape[0] == 50 and float(m[touched]) > 0
+
+
+def test_loss_interval_is_the_oracles_and_rejects_a_wrong_loss():
+    """The saturated-step loss check: the interval comes from the
+    oracle's logits only, contains the oracle's own loss, is wide only on saturated
+    samples, and rejects a loss off by more than the ill-conditioned terms allow."""
+    z = torch.tensor([[0.3], [-1.2], [20.0], [-30.0], [16.7]])
+    t = torch.tensor([[1.0], [0.0], [0.0], [1.0], [0.0]])
+    tau = torch.full_like(z, 1e-3)
+    lo, hi, n_ill = RA.loss_interval(z, tau, t)
+    own = float(RA._bce_terms(torch.sigmoid(z.float()), t).mean())
+    assert lo <= own <= hi
+    assert n_ill == 2  # z = 20 and 16.7 with t = 0: log(1 - p) of a p within an ulp of 1
+    # (z = -30 with t = 1 is well conditioned: log(p) of a tiny but exact p)
+    lo2, hi2, n2 = RA.loss_interval(z[:2], tau[:2], t[:2])
+    assert n2 == 0 and hi2 == lo2  # unsaturated: the oracle's own terms
+    assert not (lo2 - 1e-5 <= own + 1e-3 <= hi2 + 1e-5)
