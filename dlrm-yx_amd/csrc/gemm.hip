@@ -99,13 +99,16 @@ __device__ __forceinline__ int swz_kc(int r) {
 // the C3 step, profiles/r05_gemm_swizzle_ab.txt).
 template <int MN, int BKT, bool KC, bool VEC, int NT, bool SWZ = false>
 struct Stage {
-  static_assert(!SWZ || (BKT == 32 && MN >= 32), "swizzled images: BKT 32, MN >= 32");
-  static constexpr int PITCH = SWZ ? (KC ? BKT : MN) : (KC ? BKT + 4 : MN + 4);
-  static constexpr int SIZE = KC ? MN * PITCH : BKT * PITCH;  // floats per LDS buffer
+  static_assert(!SWZ || (BKT % 32 == 0 && MN >= 32), "swizzled images: BKT 32 U, MN >= 32");
+  static constexpr int PITCH = SWZ ? (KC ? 32 : MN) : (KC ? BKT + 4 : MN + 4);
+  // floats per LDS buffer (swizzled KC: BKT / 32 sub-images [MN][32], one per 32-deep
+  // sub-tile, each laid out exactly as the BKT = 32 image)
+  static constexpr int SIZE = SWZ ? MN * BKT : (KC ? MN * PITCH : BKT * PITCH);
   // float offset of element (mn, k) in the image (KC: k % 4 == 0 addresses a whole chunk)
   __device__ __forceinline__ static int at(int mn, int k) {
     if constexpr (!SWZ) return KC ? mn * PITCH + k : k * PITCH + mn;
-    else if constexpr (KC) return mn * PITCH + 4 * ((k >> 2) ^ swz_kc(mn)) + (k & 3);
+    else if constexpr (KC)
+      return ((k >> 5) * MN + mn) * 32 + 4 * (((k & 31) >> 2) ^ swz_kc(mn)) + (k & 3);
     else return k * PITCH + (mn ^ (((k >> 3) & 1) << 4));
   }
   static constexpr int NV = MN * BKT / 4 / NT;               // float4 per thread
@@ -113,7 +116,11 @@ struct Stage {
   float4 regs[NV];
 
   __device__ __forceinline__ void coords(int q, int& mn, int& k) const {
-    if constexpr (KC) {
+    if constexpr (KC && SWZ) {  // sub-image, then row, then 8 chunks of a 32-deep row
+      const int u = q / (MN * 8), r = q - u * (MN * 8);
+      mn = r >> 3;
+      k = 32 * u + 4 * (r & 7);
+    } else if constexpr (KC) {
       mn = q / (BKT / 4);
       k = 4 * (q % (BKT / 4));
     } else {
@@ -198,10 +205,11 @@ struct Stage {
   // Pipelined fetch with per-thread offsets precomputed once (32-bit, bytes, at K-tile 0 of
   // the split) so a K-tile costs one add + one compare per float4.  Out-of-range float4s
   // read as zeros: rows/columns past the operand are outside the buffer descriptor except
-  // (KC) the columns k >= K of a row and (!KC) the columns mn >= MN of a row, masked here.
+  // (KC) the columns k >= K of a row and (!KC) the columns mn >= MN of a row, masked here,
+  // and every k at or past the split's end (klim: a deep K-tile may overhang it).
   struct Fetch {
     int off[NV];   // byte offset at tile 0 (or -1: masked for every tile)
-    int kpos[NV];  // KC: the float4's k within a K-tile
+    int kpos[NV];  // the float4's k within a K-tile
   };
   __device__ __forceinline__ void fetch_init(Fetch& f, int64_t ld, int64_t mn0, int64_t mnlim,
                                              int64_t kbeg, int tid) const {
@@ -217,7 +225,7 @@ struct Stage {
   }
   __device__ __forceinline__ void fetch4(int v, const Fetch& f, __amdgpu_buffer_rsrc_t rsrc,
                                          int tile_step, int t, int kt0, int klim) {
-    const bool ok = f.off[v] >= 0 && (!KC || kt0 + f.kpos[v] < klim);
+    const bool ok = f.off[v] >= 0 && kt0 + f.kpos[v] < klim;
     const int off = ok ? f.off[v] + t * tile_step : 0x7ffffff0;
     regs[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
   }
@@ -463,18 +471,25 @@ __device__ __forceinline__ void finish_tile(const GemmParams& p, const f32x4 (&a
 
 
 // One output tile (and K split) of problem p: the software-pipelined 16x16x4 body.  The
-// workgroup is WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile.
-template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS>
+// workgroup is WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile.  A K-tile (one
+// LDS stage, one barrier) is U sub-tiles of 32: deeper stages (U = 2, 4) halve or quarter
+// the barriers and read the next sub-tile's fragments from the SAME buffer during the
+// current one's MFMAs.  The MFMA sequence over k is the U = 1 sequence for every U (sub-tile
+// after sub-tile, the same k-quarter permutation inside each): results are bitwise those of
+// U = 1 (a stage overhanging the split's end multiplies zeros).
+template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, bool RS, int U = 1>
 __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* smem) {
+  static_assert(U == 1 || U % 2 == 0, "sub-tiles per stage: 1 or even");
   constexpr int NT = WGM * WGN * 64;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(FM >= 1 && FN >= 1, "wave sub-tile");
-  constexpr int KL = kBK / 4;  // k-steps per K-tile (each lane group owns KL consecutive k)
-  using SA = Stage<BM, kBK, A_KC, true, NT, true>;
-  using SB = Stage<BN, kBK, B_KC, true, NT, true>;
-  constexpr int NS = SA::NV + SB::NV;  // staged float4 per thread per K-tile
-  static_assert(NS <= KL - 1, "staging must finish before the barrier step");
+  constexpr int KL = kBK / 4;  // k-steps per 32-deep sub-tile (a lane group owns KL consecutive k)
+  constexpr int BKT = kBK * U;  // k per LDS stage
+  using SA = Stage<BM, BKT, A_KC, true, NT, true>;
+  using SB = Stage<BN, BKT, B_KC, true, NT, true>;
+  constexpr int NS = SA::NV + SB::NV;  // staged float4 per thread per stage
+  static_assert(NS <= U * KL - 1, "staging must finish before the barrier step");
 
   const int tile = lb / p.splits;
   const int split = lb - tile * p.splits;
@@ -502,7 +517,8 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
 #pragma unroll
   for (int i = 0; i < FM; ++i) rs[i] = 0.f;
 
-  const int nk = (int)((kend - kbeg + kBK - 1) / kBK);
+  const int nsub = (int)((kend - kbeg + kBK - 1) / kBK);
+  const int nk = (nsub + U - 1) / U;
   SA sa;
   SB sb;
   // buffer descriptors over exactly the addressed extent (host guarantees < 2 GiB)
@@ -516,14 +532,14 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   typename SB::Fetch fb;
   sa.fetch_init(fa, p.lda, m0, p.M, kbeg, tid);
   sb.fetch_init(fb, p.ldb, n0, p.N, kbeg, tid);
-  const int a_step = A_KC ? kBK * 4 : (int)(kBK * p.lda * 4);
-  const int b_step = B_KC ? kBK * 4 : (int)(kBK * p.ldb * 4);
-  const int kb32 = (int)kbeg, K32 = (int)p.K;
-  auto fetch_one = [&](int c, int t) {  // staged float4 c of K-tile t (unused past nk)
+  const int a_step = A_KC ? BKT * 4 : (int)(BKT * p.lda * 4);
+  const int b_step = B_KC ? BKT * 4 : (int)(BKT * p.ldb * 4);
+  const int kb32 = (int)kbeg, kend32 = (int)kend;
+  auto fetch_one = [&](int c, int t) {  // staged float4 c of stage t (zeros past the split)
     if (c < SA::NV)
-      sa.fetch4(c, fa, ra, a_step, t, kb32 + t * kBK, K32);
+      sa.fetch4(c, fa, ra, a_step, t, kb32 + t * BKT, kend32);
     else
-      sb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * kBK, K32);
+      sb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * BKT, kend32);
   };
   auto put_one = [&](int c, float* buf) {
     if (c < SA::NV)
@@ -531,17 +547,29 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
     else
       sb.store_one(c - SA::NV, buf + SA::SIZE, tid);
   };
-  auto read_frags = [&](const float* buf, float (&a)[FM][KL], float (&b)[FN][KL]) {
+  auto read_frags = [&](const float* buf, int u, float (&a)[FM][KL], float (&b)[FN][KL]) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i) sa.template frag<KL>(buf, wm0 + i * 16, l16, kq * KL, a[i]);
+    for (int i = 0; i < FM; ++i)
+      sa.template frag<KL>(buf, wm0 + i * 16, l16, u * kBK + kq * KL, a[i]);
 #pragma unroll
     for (int j = 0; j < FN; ++j)
-      sb.template frag<KL>(buf + SA::SIZE, wn0 + j * 16, l16, kq * KL, b[j]);
+      sb.template frag<KL>(buf + SA::SIZE, wn0 + j * 16, l16, u * kBK + kq * KL, b[j]);
+  };
+  auto mfma_step = [&](float (&ca)[FM][KL], float (&cb)[FN][KL], int s) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][s], cb[j][s], acc[i][j], 0, 0, 0);
+    if constexpr (RS) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][s]);
+    }
   };
 
   float a[FM][KL], b[FN][KL];
-  // Prologue: tile 0 -> LDS buffer 0, tile 1 staged in registers, tile 0 fragments read.
-  // Every fetch is unconditional: tiles past nk load zeros (their LDS image is never used).
+  // Prologue: stage 0 -> LDS buffer 0, stage 1 staged in registers, sub-tile 0 fragments
+  // read.  Every fetch is unconditional: stages past nk load zeros (never used).
 #pragma unroll
   for (int c = 0; c < NS; ++c) fetch_one(c, 0);
 #pragma unroll
@@ -549,50 +577,58 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
 #pragma unroll
   for (int c = 0; c < NS; ++c) fetch_one(c, 1);
   __syncthreads();
-  read_frags(smem, a, b);
+  read_frags(smem, 0, a, b);
 
-  // One K-tile: MFMAs on (ca, cb) with the staging of tile t+1 / fetch of t+2 interleaved,
-  // barrier, then tile t+1's fragments into (na, nb) under the last k-step.  The loop is
-  // unrolled by two so the fragment sets ping-pong without register copies.
-  auto iteration = [&](int kt, float (&ca)[FM][KL], float (&cb)[FN][KL], float (&na)[FM][KL],
-                       float (&nb)[FN][KL]) {
+  // Sub-tile u of stage kt: MFMAs on (ca, cb) with the staging of stage kt+1 / fetch of kt+2
+  // interleaved (staged float4 g = u*KL + step); a non-final sub-tile first issues the reads
+  // of sub-tile u+1 into (na, nb) from the same buffer; the final one ends with the barrier
+  // and sub-tile 0 of stage kt+1 read under its last k-step.
+  auto subtile = [&](int kt, int u, float (&ca)[FM][KL], float (&cb)[FN][KL],
+                     float (&na)[FM][KL], float (&nb)[FN][KL]) {
+    const float* cur = smem + (kt & 1) * (SA::SIZE + SB::SIZE);
     float* nbuf = smem + ((kt + 1) & 1) * (SA::SIZE + SB::SIZE);
+    const bool last = u == U - 1;
+    if (!last) read_frags(cur, u + 1, na, nb);
 #pragma unroll
     for (int s = 0; s < KL - 1; ++s) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][s], cb[j][s], acc[i][j], 0, 0, 0);
-      if constexpr (RS) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][s]);
-      }
-      if (s < NS) {
-        put_one(s, nbuf);      // tile t+1 (staged last iteration) -> LDS
-        fetch_one(s, kt + 2);  // refill the register with tile t+2
+      mfma_step(ca, cb, s);
+      const int g = u * KL + s;
+      if (g < NS) {
+        put_one(g, nbuf);      // stage t+1 (staged last stage) -> LDS
+        fetch_one(g, kt + 2);  // refill the register with stage t+2
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the interleave: no hoisting across steps
     }
-    __syncthreads();  // tile t+1 is complete in LDS
-    read_frags(nbuf, na, nb);
-    __builtin_amdgcn_sched_barrier(0);  // issue the reads before the last step's MFMAs
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[i][KL - 1], cb[j][KL - 1], acc[i][j],
-                                                         0, 0, 0);
-    if constexpr (RS) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) rs[i] = add_f32(rs[i], ca[i][KL - 1]);
+    if (!last) {
+      mfma_step(ca, cb, KL - 1);
+      const int g = u * KL + KL - 1;
+      if (g < NS) {
+        put_one(g, nbuf);
+        fetch_one(g, kt + 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      __syncthreads();  // stage t+1 is complete in LDS
+      read_frags(nbuf, 0, na, nb);
+      __builtin_amdgcn_sched_barrier(0);  // issue the reads before the last step's MFMAs
+      mfma_step(ca, cb, KL - 1);
     }
   };
   float a1[FM][KL], b1[FN][KL];
-  for (int kt = 0; kt < nk; kt += 2) {
-    iteration(kt, a, b, a1, b1);
-    if (kt + 1 >= nk) break;
-    iteration(kt + 1, a1, b1, a, b);
+  if constexpr (U == 1) {  // fragment sets ping-pong across stages: unrolled by two
+    for (int kt = 0; kt < nk; kt += 2) {
+      subtile(kt, 0, a, b, a1, b1);
+      if (kt + 1 >= nk) break;
+      subtile(kt + 1, 0, a1, b1, a, b);
+    }
+  } else {  // an even number of sub-tiles per stage: every stage starts on (a, b)
+    for (int kt = 0; kt < nk; ++kt) {
+#pragma unroll
+      for (int u = 0; u < U; u += 2) {
+        subtile(kt, u, a, b, a1, b1);
+        subtile(kt, u + 1, a1, b1, a, b);
+      }
+    }
   }
 
   // Row sums: lanes l16, l16+16, l16+32, l16+48 hold the four k-quarters of row l16
@@ -645,11 +681,11 @@ __device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int U = 1>
 constexpr int group_smem_floats() {
-  // double-buffered A and B panels (unpadded swizzled images: the same size for every
-  // operand layout)
-  return 2 * (BM + BN) * kBK;
+  // double-buffered A and B panels of U 32-deep sub-tiles (unpadded swizzled images: the
+  // same size for every operand layout)
+  return 2 * (BM + BN) * kBK * U;
 }
 
 // Body kinds: the four operand layouts, plus 4 = layout 2 (wgrad) with the row sums.
@@ -658,7 +694,7 @@ __host__ __device__ constexpr int kind_bit(int layout, bool rs) { return 1 << (r
 // Up to kMaxGroup independent problems; block -> (problem, tile, split) after the XCD remap.
 // KINDS is the set of body kinds compiled in (a launch uses the smallest instantiation that
 // covers its problems: fewer bodies, fewer registers).
-template <int BM, int BN, int WGM, int WGN, int KINDS>
+template <int BM, int BN, int WGM, int WGN, int KINDS, int U = 1>
 __device__ __forceinline__ void group_body(const GemmGroup& g, int b, float* smem) {
   // Problems own consecutive PHYSICAL block ranges, so each one is dealt round-robin over
   // all eight XCDs (a remap across the whole launch would give each problem a few XCDs);
@@ -673,22 +709,22 @@ __device__ __forceinline__ void group_body(const GemmGroup& g, int b, float* sme
   if (p.mode == DLRM_GEMM_REDUCE) return reduce_body(p, lb);
   const int kind = (p.layout == 2 && p.ones_col >= 0) ? 4 : p.layout;
   if constexpr ((KINDS & 1) != 0)
-    if (kind == 0) return pipe_body<BM, BN, WGM, WGN, true, true, false>(p, lb, smem);
+    if (kind == 0) return pipe_body<BM, BN, WGM, WGN, true, true, false, U>(p, lb, smem);
   if constexpr ((KINDS & 2) != 0)
-    if (kind == 1) return pipe_body<BM, BN, WGM, WGN, true, false, false>(p, lb, smem);
+    if (kind == 1) return pipe_body<BM, BN, WGM, WGN, true, false, false, U>(p, lb, smem);
   if constexpr ((KINDS & 4) != 0)
-    if (kind == 2) return pipe_body<BM, BN, WGM, WGN, false, false, false>(p, lb, smem);
+    if (kind == 2) return pipe_body<BM, BN, WGM, WGN, false, false, false, U>(p, lb, smem);
   if constexpr ((KINDS & 8) != 0)
-    if (kind == 3) return pipe_body<BM, BN, WGM, WGN, false, true, false>(p, lb, smem);
+    if (kind == 3) return pipe_body<BM, BN, WGM, WGN, false, true, false, U>(p, lb, smem);
   if constexpr ((KINDS & 16) != 0)
-    if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true>(p, lb, smem);
+    if (kind == 4) return pipe_body<BM, BN, WGM, WGN, false, false, true, U>(p, lb, smem);
 }
 
-template <int BM, int BN, int WGM, int WGN, int KINDS>
+template <int BM, int BN, int WGM, int WGN, int KINDS, int U = 1>
 __global__ __launch_bounds__(WGM * WGN * 64, 2) void gemm_group_kernel(
     const GemmGroup g) {
-  __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN>()];
-  group_body<BM, BN, WGM, WGN, KINDS>(g, blockIdx.x, smem);
+  __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN, U>()];
+  group_body<BM, BN, WGM, WGN, KINDS, U>(g, blockIdx.x, smem);
 }
 
 // The group plus one pass of a deferred embedding update (tbe_bwd_roles.hpp) in the same
@@ -860,6 +896,9 @@ constexpr PlanEntry kPlans[] = {
 // profiles/r05_gemm_plans_resweep.txt).  (Other
 // wave layouts of pipe_body - 64x32 on 2x1, 32x64 on 1x2, 128x32 on 4x1 - measured slower
 // on every DLRM shape: tools/gemm_cfg_ab.py, profiles/r02_gemm_cfg_ab.txt.)
+// (Deep LDS stages - pipe_body U = 2 / 4, two or four 32-deep sub-tiles per barrier - are
+// bitwise the same and measured slower at every tile on every C3 shape:
+// profiles/r06_gemm_deep_stage_lab.txt.  The product compiles U = 1 only.)
 bool tile_ok(int bm, int bn, int wm, int wn) {
   return wm == 2 && wn == 2 &&
          ((bm == 64 && bn == 64) || (bm == 128 && bn == 64) || (bm == 64 && bn == 128) ||
@@ -961,7 +1000,7 @@ size_t group_ws_bytes(int n, const Desc* d, const Tile& t, const Plan* pl) {
   return any ? c.used + 256 : 0;
 }
 
-template <int BM, int BN, int WGM = 2, int WGN = 2>
+template <int BM, int BN, int U = 1, int WGM = 2, int WGN = 2>
 int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes,
                  const LaunchRole* role, int phase, hipStream_t st) {
   constexpr int NT = WGM * WGN * 64;
@@ -1005,7 +1044,7 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   for (int i = 0; i < n; ++i)
     if (g.p[i].mode != DLRM_GEMM_REDUCE)
       kinds |= kind_bit(g.p[i].layout, g.p[i].layout == 2 && g.p[i].ones_col >= 0);
-  if constexpr ((BM == 64 && BN == 32) || (BM == 32 && BN == 64)) {
+  if constexpr (U == 1 && ((BM == 64 && BN == 32) || (BM == 32 && BN == 64))) {
     if (role) {  // + a deferred embedding-update pass (every body kind compiled in)
       static_assert(NT == 256, "the update passes run 256-thread workgroups");
       DLRM_REQUIRE((int64_t)role->blocks + blocks < INT32_MAX, DLRM_ERR_UNSUPPORTED,
@@ -1021,7 +1060,8 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
       return DLRM_OK;
     }
   } else {
-    DLRM_REQUIRE(!role, DLRM_ERR_UNSUPPORTED, "dlrm_gemm_f32_group_role: tile %dx%d", BM, BN);
+    DLRM_REQUIRE(!role, DLRM_ERR_UNSUPPORTED, "dlrm_gemm_f32_group_role: tile %dx%d/%d", BM, BN,
+                 U);
   }
   const dim3 grid(g.total), block(NT);
   // instantiations: every single kind, the MLP-backward pairs (dgrad + wgrad with / without
@@ -1029,12 +1069,12 @@ int launch_group(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes
   switch (kinds) {
 #define K_(M_)                                                                          \
   case M_:                                                                             \
-    hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_>), grid, block, 0, st, g); \
+    hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, M_, U>), grid, block, 0, st, g); \
     break;
     K_(0) K_(1) K_(2) K_(4) K_(8) K_(16) K_(2 | 16) K_(2 | 4) K_(4 | 16)
 #undef K_
     default:
-      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, 31>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemm_group_kernel<BM, BN, WGM, WGN, 31, U>), grid, block, 0, st, g);
   }
   DLRM_LAUNCH_CHECK("dlrm_gemm_f32");
   return DLRM_OK;

@@ -501,7 +501,7 @@ def test_gather_fused_step_matches_pooled_path(graph):
         assert torch.equal(a, b)
 
 
-C4_TRAJ_CAPS = {"flips": 4, "aligned": 4, "ill_loss": 64, "bound": 4}
+C4_TRAJ_CAPS = {"flips": 2, "aligned": 2, "ill_loss": 8, "bound": 4}
 
 
 @pytest.mark.parametrize("lr", [1e-4, 1e-3])
@@ -521,15 +521,16 @@ def test_c4_terabyte_widths_trajectory_vs_oracle(lr):
     the ORACLE's logits allow (relu_align.loss_interval: every sample's clamped BCE term at
     z -+ tau, widened by one ulp of p); the engine's own Z plays no part there.
 
-    Caps (VERDICT r05 "What's weak" #1; the logged runs of r05/r06 are in the comments):
-      * explained ReLU flips <= C4_TRAJ_CAPS["flips"] (logged: 0 at lr 1e-4, 1 at 1e-3);
-      * saturated-head samples aligned <= C4_TRAJ_CAPS["aligned"] (logged: 0, 0);
-      * samples with an ill-conditioned loss term <= C4_TRAJ_CAPS["ill_loss"] over the 10
-        steps;
-      * elements explained beyond 1e-5 <= 1e-5 of the elements compared (logged: 0 and 4 of
-        ~7.6 M), of which those explained ONLY by AdagradBound <= C4_TRAJ_CAPS["bound"],
-        each with an error <= 0.1 lr (one Adagrad step moves an element by ~lr at most;
-        logged: 3.1e-5 and 3.3e-5 at lr 1e-3, profiles/r05_c4_explain_probe.txt)."""
+    Caps (VERDICT r05 "What's weak" #1), from the logged runs (r05 logs; r06
+    gpurun_out/r06/pytest_caps.log, profiles/r06_parity_caps.txt):
+      * explained ReLU flips <= 2 (logged: r05 0 at lr 1e-4 / 1 at 1e-3; r06 1 / 0);
+      * saturated-head samples aligned <= 2 (logged: 0 / 0 in every run);
+      * samples with an ill-conditioned loss term <= 8 over the 10 steps (logged: 0 / 0);
+      * elements explained beyond 1e-5 <= 1e-5 of the elements compared (13.2 M; logged: r06
+        0 at lr 1e-4, 4 at 1e-3 - 1 by the permuted twin, 3 by AdagradBound), those
+        explained ONLY by AdagradBound <= 4, each with an error <= 0.1 lr (one Adagrad step
+        moves an element by ~lr at most; logged: 2.8e-5 = 0.028 lr, r05 3.3e-5,
+        profiles/r05_c4_explain_probe.txt)."""
     import bench
     import relu_align as RA
     DLRMTrainer, TrainerConfig = _trainer()

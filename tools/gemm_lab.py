@@ -1,7 +1,8 @@
-"""GEMM body lab (experiments, not product code): times candidate bodies of
-tools/gemm_lab.hip (tools/_lab/libgemm_lab.so, built by `python tools/gemm_lab.py --build`
-on the CPU) on the C3 training-step GEMMs and checks every result bitwise against the
-library's own launch of the same problem.
+"""GEMM body lab (experiments, not product code): times the library's pipe_body at the
+tiles / occupancies / LDS-stage depths of tools/gemm_lab.hip (tools/_lab/libgemm_lab.so,
+built by `python tools/gemm_lab.py --build` on the CPU) on the C3 training-step GEMMs and
+checks every result bitwise against the library's own launch of the same problem
+(cfg = U * 100 + tile, U = 32-deep sub-tiles per LDS stage).
 
     python tools/gemm_lab.py [--cfgs 100,200,...] [--splits 1,2,4] [--shapes fwd,dgrad,wgrad]
 """
@@ -28,7 +29,7 @@ def build():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
-    ap.add_argument("--cfgs", default="100,101,102,103,200,201,202,203,204,205,206,207,208,209")
+    ap.add_argument("--cfgs", default="100,101,102,103,105,107,200,201,202,203,205,207,400,401")
     ap.add_argument("--splits", default="1,2,4")
     ap.add_argument("--wsplits", default="1,2,4,8")
     ap.add_argument("--shapes", default="fwd,dgrad,wgrad")

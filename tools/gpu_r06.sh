@@ -1,0 +1,76 @@
+#!/bin/bash
+# Round-6 GPU sessions (one stage per gpurun call):
+#   bash tools/gpu_r06.sh tests   - pytest -m gpu (per-test timeout) + smoke()
+#   bash tools/gpu_r06.sh bench   - default bench line + rocprofv3 kernel trace + PMC
+#   bash tools/gpu_r06.sh configs - bench lines of C1 (small), C2 (kaggle), C4
+set -o pipefail
+STAGE=$1
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/${OUTNAME:-r06}
+mkdir -p "$OUT"
+cd "$ROOT" || exit 1
+case $STAGE in
+tests)
+  # optional: K="expr" selects a subset (pytest -k)
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider ${K:+-k "$K"} > "$OUT/pytest_gpu.log" 2>&1 || { tail -20 "$OUT/pytest_gpu.log"; exit 1; }
+  tail -2 "$OUT/pytest_gpu.log"
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+    || { tail -5 "$OUT/smoke.log"; exit 1; }
+  tail -1 "$OUT/smoke.log"
+  ;;
+bench)
+  timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
+  tail -c 600 "$OUT/bench.json"
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o kt \
+    -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 200 --warmup 20 \
+    > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || exit $?
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc \
+      -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-kernel-timing --no-graph --preheat-ms 0 --steps 10 \
+      --warmup 2 > "$OUT/pmc_$C.json" 2> "$OUT/pmc_$C.err" || exit $?
+  done
+  echo "bench stage done"
+  ;;
+configs)
+  for cfg in small kaggle terabyte_qr_rwsadagrad; do
+    timeout -k 10 400 python bench.py --config $cfg > "$OUT/bench_$cfg.json" 2> "$OUT/bench_$cfg.err" \
+      || exit $?
+    echo "$cfg: $(head -c 200 "$OUT/bench_$cfg.json")"
+  done
+  # the C3 widths at the W = 8 per-rank batch
+  timeout -k 10 400 python bench.py --batch 256 > "$OUT/bench_b256.json" 2> "$OUT/bench_b256.err" \
+    || exit $?
+  echo "b256: $(head -c 200 "$OUT/bench_b256.json")"
+  ;;
+esac
+# (pmc only: bash tools/gpu_r06.sh pmc)
+if [ "$STAGE" = pmc ]; then
+  cd /tmp && export TMPDIR=/tmp
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc \
+      -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-kernel-timing --no-graph --preheat-ms 0 \
+      --steps 10 --warmup 2 > "$OUT/pmc_$C.json" 2> "$OUT/pmc_$C.err" || exit $?
+  done
+  echo "pmc stage done"
+fi
+# emulated W = 8 ranks (one GPU): bash tools/gpu_r06.sh emulate
+if [ "$STAGE" = emulate ]; then
+  for R in ${RANKS:-2 0}; do
+    timeout -k 10 400 python bench.py ${ECFG:+--config $ECFG} --emulate-world 8 --emulate-rank $R \
+      --emulate-capture ${ECAP:-segments} --steps 300 --no-cpu-baseline \
+      > "$OUT/bench_emul8${ECFG:+_$ECFG}_${ECAP:-segments}_r$R.json" \
+      2> "$OUT/bench_emul8_r$R.err" || exit $?
+    echo "rank $R: $(head -c 300 "$OUT/bench_emul8${ECFG:+_$ECFG}_${ECAP:-segments}_r$R.json")"
+  done
+  timeout -k 10 400 python bench.py --batch 256 --no-cpu-baseline --steps 300 \
+    > "$OUT/bench_b256.json" 2> "$OUT/bench_b256.err" || exit $?
+  echo "b256: $(head -c 200 "$OUT/bench_b256.json")"
+fi
+# per-shape GEMM table vs hipBLASLt: bash tools/gpu_r06.sh blas
+if [ "$STAGE" = blas ]; then
+  GEMM_VS_BLAS_OUT="$OUT/gemm_vs_blas.json" timeout -k 10 300 python -u tools/gemm_vs_blas.py ${BATCHES:-2048 256} \
+    > "$OUT/gemm_vs_blas.txt" 2>&1 || { tail -5 "$OUT/gemm_vs_blas.txt"; exit 1; }
+  tail -3 "$OUT/gemm_vs_blas.txt"
+fi
