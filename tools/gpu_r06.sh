@@ -74,3 +74,22 @@ if [ "$STAGE" = blas ]; then
     > "$OUT/gemm_vs_blas.txt" 2>&1 || { tail -5 "$OUT/gemm_vs_blas.txt"; exit 1; }
   tail -3 "$OUT/gemm_vs_blas.txt"
 fi
+# GEMM investigation: per-shape table vs hipBLASLt, hipBLASLt's kernel names (tile config), and
+# SQ counters of one C3 shape (library launch, lab cfgs, torch.mm): bash tools/gpu_r06.sh gemmprobe
+if [ "$STAGE" = gemmprobe ]; then
+  GEMM_VS_BLAS_OUT="$OUT/gemm_vs_blas.json" timeout -k 10 300 python -u tools/gemm_vs_blas.py 2048 256 \
+    > "$OUT/gemm_vs_blas.txt" 2>&1 || { tail -5 "$OUT/gemm_vs_blas.txt"; exit 1; }
+  tail -3 "$OUT/gemm_vs_blas.txt"
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/blas_kt" -o kt \
+    -- python3 "$ROOT/tools/gemm_vs_blas.py" 2048 --blas-only > "$OUT/blas_kt.txt" 2>&1 || exit $?
+  for SH in fwd1 wgrad1; do
+    P1="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
+    timeout -s KILL 120 rocprofv3 --pmc $P1 --output-format csv -d "$OUT/pmc_$SH" -o p1 \
+      -- python3 "$ROOT/tools/gemm_pmc_probe.py" $SH 101,105 > "$OUT/pmc_$SH.txt" 2>&1 || exit $?
+    P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES SQ_INSTS_SMEM SQ_LDS_IDX_ACTIVE"
+    timeout -s KILL 120 rocprofv3 --pmc $P2 --output-format csv -d "$OUT/pmc2_$SH" -o p2 \
+      -- python3 "$ROOT/tools/gemm_pmc_probe.py" $SH 101,105 > "$OUT/pmc2_$SH.txt" 2>&1 || exit $?
+  done
+  echo "gemmprobe done"
+fi
