@@ -13,7 +13,11 @@ namespace {
 template <int BM, int BN, int WGM, int WGN, int OCC, int KINDS, int U>
 __global__ __launch_bounds__(WGM * WGN * 64, OCC) void old_kernel(const GemmGroup g) {
   __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN, U>()];
-  group_body<BM, BN, WGM, WGN, KINDS, U>(g, blockIdx.x, smem);
+  // persistent form (grid < g.total): each workgroup walks the virtual blocks b, b + grid, ...
+  for (int b = blockIdx.x; b < g.total; b += gridDim.x) {
+    group_body<BM, BN, WGM, WGN, KINDS, U>(g, b, smem);
+    __syncthreads();  // the next tile's prologue rewrites the LDS images
+  }
 }
 
 template <int BM, int BN, int WGM, int WGN>
@@ -55,10 +59,24 @@ int lab_prepare(int n, const Desc* d, const Plan* pl, void* ws, size_t ws_bytes,
   return 0;
 }
 
+// Workgroups per CU capped at g_cap (> 0) by a dynamic-LDS pad: the dispatcher then cannot
+// pack more than g_cap of this launch's workgroups onto one CU (tests whether uneven packing
+// of the 2-6 that fit by registers / LDS is what the per-CU rate loses).
+int g_cap = 0;
+int g_persist = 0;  // > 0: grid = min(total, g_persist * 256) workgroups looping over the tiles
 template <int BM, int BN, int WGM, int WGN, int OCC, int U, int KINDS>
 void lab_go(const GemmGroup& g, hipStream_t st) {
-  const dim3 grid(g.total), block(WGM * WGN * 64);
-  hipLaunchKernelGGL((old_kernel<BM, BN, WGM, WGN, OCC, KINDS, U>), grid, block, 0, st, g);
+  const int nwg = g_persist > 0 && g.total > g_persist * 256 ? g_persist * 256 : g.total;
+  const dim3 grid(nwg), block(WGM * WGN * 64);
+  size_t pad = 0;
+  if (g_cap > 0) {
+    const size_t stat = group_smem_floats<BM, BN, U>() * sizeof(float);
+    const size_t per = 163840 / g_cap - 1024;
+    pad = per > stat ? per - stat : 0;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&old_kernel<BM, BN, WGM, WGN, OCC, KINDS, U>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
+  }
+  hipLaunchKernelGGL((old_kernel<BM, BN, WGM, WGN, OCC, KINDS, U>), grid, block, pad, st, g);
 }
 
 template <int BM, int BN, int WGM, int WGN, int OCC, int U>
@@ -91,6 +109,11 @@ extern "C" int lab_gemm(int32_t cfg, int32_t split, int32_t n, const dlrm_gemm_p
     else pl[i] = make_plan(split > 0 ? split : 1, d[i].K);
   }
   hipStream_t st = dlrm::as_stream(stream);
+  // cfg = persist * 10000 + cap * 1000 + U * 100 + tile: at most `cap` workgroups per CU;
+  // persist > 0: persist * 256 workgroups, each looping over tiles (b, b + grid, ...)
+  g_persist = cfg / 10000;
+  g_cap = (cfg / 1000) % 10;
+  cfg %= 1000;
   // cfg = U * 100 + tile: tile 0: 64x32, 1: 64x64, 2: 128x64, 3: 64x128, 4: 32x32,
   // 5: 128x64 on 4x2 waves, 6: 128x128 on 4x2 waves, 7: 64x64 at one workgroup per CU
   switch (cfg) {

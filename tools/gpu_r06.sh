@@ -93,3 +93,15 @@ if [ "$STAGE" = gemmprobe ]; then
   done
   echo "gemmprobe done"
 fi
+# W > 1 tail A/B (emulated W = 8, segment capture): bash tools/gpu_r06.sh emulab
+if [ "$STAGE" = emulab ]; then
+  for R in ${RANKS:-2}; do
+    for TR in 0 1 0 1; do
+      timeout -k 10 300 python bench.py ${ECFG:+--config $ECFG} --emulate-world 8 --emulate-rank $R \
+        --tbe-role $TR --steps 300 --no-cpu-baseline --no-kernel-timing \
+        > "$OUT/emulab${ECFG:+_$ECFG}_r${R}_tr$TR.json" 2> "$OUT/emulab_r$R.err" || exit $?
+      python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[1].split('/')[-1], d['emulated'].get('ms_per_step', d.get('ms_per_step')), d['ms_per_step_p10_p50_p90'])" \
+        "$OUT/emulab${ECFG:+_$ECFG}_r${R}_tr$TR.json"
+    done
+  done
+fi
