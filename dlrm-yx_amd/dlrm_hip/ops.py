@@ -659,6 +659,19 @@ def gemm_partial_bytes(M: int, N: int, splits: int) -> int:
     return _lib.query("dlrm_gemm_f32_partial_bytes", M, N, splits)
 
 
+def sgd_job(param: torch.Tensor, grad: torch.Tensor, lr: float):
+    """param -= lr * grad (flat fp32, numel % 4 == 0, 16-B aligned) as a one-split REDUCE job:
+    an elementwise GEMM-group problem, so the update rides on a launch that exists anyway
+    (C = SGD(alpha * sum_s part[s]) with one split: param - lr * grad, the SGD epilogue's
+    rounding)."""
+    _check_cuda(param, grad)
+    n = param.numel()
+    if grad.numel() != n or n % 4 or param.data_ptr() % 16 or grad.data_ptr() % 16:
+        raise ValueError("sgd_job: flat fp32 tensors of equal size, numel % 4 == 0, 16-B aligned")
+    return _lib.GemmProblem(0, 0, 1, n, 0, float(lr), None, 0, None, 0, param.data_ptr(), n,
+                            EPI_SGD, None, None, 0, -1, GEMM_REDUCE, 1, grad.data_ptr())
+
+
 def reduce_problem(pr_partial):
     """The REDUCE problem finishing a PARTIAL one (same C, alpha, epilogue, ones_col)."""
     q = _lib.GemmProblem.from_buffer_copy(pr_partial)

@@ -815,7 +815,10 @@ class DLRMTrainer:
                 else:
                     self._gemm(pending + [w] + rq)
 
-        def bottom_bwd(s1=None):
+        def bottom_bwd(s1=None, hold_last=False):
+            """hold_last: the last launch's problems go to st["bot_last"] instead of being
+            launched (several GPUs: it then carries the embedding update's first pass once
+            the reverse all-to-all has landed)."""
             sched = self.bot_sched
             if sched == "auto":
                 sched = "full" if Bl <= 128 else "partial"
@@ -824,25 +827,30 @@ class DLRMTrainer:
             rq = st.pop("rq")
             g = bufs["gx"]  # dLoss/d(pre-ReLU bottom output), from the interaction backward
             bg = [bufs["gb"][0], bufs["gb"][1]]
+            launches = []
             for li in range(self.n_bot - 1, -1, -1):
                 L = self.bot[li]
                 inp = bufs["bot_act"][li - 1] if li > 0 else batch.X
                 w, r = self._wg(L, g, inp, fused_opt, lr, ("bot", li), last=li == 0)
                 if li > 0 and r is not None and self.group_wgrad:
-                    self._gemm([self._dgrad(L, g, inp, bg[li % 2]), w] + rq, side=c_bot)
+                    launches.append([self._dgrad(L, g, inp, bg[li % 2]), w] + rq)
                 elif li > 0 and r is None and not fused_opt:
                     # the wgrad writes the gradient bucket, not W: beside the dgrad
-                    self._gemm([self._dgrad(L, g, inp, bg[li % 2]), w] + rq, side=c_bot)
+                    launches.append([self._dgrad(L, g, inp, bg[li % 2]), w] + rq)
                 else:
                     if li > 0:
-                        self._gemm([self._dgrad(L, g, inp, bg[li % 2])] + rq, side=c_bot)
+                        launches.append([self._dgrad(L, g, inp, bg[li % 2])] + rq)
                         rq = []
-                    self._gemm([w] + rq, side=c_bot)
+                    launches.append([w] + rq)
                 rq = [r] if r is not None else []
                 if li > 0:
                     g = bg[li % 2]
             if rq:
-                self._gemm(rq, side=c_bot)
+                launches.append(rq)
+            if hold_last:
+                st["bot_last"] = launches.pop()
+            for probs in launches:
+                self._gemm(probs, side=c_bot)
 
         def emb_bwd(defer=False):  # embedding backward + fused update
             """defer=True: the update's two passes are returned as a role for the next two
@@ -899,7 +907,11 @@ class DLRMTrainer:
         def dense_update():
             with record_function("## Backward ##"), prof("dense_update"):
                 scale = 1.0 / self.world
-                if cfg.optimizer == "sgd":
+                if cfg.optimizer == "sgd" and st.pop("top_updated", False):
+                    # the top bucket's update rode on the embedding update's second pass
+                    nb = self.n_bot_params
+                    ops.sgd_update(self.params[:nb], self.grads[:nb], lr * scale)
+                elif cfg.optimizer == "sgd":
                     ops.sgd_update(self.params, self.grads, lr * scale)
                 else:
                     if scale != 1.0:
@@ -935,12 +947,64 @@ class DLRMTrainer:
 
         a2a_fwd = lambda: st.__setitem__("a2a", self._alltoall_fwd(bufs, Bl))  # noqa: E731
         a2a_bwd = lambda: st.__setitem__("a2a", self._alltoall_bwd(bufs, Bl))  # noqa: E731
+        # the embedding update's two passes as launch roles (as on one GPU): the first on
+        # the bottom backward's last launch, held back until the reverse all-to-all has
+        # landed; the second on a launch that also applies the top bucket's SGD update.
+        # The choice must not depend on the rank (T_local): every rank issues the same
+        # collectives in the same order (a rank without tables just carries no role)
+        roles_dist = self.tbe_role and profile is None and self.weights.dtype == torch.float32
+
+        def bottom_head():
+            bottom_bwd(hold_last=roles_dist)
+
+        def bottom_tail():  # after All2All_Wait: the update's passes ride on GEMM launches
+            role = emb_bwd(defer=True)
+            if role is not None:
+                self._roles = [(role, 1)]
+                st["emb_role"] = role
+            self._gemm(st.pop("bot_last"))
+            self._roles = []
+
+        def emb_pass2():
+            role = st.pop("emb_role", None)
+            if role is None:
+                return
+            jobs = []
+            if cfg.optimizer == "sgd":  # the top bucket was all-reduced (waited) already
+                nb = self.n_bot_params
+                jobs = [ops.sgd_job(self.params[nb:], self.grads[nb:], lr * (1.0 / self.world))]
+                st["top_updated"] = True
+            self._roles = [(role, 2)]
+            self._gemm(jobs)
+            self._roles = []
+
+        # RCCL: the all-reduces capture into hipGraphs, the all-to-alls do not (DESIGN.md §8:
+        # a captured all_to_all_single or send/recv crashes hipStreamEndCapture on this
+        # stack).  Each all-reduce is waited in the graph that issues it, so the step is FOUR
+        # graphs around the two eager all-to-alls: the top bucket overlaps the bottom
+        # backward and the reverse all-to-all, the bottom bucket the embedding update's
+        # second pass.  gloo (host-staged, synchronous) runs the same order eagerly.
+        if roles_dist:
+            return [
+                ("gpu", lookup),
+                ("a2a", a2a_fwd),
+                ("gpu", bottom_fwd),
+                ("a2a", wait("a2a")),  # All2All_Wait (extend_distributed.py:489)
+                ("gpu", top),
+                ("gpu", interaction_bwd),
+                ("a2a", a2a_bwd),
+                ("ar", ar("top")),
+                ("gpu", record_function("## Backward ##")(bottom_head)),
+                ("ar", wait("ar_top")),
+                ("a2a", wait("a2a")),
+                ("gpu", record_function("## Backward ##")(bottom_tail)),
+                ("ar", ar("bot")),
+                ("gpu", record_function("## Backward ##")(emb_pass2)),
+                ("ar", wait("ar_bot")),
+                ("gpu", dense_update),
+                ("host", done),
+            ]
         if getattr(self.comm, "capture_ar", False):
-            # RCCL: the all-reduces capture into hipGraphs, the all-to-alls do not (DESIGN.md
-            # §8: a captured all_to_all_single crashes hipStreamEndCapture on this stack).
-            # Each all-reduce is waited in the graph that issues it, so the step is FOUR
-            # graphs around the two eager all-to-alls: the top bucket overlaps the bottom
-            # backward and the reverse all-to-all, the bottom bucket the embedding update
             return [
                 ("gpu", lookup),
                 ("a2a", a2a_fwd),
