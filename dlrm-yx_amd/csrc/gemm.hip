@@ -41,6 +41,12 @@
 #include "common.hpp"
 #include "tbe_bwd_roles.hpp"
 
+// Timeline hook of the pipelined body (tools/gemm_lab.hip defines it to stamp the clock at
+// the prologue, every K-tile and the epilogue; empty in the library).
+#ifndef DLRM_GEMM_STAMP
+#define DLRM_GEMM_STAMP(slot)
+#endif
+
 namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
@@ -230,6 +236,15 @@ struct Stage {
     regs[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
   }
 
+  // The same load for a stage wholly inside the split (no k test): the lane's tile-0 offset
+  // (or a past-the-end one for a masked mn) in the VGPR, the stage's advance t * tile_step in
+  // the scalar offset - no per-load VALU.
+  __device__ __forceinline__ void fetch4s(int v, const Fetch& f, __amdgpu_buffer_rsrc_t rsrc,
+                                          int soff) {
+    const int off = f.off[v] >= 0 ? f.off[v] : 0x7ffffff0;
+    regs[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, soff, 0));
+  }
+
   // (!KC: a float4 is a 4-aligned mn run, which the bit-4 flip keeps contiguous)
   __device__ __forceinline__ void store_one(int v, float* __restrict__ lds, int tid) const {
     int mn, k;
@@ -307,6 +322,87 @@ __device__ __forceinline__ float apply_epilogue(const GemmParams& p, int64_t row
   }
   *cp = v;
   return v;
+}
+
+// The same epilogue for a compile-time kind, on values already loaded: old = the C element
+// (SGD / ACCUM), aux = the mask operand (DRELU), bias = bias[col] (BIAS / BIAS_RELU).  The
+// arithmetic is apply_epilogue's, so results are bitwise the same.
+template <int EPI>
+__device__ __forceinline__ float epi_value(float v, float old, float aux, float bias) {
+  if constexpr (EPI == DLRM_EPI_BIAS) return v + bias;
+  else if constexpr (EPI == DLRM_EPI_BIAS_RELU) return fmaxf(v + bias, 0.f);
+  else if constexpr (EPI == DLRM_EPI_RELU) return fmaxf(v, 0.f);
+  else if constexpr (EPI == DLRM_EPI_DRELU) return aux > 0.f ? v : 0.f;
+  else if constexpr (EPI == DLRM_EPI_SGD) return old - v;
+  else if constexpr (EPI == DLRM_EPI_ACCUM) return old + v;
+  else return v;
+}
+
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int off) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, 0);
+}
+constexpr int kOob = 0x7ffffff0;  // a byte offset past every descriptor (loads 0, stores dropped)
+
+// The tile's epilogue for one kind, with no per-element branches and every operand load in
+// flight at once: byte offsets from buffer descriptors over exactly the addressed extents,
+// so rows past M land outside them (loads read 0, stores are dropped) and columns past N get
+// kOob.  n elements at (row[q], col[q]) with values v[q] (already alpha-scaled).
+template <int EPI, int NE>
+__device__ __forceinline__ void store_elems(const GemmParams& p, const int (&row)[NE],
+                                            const int (&col)[NE], const bool (&ok)[NE],
+                                            const float (&v)[NE]) {
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.C, (short)0, (int)(((p.M - 1) * p.ldc + p.ldc) * 4), 0x00020000);
+  int off[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q)
+    off[q] = ok[q] && row[q] < p.M ? (int)(((int64_t)row[q] * p.ldc + col[q]) * 4) : kOob;
+  float old[NE], aux[NE], bias[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) old[q] = aux[q] = bias[q] = 0.f;
+  if constexpr (EPI == DLRM_EPI_SGD || EPI == DLRM_EPI_ACCUM) {
+#pragma unroll
+    for (int q = 0; q < NE; ++q) old[q] = buf_ld(rc, off[q]);
+  }
+  if constexpr (EPI == DLRM_EPI_DRELU) {
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.aux, (short)0, (int)(((p.M - 1) * p.ldaux + p.ldaux) * 4), 0x00020000);
+#pragma unroll
+    for (int q = 0; q < NE; ++q)
+      aux[q] = buf_ld(ra, ok[q] && row[q] < p.M ? (int)(((int64_t)row[q] * p.ldaux + col[q]) * 4)
+                                                : kOob);
+  }
+  if constexpr (EPI == DLRM_EPI_BIAS || EPI == DLRM_EPI_BIAS_RELU) {
+#pragma unroll
+    for (int q = 0; q < NE; ++q) bias[q] = ok[q] ? p.bias[col[q]] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < NE; ++q) buf_st(epi_value<EPI>(v[q], old[q], aux[q], bias[q]), rc, off[q]);
+}
+
+// Offsets of C (and aux) fit the 32-bit buffer offsets with a tile of slack.
+__device__ __forceinline__ bool epi_fits(const GemmParams& p) {
+  const int64_t lim = 0x7ff00000LL;
+  return (p.M + 256) * p.ldc * 4 < lim &&
+         (p.epi != DLRM_EPI_DRELU || (p.M + 256) * p.ldaux * 4 < lim);
+}
+
+template <int NE>
+__device__ __forceinline__ void store_elems_any(const GemmParams& p, const int (&row)[NE],
+                                                const int (&col)[NE], const bool (&ok)[NE],
+                                                const float (&v)[NE]) {
+  switch (p.epi) {
+    case DLRM_EPI_BIAS: return store_elems<DLRM_EPI_BIAS>(p, row, col, ok, v);
+    case DLRM_EPI_BIAS_RELU: return store_elems<DLRM_EPI_BIAS_RELU>(p, row, col, ok, v);
+    case DLRM_EPI_RELU: return store_elems<DLRM_EPI_RELU>(p, row, col, ok, v);
+    case DLRM_EPI_DRELU: return store_elems<DLRM_EPI_DRELU>(p, row, col, ok, v);
+    case DLRM_EPI_SGD: return store_elems<DLRM_EPI_SGD>(p, row, col, ok, v);
+    case DLRM_EPI_ACCUM: return store_elems<DLRM_EPI_ACCUM>(p, row, col, ok, v);
+    default: return store_elems<DLRM_EPI_STORE>(p, row, col, ok, v);
+  }
 }
 
 
@@ -423,6 +519,33 @@ __device__ __forceinline__ void finish_tile(const GemmParams& p, const f32x4 (&a
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[(i * FN + j) * 4 + r] = acc[i][j][r];
+  if (p.mode == DLRM_GEMM_PARTIAL && p.M * p.N * 4 < 0x7ff00000LL) {
+    // raw partial sums for a REDUCE job of a later launch (the kernel boundary publishes),
+    // as buffer stores from one descriptor per slab: no per-element branch or 64-bit address
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.part + (int64_t)split * p.M * p.N), (short)0, (int)(p.M * p.N * 4), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = (int)(n0 + wn0 + j * 16 + l16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = (int)(m0 + wm0 + i * 16 + 4 * kq + r);
+          buf_st(v[(i * FN + j) * 4 + r], rp,
+                 row < p.M && col < p.N ? (int)(((int64_t)row * p.N + col) * 4) : kOob);
+        }
+      }
+    if (rs_owner) {
+      float* rslab = p.part + (int64_t)p.splits * p.M * p.N + (int64_t)split * p.M;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int64_t row = m0 + wm0 + i * 16 + l16;
+        if (row < p.M) rslab[row] = rs[i];
+      }
+    }
+    return;
+  }
   if (p.mode == DLRM_GEMM_PARTIAL) {
     // raw partial sums for a REDUCE job of a later launch (the kernel boundary publishes)
     float* slab = p.part + (int64_t)split * p.M * p.N;
@@ -449,6 +572,38 @@ __device__ __forceinline__ void finish_tile(const GemmParams& p, const f32x4 (&a
   }
   if (!splitk_reduce<BM, BN, NV, FM>(p, tile, split, v, rs, wm0 + l16, 16, rs_owner, smem))
     return;
+  if (epi_fits(p)) {  // batched: every operand load in flight at once, no per-element branch
+    int row[NV], col[NV];
+    bool ok[NV];
+    float w[NV];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = (i * FN + j) * 4 + r;
+          row[q] = (int)(m0 + wm0 + i * 16 + 4 * kq + r);
+          col[q] = (int)(n0 + wn0 + j * 16 + l16);
+          ok[q] = col[q] < p.N;
+          w[q] = __fmul_rn(p.alpha, v[q]);  // rounded alone, as apply_epilogue sees it
+        }
+    store_elems_any<NV>(p, row, col, ok, w);
+    if constexpr (RS) {
+      int rrow[FM], rcol[FM];
+      bool rok[FM];
+      float rw[FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        rrow[i] = (int)(m0 + wm0 + i * 16 + l16);
+        rcol[i] = (int)p.ones_col;
+        rok[i] = rs_owner;
+        rw[i] = __fmul_rn(p.alpha, rs[i]);
+      }
+      store_elems_any<FM>(p, rrow, rcol, rok, rw);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -541,6 +696,17 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
     else
       sb.fetch4(c - SA::NV, fb, rb, b_step, t, kb32 + t * BKT, kend32);
   };
+  // fast: stage t lies wholly inside the split (uniform; see Stage::fetch4s)
+  auto fetch_any = [&](int c, int t, auto fast) {
+    if constexpr (decltype(fast)::value) {
+      if (c < SA::NV)
+        sa.fetch4s(c, fa, ra, t * a_step);
+      else
+        sb.fetch4s(c - SA::NV, fb, rb, t * b_step);
+    } else {
+      fetch_one(c, t);
+    }
+  };
   auto put_one = [&](int c, float* buf) {
     if (c < SA::NV)
       sa.store_one(c, buf, tid);
@@ -570,21 +736,36 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   float a[FM][KL], b[FN][KL];
   // Prologue: stage 0 -> LDS buffer 0, stage 1 staged in registers, sub-tile 0 fragments
   // read.  Every fetch is unconditional: stages past nk load zeros (never used).
+  DLRM_GEMM_STAMP(0);
+  {
+    // stage 1's loads are issued into a second register set before stage 0 is waited for,
+    // so the two cold-cache round trips of the prologue overlap; stage 1 then moves to the
+    // set the loop stages from
+    SA sa1;
+    SB sb1;
 #pragma unroll
-  for (int c = 0; c < NS; ++c) fetch_one(c, 0);
+    for (int c = 0; c < NS; ++c) fetch_one(c, 0);
 #pragma unroll
-  for (int c = 0; c < NS; ++c) put_one(c, smem);
+    for (int c = 0; c < SA::NV; ++c) sa1.fetch4(c, fa, ra, a_step, 1, kb32 + BKT, kend32);
 #pragma unroll
-  for (int c = 0; c < NS; ++c) fetch_one(c, 1);
+    for (int c = 0; c < SB::NV; ++c) sb1.fetch4(c, fb, rb, b_step, 1, kb32 + BKT, kend32);
+#pragma unroll
+    for (int c = 0; c < NS; ++c) put_one(c, smem);
+#pragma unroll
+    for (int c = 0; c < SA::NV; ++c) sa.regs[c] = sa1.regs[c];
+#pragma unroll
+    for (int c = 0; c < SB::NV; ++c) sb.regs[c] = sb1.regs[c];
+  }
   __syncthreads();
   read_frags(smem, 0, a, b);
+  DLRM_GEMM_STAMP(1);
 
   // Sub-tile u of stage kt: MFMAs on (ca, cb) with the staging of stage kt+1 / fetch of kt+2
   // interleaved (staged float4 g = u*KL + step); a non-final sub-tile first issues the reads
   // of sub-tile u+1 into (na, nb) from the same buffer; the final one ends with the barrier
   // and sub-tile 0 of stage kt+1 read under its last k-step.
   auto subtile = [&](int kt, int u, float (&ca)[FM][KL], float (&cb)[FN][KL],
-                     float (&na)[FM][KL], float (&nb)[FN][KL]) {
+                     float (&na)[FM][KL], float (&nb)[FN][KL], auto fast) {
     const float* cur = smem + (kt & 1) * (SA::SIZE + SB::SIZE);
     float* nbuf = smem + ((kt + 1) & 1) * (SA::SIZE + SB::SIZE);
     const bool last = u == U - 1;
@@ -594,8 +775,8 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
       mfma_step(ca, cb, s);
       const int g = u * KL + s;
       if (g < NS) {
-        put_one(g, nbuf);      // stage t+1 (staged last stage) -> LDS
-        fetch_one(g, kt + 2);  // refill the register with stage t+2
+        put_one(g, nbuf);            // stage t+1 (staged last stage) -> LDS
+        fetch_any(g, kt + 2, fast);  // refill the register with stage t+2
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the interleave: no hoisting across steps
     }
@@ -604,7 +785,7 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
       const int g = u * KL + KL - 1;
       if (g < NS) {
         put_one(g, nbuf);
-        fetch_one(g, kt + 2);
+        fetch_any(g, kt + 2, fast);
       }
       __builtin_amdgcn_sched_barrier(0);
     } else {
@@ -616,17 +797,29 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   };
   float a1[FM][KL], b1[FN][KL];
   if constexpr (U == 1) {  // fragment sets ping-pong across stages: unrolled by two
+    // the fetches of sub-tile kt are stage kt + 2's: wholly inside the split while
+    // kbeg + (kt + 3) * BKT <= kend (then no per-load k test)
+    const std::true_type fast{};
+    const std::false_type slow{};
     for (int kt = 0; kt < nk; kt += 2) {
-      subtile(kt, 0, a, b, a1, b1);
+      if (kb32 + (kt + 3) * BKT <= kend32)
+        subtile(kt, 0, a, b, a1, b1, fast);
+      else
+        subtile(kt, 0, a, b, a1, b1, slow);
+      DLRM_GEMM_STAMP(2 + kt);
       if (kt + 1 >= nk) break;
-      subtile(kt + 1, 0, a1, b1, a, b);
+      if (kb32 + (kt + 4) * BKT <= kend32)
+        subtile(kt + 1, 0, a1, b1, a, b, fast);
+      else
+        subtile(kt + 1, 0, a1, b1, a, b, slow);
+      DLRM_GEMM_STAMP(3 + kt);
     }
   } else {  // an even number of sub-tiles per stage: every stage starts on (a, b)
     for (int kt = 0; kt < nk; ++kt) {
 #pragma unroll
       for (int u = 0; u < U; u += 2) {
-        subtile(kt, u, a, b, a1, b1);
-        subtile(kt, u + 1, a1, b1, a, b);
+        subtile(kt, u, a, b, a1, b1, std::false_type{});
+        subtile(kt, u + 1, a1, b1, a, b, std::false_type{});
       }
     }
   }
@@ -638,7 +831,9 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
     rs[i] += __shfl_xor(rs[i], 16, 64);
     rs[i] += __shfl_xor(rs[i], 32, 64);
   }
+  DLRM_GEMM_STAMP(-2);
   finish_tile<BM, BN, WGM, WGN, RS>(p, acc, rs, tile, split, tn, m0, n0, smem);
+  DLRM_GEMM_STAMP(-1);
 }
 
 // REDUCE job: C = epi(alpha * sum_s part[s]) in split order (the same additions as the
@@ -668,6 +863,21 @@ __device__ __forceinline__ void reduce_body(const GemmParams& p, int lb) {
         }
     }
     const int64_t e = 4 * i, row = e / p.N, col = e - row * p.N;
+    if (p.epi == DLRM_EPI_SGD || p.epi == DLRM_EPI_ACCUM) {
+      // the four old values loaded together (the generic path waits for each in turn)
+      float* cp = p.C + row * p.ldc + col;
+      const float o0 = cp[0], o1 = cp[1], o2 = cp[2], o3 = cp[3];
+      const bool sgd = p.epi == DLRM_EPI_SGD;
+      // alpha * acc rounded on its own (no contraction into the add): apply_epilogue's
+      // arithmetic, bitwise
+      const float v0 = __fmul_rn(p.alpha, acc.x), v1 = __fmul_rn(p.alpha, acc.y);
+      const float v2 = __fmul_rn(p.alpha, acc.z), v3 = __fmul_rn(p.alpha, acc.w);
+      cp[0] = sgd ? o0 - v0 : o0 + v0;
+      cp[1] = sgd ? o1 - v1 : o1 + v1;
+      cp[2] = sgd ? o2 - v2 : o2 + v2;
+      cp[3] = sgd ? o3 - v3 : o3 + v3;
+      return;
+    }
     apply_epilogue(p, row, col, p.alpha * acc.x);
     apply_epilogue(p, row, col + 1, p.alpha * acc.y);
     apply_epilogue(p, row, col + 2, p.alpha * acc.z);

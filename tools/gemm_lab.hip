@@ -6,6 +6,28 @@
 // bitwise the library's at the same split (the MFMA order does not depend on the tile or U).
 // (Round 5's candidate bodies - fragment groups, LDS-DMA rings - measured slower and left
 // with their commit, e02bb7a.)
+#ifdef LAB_TRACE
+// Timeline build (tools/gemm_trace.py): thread 0 of every workgroup stamps the shader clock
+// (s_memtime) at the body's hooks into g_stamps[blockIdx.x][slot]; slot 0 = start, 1 = after
+// the prologue, 2 + t = after K-tile t (t < 66), 68 = before the epilogue, 69 = end; 70 / 71 =
+// s_memrealtime (100 MHz, chip-wide) at start / end.
+#include <hip/hip_runtime.h>
+__device__ long long* g_stamps;
+#define DLRM_GEMM_STAMP(slot)                                                          \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && g_stamps) {                                                \
+      const int s_ = (slot) < 0 ? 70 + (slot) : ((slot) < 68 ? (slot) : -1);           \
+      long long* r_ = g_stamps + (long long)blockIdx.x * 72;                           \
+      if (s_ >= 0) r_[s_] = (long long)__builtin_amdgcn_s_memtime();                   \
+      if ((slot) == 0) r_[70] = (long long)__builtin_amdgcn_s_memrealtime();           \
+      if ((slot) == -1) r_[71] = (long long)__builtin_amdgcn_s_memrealtime();          \
+    }                                                                                  \
+  } while (0)
+extern "C" int lab_set_stamps(void* p) {
+  long long* q = static_cast<long long*>(p);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &q, sizeof(q)) == hipSuccess ? 0 : -1;
+}
+#endif
 #include "../dlrm-yx_amd/csrc/gemm.hip"
 
 namespace {

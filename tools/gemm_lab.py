@@ -17,26 +17,30 @@ ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "_lab", "libgemm_lab.so")
 
 
-def build():
+TRACE_LIB = os.path.join(HERE, "_lab", "libgemm_trace.so")
+
+
+def build(trace=False):
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
            f"-I{ROOT}/include", f"-I{ROOT}/dlrm-yx_amd/csrc", "-fno-slp-vectorize", "-shared",
            os.path.join(HERE, "gemm_lab.hip"), os.path.join(ROOT, "dlrm-yx_amd/csrc/abi.cpp"),
-           "-o", LIB]
+           "-o", TRACE_LIB if trace else LIB] + (["-DLAB_TRACE"] if trace else [])
     subprocess.run(cmd, check=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
+    ap.add_argument("--build-trace", action="store_true")
     ap.add_argument("--cfgs", default="100,101,102,103,105,107,200,201,202,203,205,207,400,401")
     ap.add_argument("--splits", default="1,2,4")
     ap.add_argument("--wsplits", default="1,2,4,8")
     ap.add_argument("--shapes", default="fwd,dgrad,wgrad")
     ap.add_argument("--B", type=int, default=2048)
     args = ap.parse_args()
-    if args.build:
-        build()
+    if args.build or args.build_trace:
+        build(trace=args.build_trace)
         return
     import torch
     sys.path.insert(0, os.path.join(ROOT, "dlrm-yx_amd"))
