@@ -650,6 +650,11 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
   const int split = lb - tile * p.splits;
   const int tm = tile / p.tiles_n;
   const int tn = tile - tm * p.tiles_n;
+  if constexpr (RS) {
+    // only the first column of tiles owns the row sums (finish_tile): the others run the
+    // body without the per-k-step adds (one VALU per MFMA)
+    if (tn != 0) return pipe_body<BM, BN, WGM, WGN, A_KC, B_KC, false, U>(p, lb, smem);
+  }
   const int64_t m0 = (int64_t)tm * BM;
   const int64_t n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)split * p.kchunk;
