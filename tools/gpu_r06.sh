@@ -105,3 +105,19 @@ if [ "$STAGE" = emulab ]; then
     done
   done
 fi
+# bottom-MLP parts A/B at C3: bash tools/gpu_r06.sh partsab
+if [ "$STAGE" = partsab ]; then
+  for i in 1 2; do
+    for P in 0 2; do
+      timeout -k 10 300 python bench.py --no-cpu-baseline --no-kernel-timing --steps 300 --bottom-parts $P \
+        > "$OUT/parts$P_$i.json" 2> "$OUT/parts.err" || exit $?
+      python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print('parts $P', d['value'], d['ms_per_step'], d['ms_per_step_p10_p50_p90'])" "$OUT/parts$P_$i.json" | tee -a "$OUT/partsab.txt"
+    done
+  done
+fi
+# one-step kernel timelines: bash tools/gpu_r06.sh trace
+if [ "$STAGE" = trace ]; then
+  bash tools/step_trace.sh gpurun_out/${OUTNAME:-r06}/trace_c3 || exit $?
+  bash tools/step_trace.sh gpurun_out/${OUTNAME:-r06}/trace_b256 --batch 256 || exit $?
+  bash tools/step_trace.sh gpurun_out/${OUTNAME:-r06}/trace_kaggle --config kaggle || exit $?
+fi
