@@ -56,6 +56,7 @@ constexpr int kMaxSplit = 32;
 constexpr int kMaxGroup = 6;
 constexpr int64_t kTicketCap = 16384;  // int32 tickets in the fixed 64 KiB workspace head
 constexpr int kBK = 32;
+constexpr int kRasterRows = 8;  // tile rows per raster group (pipe_body)
 
 struct GemmParams {
   int64_t M, N, K;
@@ -648,8 +649,20 @@ __device__ __forceinline__ void pipe_body(const GemmParams& p, int lb, float* sm
 
   const int tile = lb / p.splits;
   const int split = lb - tile * p.splits;
-  const int tm = tile / p.tiles_n;
-  const int tn = tile - tm * p.tiles_n;
+  // Grouped raster: runs of kRasterRows tile rows are walked column by column, so the
+  // contiguous run of tiles an XCD receives (xcd_remap) is a 2-D block - a few hundred rows
+  // of each operand in its 4 MiB L2 instead of a band of A rows against ALL of B.  A
+  // bijection on the tiles (the tail group takes the rows left); the sums are unchanged.
+  int tm, tn;
+  {
+    constexpr int G = kRasterRows;
+    const int per_group = G * p.tiles_n;
+    const int grp = tile / per_group, first = grp * G;
+    const int gsz = p.tiles_m - first < G ? p.tiles_m - first : G;
+    const int pos = tile - grp * per_group;
+    tm = first + pos % gsz;
+    tn = pos / gsz;
+  }
   if constexpr (RS) {
     // only the first column of tiles owns the row sums (finish_tile): the others run the
     // body without the per-k-step adds (one VALU per MFMA)
