@@ -244,11 +244,11 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p,
 __global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ p,
                                                       const float* __restrict__ g,
                                                       float* __restrict__ ss, int64_t n,
-                                                      float clr, float eps) {
+                                                      float clr, float eps, float gs) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = i; j < n; j += stride) {
-    const float gj = g[j];
+    const float gj = g[j] * gs;  // (gs = 1: exact; else the rounding dlrm_scale_f32 gives)
     const float s = fmaf(gj, gj, ss[j]);
     ss[j] = s;
     p[j] = fmaf(-clr, gj / (sqrtf(s) + eps), p[j]);
@@ -421,8 +421,20 @@ extern "C" int dlrm_adagrad_update(float* param, const float* grad, float* state
   if (n == 0) return DLRM_OK;
   DLRM_ARG(param && grad && state_sum, "dlrm_adagrad_update: null pointer");
   hipLaunchKernelGGL(adagrad_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
-                     dlrm::as_stream(stream), param, grad, state_sum, n, clr, eps);
+                     dlrm::as_stream(stream), param, grad, state_sum, n, clr, eps, 1.0f);
   DLRM_LAUNCH_CHECK("dlrm_adagrad_update");
+  return DLRM_OK;
+}
+
+extern "C" int dlrm_adagrad_update_scaled(float* param, const float* grad, float* state_sum,
+                                          int64_t n, float grad_scale, float clr, float eps,
+                                          dlrm_stream_t stream) {
+  DLRM_ARG(n >= 0, "dlrm_adagrad_update_scaled: bad n");
+  if (n == 0) return DLRM_OK;
+  DLRM_ARG(param && grad && state_sum, "dlrm_adagrad_update_scaled: null pointer");
+  hipLaunchKernelGGL(adagrad_kernel, dim3(grid_stride_blocks(n)), dim3(256), 0,
+                     dlrm::as_stream(stream), param, grad, state_sum, n, clr, eps, grad_scale);
+  DLRM_LAUNCH_CHECK("dlrm_adagrad_update_scaled");
   return DLRM_OK;
 }
 

@@ -13,7 +13,7 @@ from ctypes import c_float, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DLRM_ABI_VERSION of include/dlrm_hip.h that these signatures mirror; load() refuses a
 # library built from any other header (tests/test_cpu_host.py checks header == this).
-ABI_VERSION = 8
+ABI_VERSION = 9
 LIB_PATH = os.environ.get("DLRM_HIP_LIB", os.path.join(_HERE, "libdlrm_hip.so"))
 
 
@@ -139,6 +139,7 @@ SIGNATURES = {
     "dlrm_outer_drelu": (c_int32, [c_int64, c_int64, P, P, P, c_int64, c_int32, P, c_int64, P]),
     "dlrm_sgd_update": (c_int32, [P, P, c_int64, c_float, P]),
     "dlrm_adagrad_update": (c_int32, [P, P, P, c_int64, c_float, c_float, P]),
+    "dlrm_adagrad_update_scaled": (c_int32, [P, P, P, c_int64, c_float, c_float, c_float, P]),
     "dlrm_scale_f32": (c_int32, [P, c_int64, c_float, P]),
     "dlrm_sigmoid_forward": (c_int32, [c_int64, P, P, P]),
     "dlrm_sigmoid_backward": (c_int32, [c_int64, P, P, P, P]),

@@ -831,7 +831,14 @@ def sgd_update(param: torch.Tensor, grad: torch.Tensor, lr: float) -> None:
 
 
 def adagrad_update(param: torch.Tensor, grad: torch.Tensor, state_sum: torch.Tensor, clr: float,
-                   eps: float) -> None:
+                   eps: float, grad_scale: float = 1.0) -> None:
+    """state_sum += g'^2; param -= clr * g' / (sqrt(state_sum) + eps) with g' = grad_scale * g
+    (grad itself is not modified)."""
+    if grad_scale != 1.0:
+        _lib.call("dlrm_adagrad_update_scaled", _p(param), _p(grad), _p(state_sum),
+                  param.numel(), float(grad_scale), float(clr), float(eps),
+                  _stream(param.device))
+        return
     _lib.call("dlrm_adagrad_update", _p(param), _p(grad), _p(state_sum), param.numel(),
               float(clr), float(eps), _stream(param.device))
 

@@ -913,11 +913,9 @@ class DLRMTrainer:
                     ops.sgd_update(self.params[:nb], self.grads[:nb], lr * scale)
                 elif cfg.optimizer == "sgd":
                     ops.sgd_update(self.params, self.grads, lr * scale)
-                else:
-                    if scale != 1.0:
-                        ops.scale_(self.grads, scale)
+                else:  # the 1/W folded into the update (one pass over the bucket)
                     ops.adagrad_update(self.params, self.grads, self.adagrad_sum, lr,
-                                       cfg.adagrad_eps)
+                                       cfg.adagrad_eps, grad_scale=scale)
 
         def done():
             self.step_count += 1

@@ -109,8 +109,10 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  *    (round 5).
  * 8: dlrm_mlp_chain_backward removed (the bottom MLP's data gradients as one row-block
  *    launch lost to the grouped GEMM schedules at every batch size,
- *    profiles/r04_bot_sched_ab.txt) (round 5). */
-#define DLRM_ABI_VERSION 8 /* the one source of truth: abi.cpp returns it, dlrm_hip/_lib.py
+ *    profiles/r04_bot_sched_ab.txt) (round 5).
+ * 9: dlrm_adagrad_update_scaled (the W-rank dense Adagrad step with the 1/W folded in)
+ *    (round 6). */
+#define DLRM_ABI_VERSION 9 /* the one source of truth: abi.cpp returns it, dlrm_hip/_lib.py
                              pins it (tests/test_cpu_host.py checks all of them agree) */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
@@ -648,6 +650,12 @@ int dlrm_sgd_update(float* param, const float* grad, int64_t n, float lr, dlrm_s
 /* state_sum += g^2; param -= clr * g / (sqrt(state_sum) + eps) */
 int dlrm_adagrad_update(float* param, const float* grad, float* state_sum, int64_t n, float clr,
                         float eps, dlrm_stream_t stream);
+/* The same with the gradient scaled first, g' = grad_scale * g (the several-GPU dense update:
+ * the 1/W of the averaged gradient folded in; bitwise dlrm_scale_f32 + dlrm_adagrad_update
+ * without the extra pass over the bucket; ABI v9).  Replaces the reference's DDP-averaged
+ * RWSAdagrad dense step (optim/rwsadagrad.py:56-122 on dlrm_s_pytorch.py:1626-1633 grads). */
+int dlrm_adagrad_update_scaled(float* param, const float* grad, float* state_sum, int64_t n,
+                               float grad_scale, float clr, float eps, dlrm_stream_t stream);
 int dlrm_scale_f32(float* x, int64_t n, float alpha, dlrm_stream_t stream);
 
 /* Elementwise activations (nn.Sigmoid / nn.ReLU forward & backward on n floats). */

@@ -586,6 +586,22 @@ def test_dense_optimizers(ops):
     assert ok, msg
 
 
+@pytest.mark.parametrize("scale", [0.125, 1.0 / 3.0])
+def test_adagrad_update_scaled_is_scale_then_update_bitwise(ops, scale):
+    """dlrm_adagrad_update_scaled (ABI v9, the W-rank dense step with 1/W folded in) gives
+    bitwise the two-pass form dlrm_scale_f32 + dlrm_adagrad_update, and leaves grad alone."""
+    torch.manual_seed(6)
+    p, g, s = torch.randn(4099), torch.randn(4099), torch.rand(4099)
+    pa, ga, sa = p.to(dev), g.to(dev), s.to(dev)
+    ops.scale_(ga, scale)
+    ops.adagrad_update(pa, ga, sa, 0.05, 1e-8)
+    pb, gb, sb = p.to(dev), g.to(dev), s.to(dev)
+    ops.adagrad_update(pb, gb, sb, 0.05, 1e-8, grad_scale=scale)
+    torch.cuda.synchronize()
+    assert torch.equal(pa, pb) and torch.equal(sa, sb)
+    assert torch.equal(gb.cpu(), g)
+
+
 def test_qr_split_and_combine(ops, golden):
     g = golden("qr.npz")
     q, r = ops.qr_split_indices(torch.tensor(g["split_idx"]).to(dev), 3)
