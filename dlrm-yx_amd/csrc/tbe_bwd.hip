@@ -246,6 +246,8 @@ struct PassView {
   const int32_t* pin;
   uint32_t* kout;
   int32_t* pout;
+  int shift;      // this pass's digit: (key >> shift) & mask
+  uint32_t mask;
 };
 
 template <int DB>
@@ -254,12 +256,19 @@ __device__ __forceinline__ PassView pass_view(const TiledPass& a, int64_t nrows)
   if (a.global) {
     v.first = a.first, v.last = a.last, v.kin = a.kin, v.pin = a.pin;
     v.kout = a.kout, v.pout = a.pout;
+    v.shift = a.shift, v.mask = (1u << DB) - 1;
     return v;
   }
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) <= nrows) ++bits;  // keys in [0, nrows]
   int passes = (bits + DB - 1) / DB;
   if (passes > a.npass) passes = a.npass;
+  // the table's bits split evenly over its passes (17 bits: 9 + 8, not 10 + 7): fewer
+  // digits in the first pass, so each tile's runs per digit - the scatter's store segments -
+  // are longer (a stable LSD sort by any digit split gives the same order)
+  const int width = (bits + passes - 1) / passes < DB ? (bits + passes - 1) / passes : DB;
+  v.shift = a.ps * width;
+  v.mask = (1u << width) - 1;
   v.skip = a.ps >= passes;
   v.first = a.ps == 0;
   v.last = a.ps == passes - 1;
@@ -342,7 +351,7 @@ __device__ __forceinline__ void hist_body(const IdxT* __restrict__ idx,
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < kTileItems; ++u)
-    if (ok[u]) atomicAdd(&cnt[(key[u] >> a.shift) & (NB - 1)], 1u);
+    if (ok[u]) atomicAdd(&cnt[(key[u] >> v.shift) & v.mask], 1u);
   __syncthreads();
   uint32_t* h = a.hist + ((int64_t)t * a.J + j) * NB;
   for (int d = threadIdx.x; d < NB; d += kTileThreads) h[d] = cnt[d];
@@ -635,7 +644,7 @@ __global__ __launch_bounds__(kScatThreads) void tbe_tiled_scatter_kernel(
   uint32_t rank[kScatItems], dig[kScatItems];
 #pragma unroll
   for (int u = 0; u < kScatItems; ++u) {
-    const uint32_t d = (key[u] >> a.shift) & (NB - 1);
+    const uint32_t d = (key[u] >> v.shift) & v.mask;
     uint64_t peers = __ballot(ok[u]);
 #pragma unroll
     for (int b = 0; b < DB; ++b) {
@@ -734,7 +743,7 @@ __global__ __launch_bounds__(kScatThreads) void tbe_tiled_scatter_kernel(
     const int i = u * kScatThreads + tid;
     if (i >= nt) continue;
     const uint32_t k = sm.key[i];
-    const uint32_t d = (k >> a.shift) & (NB - 1);
+    const uint32_t d = (k >> v.shift) & v.mask;
     const int64_t dst = s + h[d] + (a.wide ? sm.dbase[d] : 0u) + (i - sm.dstart[d]);
     if (v.last && !a.global)
       v.kout[dst] = k < (uint32_t)nrows ? (uint32_t)(rb + k) : a.sentinel;
