@@ -130,7 +130,10 @@ __global__ __launch_bounds__(kSegThreads) void tbe_bwd_segsort_kernel(
 // the bandwidth-bound gather instead of as a separate launch in the backward.  Blocks
 // [0, T] sort (started first), the rest gather.  512 threads per workgroup.
 // With mlp_blocks > 0 a third role, the bottom MLP forward (mlp_rows.hpp), takes blocks
-// [T+1, T+1+mlp_blocks): it reads only X and the bottom weights, independent of the rest.
+// [nsort, nsort+mlp_blocks): it reads only X and the bottom weights, independent of the rest.
+// nsort = T + 1 with the sort, 0 without it (tables too large for the per-table LDS sort,
+// e.g. C1's L = 100: the lookup and the bottom MLP still share one launch - the gather is
+// HBM-bound, the MLP rides on MFMA and LDS).
 constexpr int kPreThreads = kSegThreads;
 static_assert(kPreThreads == kMlpWaves * 64, "one workgroup size for every role");
 union PresortLds {
@@ -143,20 +146,20 @@ __global__ __launch_bounds__(kPreThreads) void tbe_fwd_presort_kernel(
     const IdxT* __restrict__ idx, const OffT* __restrict__ off, const float* __restrict__ psw,
     float* __restrict__ out, int64_t out_bs, int32_t* __restrict__ err, int64_t N,
     uint32_t sentinel, uint32_t* __restrict__ keys_out, int32_t* __restrict__ pos_out,
-    int32_t* __restrict__ bag_of, const MlpChain mc, int mlp_blocks) {
+    int32_t* __restrict__ bag_of, const MlpChain mc, int mlp_blocks, int nsort) {
   __shared__ __attribute__((aligned(16))) PresortLds sm;
   const int b = blockIdx.x;
-  if (b <= T) {
+  if (b < nsort) {
     segsort_body<kSegThreads, kSegItems, false, IdxT, OffT>(idx, off, row_base, T, B, N,
                                                             sentinel, keys_out, pos_out, bag_of,
                                                             err, b, sm.sort);
     return;
   }
-  if (b < T + 1 + mlp_blocks) {
-    mlp_rows_body(mc, b - (T + 1), sm.mlp);
+  if (b < nsort + mlp_blocks) {
+    mlp_rows_body(mc, b - nsort, sm.mlp);
     return;
   }
-  const int g0 = T + 1 + mlp_blocks;
+  const int g0 = nsort + mlp_blocks;
   tbe_fwd_body<LPB, VW, MAXV, IdxT, OffT>(W, D, row_base, T, B, idx, off, psw, out, out_bs, err,
                                           (int64_t)b - g0, (int64_t)gridDim.x - g0);
 }
@@ -1204,12 +1207,17 @@ template <typename IdxT, typename OffT>
 int launch_fwd_presort(const float* W, int64_t D, const int64_t* row_base, int T, int B,
                        const void* idx, const void* off, const float* psw, float* out,
                        int64_t out_bs, int64_t N, int64_t total_rows, void* ws, size_t ws_bytes,
-                       int32_t* err, const MlpChain& mc, int mlp_blocks, hipStream_t st) {
+                       int32_t* err, const MlpChain& mc, int mlp_blocks, bool sort,
+                       hipStream_t st) {
   const char* name = "dlrm_tbe_forward_presort";
-  const int end_bit = bit_width_u64((uint64_t)total_rows);
-  BwdWs<uint32_t> w = carve_bwd_ws<uint32_t>(ws, N, D, end_bit);
-  DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu", name,
-               ws_bytes, w.total);
+  BwdWs<uint32_t> w{};
+  if (sort) {
+    const int end_bit = bit_width_u64((uint64_t)total_rows);
+    w = carve_bwd_ws<uint32_t>(ws, N, D, end_bit);
+    DLRM_REQUIRE(ws_bytes >= w.total, DLRM_ERR_WORKSPACE, "%s: workspace %zu < required %zu",
+                 name, ws_bytes, w.total);
+  }
+  const int nsort = sort ? T + 1 : 0;
   const bool vec4 = (D % 4 == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) &&
                     ((reinterpret_cast<uintptr_t>(out) & 15) == 0) && (out_bs % 4 == 0);
   const int64_t nchunks = vec4 ? D / 4 : D;
@@ -1223,7 +1231,7 @@ int launch_fwd_presort(const float* W, int64_t D, const int64_t* row_base, int T
   if (gblocks > 8192) gblocks = 8192;
   if (gblocks < 1) gblocks = 1;
   if (!out) gblocks = 0;  // the lookup is fused into its consumer (interaction gather)
-  const dim3 grid((unsigned)(T + 1 + mlp_blocks + gblocks)), block(kPreThreads);
+  const dim3 grid((unsigned)(nsort + mlp_blocks + gblocks)), block(kPreThreads);
   const IdxT* ip = static_cast<const IdxT*>(idx);
   const OffT* op = static_cast<const OffT*>(off);
   const uint32_t sentinel = (uint32_t)total_rows;
@@ -1231,7 +1239,7 @@ int launch_fwd_presort(const float* W, int64_t D, const int64_t* row_base, int T
   hipLaunchKernelGGL((tbe_fwd_presort_kernel<LPB, VW, MV, IdxT, OffT>), grid, block, 0, st, W, D, \
                      row_base, T, B, ip, op, psw, out, out_bs, err, N, sentinel,                  \
                      reinterpret_cast<uint32_t*>(w.keys_out), w.pos_out, w.bag_of, mc,       \
-                     mlp_blocks)
+                     mlp_blocks, nsort)
 #define PRE_LPB(VW)                        \
   switch (lpb) {                           \
     case 1: PRE(1, VW, 1); break;          \
@@ -1275,8 +1283,14 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
     DLRM_ARG(mlp_chain_prepare(bottom, mc), "%s: unsupported bottom MLP chain", name);
     mlp_blocks = (int)mlp_chain_blocks(mc);
   }
-  if (!presort_applies((uint64_t)total_rows < 0xFFFFFFFFull ? 4 : 8, max_lookups_per_table,
-                       num_lookups) || num_lookups == 0 || T * (int64_t)B >= INT32_MAX) {
+  const bool sort = presort_applies((uint64_t)total_rows < 0xFFFFFFFFull ? 4 : 8,
+                                    max_lookups_per_table, num_lookups) &&
+                    num_lookups > 0 && T * (int64_t)B < INT32_MAX;
+  // no per-table sort (the backward sorts itself) but a bottom MLP to run: one launch of
+  // the lookup and the MLP roles (D <= 512 keeps the gather within its 8 chunks per lane)
+  const bool pair = !sort && bottom && out && num_lookups > 0 && T * (int64_t)B < INT32_MAX &&
+                    D <= 512;
+  if (!sort && !pair) {
     DLRM_REQUIRE(out, DLRM_ERR_UNSUPPORTED,
                  "%s: out = NULL needs the per-table sort (32-bit keys, bounded tables)", name);
     const int rc = dlrm_tbe_forward(weights, D, row_base, T, B, indices, index_bits, offsets,
@@ -1290,13 +1304,13 @@ extern "C" int dlrm_tbe_forward_presort(const float* weights, int64_t D, const i
   DLRM_ARG(index_bits == 32 || index_bits == 64, "%s: index_bits must be 32|64", name);
   DLRM_ARG(offset_bits == 32 || offset_bits == 64, "%s: offset_bits must be 32|64", name);
   DLRM_ARG(out_batch_stride >= (int64_t)T * D, "%s: out_batch_stride < T*D", name);
-  DLRM_ARG(workspace, "%s: null workspace", name);
+  DLRM_ARG(workspace || !sort, "%s: null workspace", name);
   hipStream_t st = dlrm::as_stream(stream);
 #define PS(I, O)                                                                           \
   return launch_fwd_presort<I, O>(weights, D, row_base, T, B, indices, offsets,            \
                                   per_sample_weights, out, out_batch_stride, num_lookups,  \
                                   total_rows, workspace, workspace_bytes, error_flag, mc,  \
-                                  mlp_blocks, st)
+                                  mlp_blocks, sort, st)
   if (index_bits == 32 && offset_bits == 32) PS(int32_t, int32_t);
   if (index_bits == 32) PS(int32_t, int64_t);
   if (offset_bits == 32) PS(int64_t, int32_t);

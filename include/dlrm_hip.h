@@ -220,7 +220,8 @@ int dlrm_mlp_chain_forward(const dlrm_mlp_chain* chain, dlrm_stream_t stream);
  * sorts as usual.
  * bottom != NULL: the bottom MLP forward (an independent input of the same step) runs as
  * a third role of the same launch (dlrm_mlp_chain semantics; it must be supported); when
- * the presort does not apply it runs as its own launch.
+ * the presort does not apply it still shares the lookup launch (round 6; D <= 512, out != NULL;
+ * otherwise its own launch after the lookup).
  * out == NULL (round 3): no lookup role - its consumer gathers the rows itself
  * (dlrm_interact_dot_forward_gather); needs the per-table sort to apply (else UNSUPPORTED).
  */

@@ -1097,6 +1097,56 @@ def test_tbe_forward_presort_with_bottom_chain(ops):
     assert torch.equal(Wa, Wb)
 
 
+@pytest.mark.parametrize("D,L,bound,idx_dtype,weighted", [
+    (64, 3, False, torch.int32, False),   # no bound: no sort, lookup + MLP in one launch
+    (64, 3, True, torch.int64, True),     # bound B * L above the LDS sort's 4096 per table
+    (40, 5, False, torch.int32, False),   # D % 4 != 0: the scalar gather lanes
+    (600, 9, True, torch.int32, False),   # D > 512: lookup, then the chain's own launch
+])
+def test_tbe_forward_presort_unsorted_with_bottom_chain(ops, D, L, bound, idx_dtype, weighted):
+    """Tables too large for the per-table sort (C1's L = 100 shape): the lookup and the
+    bottom MLP still share one launch (no sort role).  E and the error flag equal the plain
+    forward's bitwise (an out-of-range index included), the chain's activations the
+    standalone chain's bitwise, and the backward (which then sorts itself) is unchanged."""
+    torch.manual_seed(5)
+    rows, B = [3, 5000, 700, 90000], 2048 if D <= 64 else 512
+    T = len(rows)
+    mx = B * L if bound else 0
+    lo = [torch.arange(B) * L for _ in rows]
+    li = [torch.randint(0, n, (B * L,)) for n in rows]
+    li[1][11] = 10 ** 6
+    off, idx = O.batched_csr(lo, li)
+    idx, off = idx.to(idx_dtype).to(dev), off.to(dev)
+    psw = torch.rand(idx.numel(), device=dev) if weighted else None
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    W = torch.randn(sum(rows), D, device=dev)
+    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), sum(rows), D),
+                     dtype=torch.uint8, device=dev)
+    X, layers = _mlp_setup(B, [13, 512, 256, 64])
+    X2, layers2 = X.clone(), [(w, y.clone(), k) for w, y, k in layers]
+    f0 = torch.zeros(1, dtype=torch.int32, device=dev)
+    f1 = torch.zeros(1, dtype=torch.int32, device=dev)
+    E0 = ops.tbe_forward(W, row_base, T, B, idx, off, per_sample_weights=psw, error_flag=f0)
+    for _ in range(2):  # twice: the split chain's tickets are reusable
+        E1 = ops.tbe_forward_presort(W, row_base, T, B, idx, off, ws, mx,
+                                     per_sample_weights=psw, error_flag=f1,
+                                     bottom=ops.mlp_chain(X, layers))
+    ops.mlp_chain_forward(ops.mlp_chain(X2, layers2))
+    torch.cuda.synchronize()
+    assert torch.equal(E0, E1)
+    assert int(f0.item()) == int(f1.item()) != 0
+    for (_, y1, _), (_, y2, _) in zip(layers, layers2):
+        assert torch.equal(y1, y2)
+    if weighted:
+        return
+    G = torch.randn(B, T, D, device=dev)
+    Wa, Wb = W.clone(), W.clone()
+    ops.tbe_backward("sgd", Wa, row_base, T, B, idx, off, G, lr=0.1, workspace=ws,
+                     max_lookups_per_table=mx, presorted=True)
+    ops.tbe_backward("sgd", Wb, row_base, T, B, idx, off, G, lr=0.1, max_lookups_per_table=mx)
+    assert torch.equal(Wa, Wb)
+
+
 def _tbe_bwd_case(rows, B, L, D, seed, invalid=False, idx_dtype=torch.int32):
     torch.manual_seed(seed)
     T = len(rows)
