@@ -682,6 +682,8 @@ def main():
                     "wgrad reduces its K split inside its own launch (no trailing REDUCE launch)")
     ap.add_argument("--head-role", type=int, default=-1, help="A/B: 1 = the head's finalize "
                     "pass rides on the top-MLP backward's first launch, 0 = own launch")
+    ap.add_argument("--early-sort", type=int, default=-1, help="A/B: 1 = the backward's "
+                    "sort on the side stream beside the forward (tables past the LDS sort)")
     ap.add_argument("--bottom-parts", type=int, default=-1, help="A/B: workgroups per 16-row "
                     "block of the fused bottom MLP (1, 2, 4; 0 = auto)")
     ap.add_argument("--tbe-role-at", default="", help="A/B: bottom-backward launches "
@@ -771,6 +773,8 @@ def main():
         tr.full_last_wgrad = bool(args.full_last_wgrad)
     if args.head_role >= 0:
         tr.head_role = bool(args.head_role)
+    if args.early_sort >= 0:
+        tr.early_sort = bool(args.early_sort)
     if args.bottom_parts >= 0:
         tr.bottom_parts = args.bottom_parts
     if args.tbe_role_at:
@@ -972,7 +976,8 @@ def main():
                        "graphs_per_step": tr.graphs_per_step if use_graph else None,
                        "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
                        "tbe_role_at": list(tr.tbe_role_at), "bottom_parts": tr.bottom_parts,
-                       "head_role": tr.head_role, "full_last_wgrad": tr.full_last_wgrad,
+                       "head_role": tr.head_role, "early_sort": tr.early_sort,
+                       "full_last_wgrad": tr.full_last_wgrad,
                        "tune": args.tune or None},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,
             "comm": comm,

@@ -896,7 +896,7 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
                const void* idx, const void* off, int64_t N, int64_t total_rows, const float* psw,
                const float* gout, int64_t gbs, float lr, float eps, void* ws, size_t ws_bytes,
                int64_t max_seg, int32_t* err, int presorted, LaunchRole* defer, hipStream_t st,
-               const char* name) {
+               const char* name, bool sort_only = false) {
   if (defer) {  // until proven fusable: nothing deferred
     *defer = LaunchRole{};
     defer->magic = kRoleMagic;
@@ -925,8 +925,13 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
   // the tiled and global sorts carry each lookup's bag (not its position) when no
   // per-sample weights need the position: the block kernel then reads bags in sorted order
   const int32_t* bags = (!per_table && psw == nullptr) ? w.bag_of : nullptr;
-  if (per_table && presorted) {
-    // this batch's per-table sort already ran inside dlrm_tbe_forward_presort
+  if (presorted == DLRM_PRESORTED_ANY || (per_table && presorted)) {
+    // this batch's sort already ran: inside dlrm_tbe_forward_presort (per-table), or in
+    // dlrm_tbe_backward_sort (any variant; the device-wide one ends in x or y by its parity)
+    if (!per_table && !tiled && ((end_bit + tdb - 1) / tdb) % 2 == 0) {
+      std::swap(w.keys_in, w.keys_out);
+      std::swap(w.pos_in, w.pos_out);
+    }
   } else if (per_table) {
     hipLaunchKernelGGL((tbe_bwd_segsort_kernel<IdxT, OffT>), dim3(T + 1), dim3(kSegThreads), 0,
                        st, static_cast<const IdxT*>(idx), static_cast<const OffT*>(off), row_base,
@@ -977,6 +982,8 @@ int launch_bwd(int mode, float* W, float* mom, int64_t D, const int64_t* row_bas
       std::swap(w.pos_in, w.pos_out);
     }
   }
+
+  if (sort_only) return DLRM_OK;
 
   const bool vec4 = (D % 4 == 0) &&
                     ((reinterpret_cast<uintptr_t>(W) & (mode == MODE_SGD_F16 ? 7 : 15)) == 0) &&
@@ -1074,8 +1081,12 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
                  int B, const void* idx, int ib, const void* off, int ob, int64_t N,
                  int64_t total_rows, const float* psw, const float* gout, int64_t gbs, float lr,
                  float eps, void* ws, size_t ws_bytes, int64_t max_seg, int32_t* err,
-                 int presorted, LaunchRole* defer, dlrm_stream_t stream, const char* name) {
-  DLRM_ARG(W && row_base && gout && (N == 0 || (idx && off)), "%s: null pointer", name);
+                 int presorted, LaunchRole* defer, dlrm_stream_t stream, const char* name,
+                 bool sort_only = false) {
+  DLRM_ARG(((W && gout) || sort_only) && row_base && (N == 0 || (idx && off)),
+           "%s: null pointer", name);
+  DLRM_ARG(presorted >= 0 && presorted <= DLRM_PRESORTED_ANY, "%s: bad presorted %d", name,
+           presorted);
   DLRM_ARG(T > 0 && B > 0 && D > 0 && N >= 0 && total_rows > 0, "%s: bad sizes", name);
   DLRM_ARG(ib == 32 || ib == 64, "%s: index_bits must be 32 or 64", name);
   DLRM_ARG(ob == 32 || ob == 64, "%s: offset_bits must be 32 or 64", name);
@@ -1091,7 +1102,7 @@ int bwd_dispatch(int mode, float* W, float* mom, int64_t D, const int64_t* row_b
 #define BWD(K, I, O)                                                                     \
   return launch_bwd<K, I, O>(mode, W, mom, D, row_base, T, B, idx, off, N, total_rows, psw, \
                              gout, gbs, lr, eps, ws, ws_bytes, max_seg, err, presorted, defer, \
-                             st, name)
+                             st, name, sort_only)
   if (ib == 32 && ob == 32) BWD(uint32_t, int32_t, int32_t);
   if (ib == 32 && ob == 64) BWD(uint32_t, int32_t, int64_t);
   if (ib == 64 && ob == 32) BWD(uint32_t, int64_t, int32_t);
@@ -1174,6 +1185,21 @@ extern "C" int dlrm_tbe_backward_dense(float* grad_weights, int64_t D, const int
 }
 
 static_assert(sizeof(LaunchRole) <= sizeof(dlrm_launch_role), "dlrm_launch_role too small");
+
+extern "C" int dlrm_tbe_backward_sort(int64_t D, const int64_t* row_base, int32_t T, int32_t B,
+                                      const void* indices, int32_t index_bits,
+                                      const void* offsets, int32_t offset_bits,
+                                      int64_t num_lookups, int64_t total_rows,
+                                      const float* per_sample_weights,
+                                      int64_t max_lookups_per_table, void* workspace,
+                                      size_t workspace_bytes, int32_t* error_flag,
+                                      dlrm_stream_t stream) {
+  return bwd_dispatch(MODE_SGD, nullptr, nullptr, D, row_base, T, B, indices, index_bits,
+                      offsets, offset_bits, num_lookups, total_rows, per_sample_weights, nullptr,
+                      (int64_t)T * D, 0.f, 0.f, workspace, workspace_bytes,
+                      max_lookups_per_table, error_flag, 0, nullptr, stream,
+                      "dlrm_tbe_backward_sort", true);
+}
 
 extern "C" int dlrm_tbe_backward_defer(
     int32_t mode, float* weights, float* momentum, int64_t D, const int64_t* row_base,

@@ -13,7 +13,7 @@ from ctypes import c_float, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DLRM_ABI_VERSION of include/dlrm_hip.h that these signatures mirror; load() refuses a
 # library built from any other header (tests/test_cpu_host.py checks header == this).
-ABI_VERSION = 9
+ABI_VERSION = 10
 LIB_PATH = os.environ.get("DLRM_HIP_LIB", os.path.join(_HERE, "libdlrm_hip.so"))
 
 
@@ -66,6 +66,8 @@ SIGNATURES = {
     "dlrm_tbe_forward": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32, P, P,
                                    c_int64, P, P]),
     "dlrm_tbe_backward_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
+    "dlrm_tbe_backward_sort": (c_int32, [c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32,
+                                         c_int64, c_int64, P, c_int64, P, c_size_t, P, P]),
     "dlrm_tbe_backward_sgd": (c_int32, [P, c_int64, P, c_int32, c_int32, P, c_int32, P, c_int32,
                                         c_int64, c_int64, P, P, c_int64, c_float, c_int64, P,
                                         c_size_t, P, c_int32, P]),

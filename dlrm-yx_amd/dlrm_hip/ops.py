@@ -321,6 +321,25 @@ def tbe_backward_workspace_size(num_lookups: int, total_rows: int, D: int) -> in
     return _lib.query("dlrm_tbe_backward_workspace_size", num_lookups, total_rows, D)
 
 
+PRESORTED_ANY = 2  # DLRM_PRESORTED_ANY
+
+
+def tbe_backward_sort(weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
+                      indices: torch.Tensor, offsets: torch.Tensor, workspace: torch.Tensor,
+                      max_lookups_per_table: int = 0,
+                      per_sample_weights: Optional[torch.Tensor] = None,
+                      error_flag: Optional[torch.Tensor] = None) -> None:
+    """The backward's sort alone (dlrm_tbe_backward_sort): it depends only on the indices,
+    so it can run early (e.g. on a side stream beside the forward); follow with
+    tbe_backward(..., workspace, presorted=PRESORTED_ANY) of the same batch (same bound and
+    per_sample_weights nullness)."""
+    _check_cuda(weights, row_base, indices, offsets, workspace, per_sample_weights)
+    _lib.call("dlrm_tbe_backward_sort", weights.shape[1], _p(row_base), T, B, _p(indices),
+              _bits(indices), _p(offsets), _bits(offsets), indices.numel(), weights.shape[0],
+              _p(per_sample_weights), int(max_lookups_per_table), _p(workspace),
+              workspace.numel(), _p(error_flag), _stream(weights.device))
+
+
 def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: int, B: int,
                  indices: torch.Tensor, offsets: torch.Tensor, grad_out: torch.Tensor,
                  lr: float = 0.0, eps: float = 0.0, momentum: Optional[torch.Tensor] = None,
@@ -328,12 +347,14 @@ def tbe_backward(mode: str, weights: torch.Tensor, row_base: torch.Tensor, T: in
                  grad_batch_stride: Optional[int] = None,
                  workspace: Optional[torch.Tensor] = None,
                  max_lookups_per_table: int = 0,
-                 error_flag: Optional[torch.Tensor] = None, presorted: bool = False) -> None:
+                 error_flag: Optional[torch.Tensor] = None, presorted: int = False) -> None:
     """mode: 'sgd' (fused exact SGD; fp32 or fp16 weights), 'rowwise_adagrad' (fused
     RWSAdagrad) or 'dense' (weights is a gradient buffer to accumulate into).  max_lookups_per_table:
     upper bound on any table's lookups (0 = unknown); <= 4096 selects the per-table LDS
     sort (bitwise the same result as the device-wide radix sort).  ``error_flag``: device
-    int32 that receives TBE_ERR_INDEX / TBE_ERR_TABLE_CAP bits (see check_tbe_errors)."""
+    int32 that receives TBE_ERR_INDEX / TBE_ERR_TABLE_CAP bits (see check_tbe_errors).
+    ``presorted``: True - the per-table sort ran in tbe_forward_presort; PRESORTED_ANY -
+    tbe_backward_sort ran for this batch."""
     _check_cuda(weights, row_base, indices, offsets, grad_out, momentum, per_sample_weights)
     D = weights.shape[1]
     N = indices.numel()

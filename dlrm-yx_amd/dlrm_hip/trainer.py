@@ -247,6 +247,12 @@ class DLRMTrainer:
         # W = 8 rank 2 step: 16.3 us of chain launch -> a few us inside the lookup launch;
         # the cost is the all-to-all starting after the (longer) fused launch
         self.dist_bottom_in_lookup = True
+        # one GPU, tables past the per-table LDS sort (C1's L = 100): the backward's tiled
+        # sort (dlrm_tbe_backward_sort) on the side stream at the start of the step, beside
+        # the forward, joined before the embedding backward.  The one cross-queue join of
+        # the graph costs ~11 us of idle GPU; the 6 sort launches (~69 us) hide behind the
+        # forward: C1 step 0.588 -> 0.572 ms (profiles/r06_early_sort_ab.txt)
+        self.early_sort = True
         # one GPU, one-hot batches: the dot interaction gathers the embedding rows itself
         # (dlrm_interact_dot_forward_gather); the lookup launch keeps only its sort role
         self.fuse_gather = True
@@ -639,7 +645,9 @@ class DLRMTrainer:
             with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
                     prof("tbe_fwd"):
                 if self.T_local > 0:
-                    idx, off = st["csr"] = self._phys_csr(batch, B)
+                    if "csr" not in st:
+                        st["csr"] = self._phys_csr(batch, B)
+                    idx, off = st["csr"]
                     out = bufs["P"] if self.qr_active else bufs["E"]
                 if self.T_local > 0 and presort:
                     # the backward's per-table sort runs inside the lookup launch (alone,
@@ -675,17 +683,32 @@ class DLRMTrainer:
                     self._gemm([self._fwd(L, h, out)], side=c_fwd)
                     h = out
 
+        def early_sort():  # the backward's sort on the side stream, beside the forward
+            s0, s1 = streams()
+            idx, off = st["csr"] = self._phys_csr(batch, B)
+            s1.wait_stream(s0)
+            with torch.cuda.stream(s1), prof("tbe_sort"):
+                ops.tbe_backward_sort(self.weights, self.row_base, self.T_phys, B, idx, off,
+                                      self._ws_tbe(idx.numel()), batch.max_per_table,
+                                      error_flag=self.tbe_error_flag)
+            st["sorted"] = s1
+
         def fwd_single():  # one GPU: bottom MLP || lookup
             # first segment of the step: a launch role deferred by an aborted step (raw
             # pointers of that step) must never ride on this step's launches
             self._roles = []
+            if (self.early_sort and conc and self.T_local > 0 and presort
+                    and not 0 < batch.max_per_table <= ops.TBE_PRESORT_SEG_CAP):
+                early_sort()
             chain = self._bottom_chain(batch, bufs) if presort and not c_fwd else None
             self.bottom_fused = chain is not None
             if chain is not None:
                 # the bottom MLP forward runs as a role of the lookup launch
                 with record_function("module::forward_pass::embedding_lookup", emb_sizes), \
                         record_function("module::forward_pass::bottom_mlp"), prof("tbe_fwd"):
-                    idx, off = st["csr"] = self._phys_csr(batch, B)
+                    if "csr" not in st:
+                        st["csr"] = self._phys_csr(batch, B)
+                    idx, off = st["csr"]
                     out = None if gather else bufs["P"] if self.qr_active else bufs["E"]
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
@@ -866,11 +889,15 @@ class DLRMTrainer:
                                                      bufs["dE"], bufs["dP"])
                         grad = bufs["dP"]
                     fn = ops.tbe_backward_defer if defer else ops.tbe_backward
+                    s1 = st.pop("sorted", None)
+                    if s1 is not None:  # join the early sort
+                        torch.cuda.current_stream(self.dev).wait_stream(s1)
                     return fn(mode, self.weights, self.row_base, self.T_phys, B, idx, off,
                               grad, lr=elr, eps=cfg.adagrad_eps, momentum=self.momentum,
                               workspace=self._ws_tbe(idx.numel()),
                               max_lookups_per_table=batch.max_per_table,
-                              error_flag=self.tbe_error_flag, presorted=presort)
+                              error_flag=self.tbe_error_flag,
+                              presorted=ops.PRESORTED_ANY if s1 is not None else presort)
 
         @record_function("## Backward ##")
         def backward_single():  # one GPU: bottom backward || embedding backward

@@ -111,8 +111,10 @@ enum dlrm_qr_op { DLRM_QR_MULT = 0, DLRM_QR_ADD = 1, DLRM_QR_CONCAT = 2 };
  *    launch lost to the grouped GEMM schedules at every batch size,
  *    profiles/r04_bot_sched_ab.txt) (round 5).
  * 9: dlrm_adagrad_update_scaled (the W-rank dense Adagrad step with the 1/W folded in)
- *    (round 6). */
-#define DLRM_ABI_VERSION 9 /* the one source of truth: abi.cpp returns it, dlrm_hip/_lib.py
+ *    (round 6).
+ * 10: dlrm_tbe_backward_sort + presorted = DLRM_PRESORTED_ANY (the backward's sort run
+ *    early, e.g. on a second stream) (round 6). */
+#define DLRM_ABI_VERSION 10 /* the one source of truth: abi.cpp returns it, dlrm_hip/_lib.py
                              pins it (tests/test_cpu_host.py checks all of them agree) */
 int dlrm_abi_version(void);
 const char* dlrm_last_error(void);
@@ -281,6 +283,21 @@ int dlrm_tbe_psw_grad(const float* weights, int64_t D, const int64_t* row_base, 
 size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows, int64_t D);
 
 /*
+ * ABI v10: the sort phase of the backward alone (whichever sort the backward would run for
+ * the same D, tables, indices, offsets, bound, workspace and per_sample_weights nullness:
+ * per-table, tiled per-table, or device-wide), into `workspace`.  It depends only on the
+ * indices, so a caller can run it early - e.g. on a second stream beside the forward - and
+ * then call the backward of the same batch with presorted = DLRM_PRESORTED_ANY.
+ */
+#define DLRM_PRESORTED_ANY 2
+int dlrm_tbe_backward_sort(int64_t D, const int64_t* row_base, int32_t T, int32_t B,
+                           const void* indices, int32_t index_bits, const void* offsets,
+                           int32_t offset_bits, int64_t num_lookups, int64_t total_rows,
+                           const float* per_sample_weights, int64_t max_lookups_per_table,
+                           void* workspace, size_t workspace_bytes, int32_t* error_flag,
+                           dlrm_stream_t stream);
+
+/*
  * Exact-SGD backward fused with the update: for every lookup l of bag (t,b),
  *   W[row_base[t]+indices[l]] -= lr * w_l * grad_out[b*grad_batch_stride + t*D + :]
  * Duplicate rows are combined deterministically: lookups are sorted by (global row,
@@ -297,6 +314,8 @@ size_t dlrm_tbe_backward_workspace_size(int64_t num_lookups, int64_t total_rows,
  * presorted != 0: the per-table sort of THIS batch (same indices, offsets, workspace)
  * already ran inside dlrm_tbe_forward_presort and is skipped here (ignored when the
  * per-table sort does not apply: 32-bit row ids, bound <= 4096).
+ * presorted == DLRM_PRESORTED_ANY (ABI v10): dlrm_tbe_backward_sort already ran for THIS
+ * batch with the same arguments; whichever sort applies is skipped.
  * (The same applies to the two functions below.)
  */
 int dlrm_tbe_backward_sgd(float* weights, int64_t D, const int64_t* row_base, int32_t T,

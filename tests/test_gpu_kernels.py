@@ -1147,6 +1147,53 @@ def test_tbe_forward_presort_unsorted_with_bottom_chain(ops, D, L, bound, idx_dt
     assert torch.equal(Wa, Wb)
 
 
+@pytest.mark.parametrize("L,bound,idx_dtype,weighted,mode", [
+    (1, True, torch.int32, False, "sgd"),       # per-table LDS sort
+    (3, True, torch.int32, False, "sgd"),       # tiled per-table sort
+    (3, True, torch.int64, True, "rowwise_adagrad"),
+    (3, False, torch.int32, False, "sgd"),      # device-wide sort (its pass parity)
+    (2, False, torch.int64, True, "dense"),
+])
+def test_tbe_backward_sort_then_presorted_any(ops, L, bound, idx_dtype, weighted, mode):
+    """dlrm_tbe_backward_sort (the backward's sort alone, run early) followed by the backward
+    with presorted = PRESORTED_ANY: bitwise the backward that sorts itself, for every sort
+    variant (per-table, tiled, device-wide), an out-of-range index flagged the same."""
+    torch.manual_seed(9)
+    rows, B, D = [3, 5000, 700, 90000], 2048, 64
+    T = len(rows)
+    mx = B * L if bound else 0
+    lo = [torch.arange(B) * L for _ in rows]
+    li = [torch.randint(0, n, (B * L,)) for n in rows]
+    li[2][5] = 10 ** 6
+    off, idx = O.batched_csr(lo, li)
+    idx, off = idx.to(idx_dtype).to(dev), off.to(dev)
+    psw = torch.rand(idx.numel(), device=dev) if weighted else None
+    row_base = torch.tensor([0] + np.cumsum(rows).tolist(), dtype=torch.int64, device=dev)
+    W = torch.randn(sum(rows), D, device=dev)
+    G = torch.randn(B, T, D, device=dev)
+    mom = torch.rand(sum(rows), device=dev) if mode == "rowwise_adagrad" else None
+    ws = torch.zeros(ops.tbe_backward_workspace_size(idx.numel(), sum(rows), D),
+                     dtype=torch.uint8, device=dev)
+    out = []
+    for early in (False, True):
+        Wx = torch.zeros_like(W) if mode == "dense" else W.clone()
+        mx_ = mom.clone() if mom is not None else None
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ws.fill_(0xA5)
+        if early:
+            ops.tbe_backward_sort(Wx, row_base, T, B, idx, off, ws, mx,
+                                  per_sample_weights=psw, error_flag=flag)
+        ops.tbe_backward(mode, Wx, row_base, T, B, idx, off, G, lr=0.05, eps=1e-6,
+                         momentum=mx_, per_sample_weights=psw, workspace=ws,
+                         max_lookups_per_table=mx, error_flag=flag,
+                         presorted=ops.PRESORTED_ANY if early else False)
+        torch.cuda.synchronize()
+        out.append((Wx.cpu(), None if mx_ is None else mx_.cpu(), int(flag.item())))
+    assert torch.equal(out[0][0], out[1][0])
+    assert out[0][1] is None or torch.equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2] != 0
+
+
 def _tbe_bwd_case(rows, B, L, D, seed, invalid=False, idx_dtype=torch.int32):
     torch.manual_seed(seed)
     T = len(rows)

@@ -732,6 +732,50 @@ def test_tbe_update_roles_match_own_launches(name, sched, optimizer, at, graph):
         assert (a is None and b is None) or torch.equal(a, b)
 
 
+@pytest.mark.parametrize("name,optimizer,L", [("c3_small", "sgd", 20),
+                                              ("c2_small", "rwsadagrad", 40)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_early_sort_matches_in_backward_sort(name, optimizer, L, graph):
+    """Tables past the per-table LDS sort (B * L > 4096 lookups, C1's shape): the backward's
+    tiled sort on the side stream at the start of the step (early_sort, joined before the
+    embedding backward) vs inside the backward - 3 steps leave bitwise the same tables,
+    momentum, dense parameters and predictions, eager and replayed from a captured graph
+    (the fork and join inside one graph)."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function=c["loss"],
+                        learning_rate=c["lr"] if optimizer == "sgd" else 1e-3,
+                        optimizer=optimizer)
+    B = 256
+    res = []
+    for early in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.early_sort = early
+        batches = [tr.synthetic_batch(B, L, seed=s) for s in range(3)]
+        assert batches[0].max_per_table > 4096
+        if graph:
+            tr.step(batches[0])
+            run = tr.capture(batches[0])
+            for b in batches[1:]:
+                for src, dst in zip((b.X, b.offsets, b.indices, b.target),
+                                    (batches[0].X, batches[0].offsets, batches[0].indices,
+                                     batches[0].target)):
+                    dst.copy_(src)
+                run()
+        else:
+            for b in batches:
+                tr.step(b)
+        torch.cuda.synchronize()
+        tr.check_errors()
+        mom = tr.momentum.cpu().clone() if tr.momentum is not None else None
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(), mom,
+                    tr._bufs[(B, B)]["prob"].cpu().clone()))
+    for a, b in zip(*res):
+        assert (a is None and b is None) or torch.equal(a, b)
+
+
 @pytest.mark.parametrize("name,B", [("c2_small", 128), ("c3_small", 256)])
 def test_bottom_parts_split_chain_matches_single(name, B):
     """The fused bottom MLP with 2 / 4 workgroups per 16-row block (auto at these batch
