@@ -684,6 +684,8 @@ def main():
                     "pass rides on the top-MLP backward's first launch, 0 = own launch")
     ap.add_argument("--early-sort", type=int, default=-1, help="A/B: 1 = the backward's "
                     "sort on the side stream beside the forward (tables past the LDS sort)")
+    ap.add_argument("--feature-pad", type=int, default=-1, help="A/B: 1 = E / dE rows at a "
+                    "batch stride of an odd number of 256-byte chunks (one GPU)")
     ap.add_argument("--bottom-parts", type=int, default=-1, help="A/B: workgroups per 16-row "
                     "block of the fused bottom MLP (1, 2, 4; 0 = auto)")
     ap.add_argument("--tbe-role-at", default="", help="A/B: bottom-backward launches "
@@ -775,6 +777,8 @@ def main():
         tr.head_role = bool(args.head_role)
     if args.early_sort >= 0:
         tr.early_sort = bool(args.early_sort)
+    if args.feature_pad >= 0:
+        tr.feature_pad = bool(args.feature_pad)
     if args.bottom_parts >= 0:
         tr.bottom_parts = args.bottom_parts
     if args.tbe_role_at:
@@ -977,6 +981,7 @@ def main():
                        "bot_sched": tr.bot_sched, "tbe_role": tr.tbe_role,
                        "tbe_role_at": list(tr.tbe_role_at), "bottom_parts": tr.bottom_parts,
                        "head_role": tr.head_role, "early_sort": tr.early_sort,
+                       "feature_pad": tr.feature_pad,
                        "full_last_wgrad": tr.full_last_wgrad,
                        "tune": args.tune or None},
             "shard_balance": tr.lookup_balance(B, c["L"]) if world > 1 else None,

@@ -253,6 +253,13 @@ class DLRMTrainer:
         # the graph costs ~11 us of idle GPU; the 6 sort launches (~69 us) hide behind the
         # forward: C1 step 0.588 -> 0.572 ms (profiles/r06_early_sort_ab.txt)
         self.early_sort = True
+        # one GPU: the pooled embeddings E and their gradient dE with a batch stride of an odd
+        # number of 256-byte chunks.  The embedding update reads dE[b, t] in sorted-row order
+        # (random b) and each XCD works through one table's lookups: at a stride of 8 chunks
+        # (C1: 8 x 64 floats) every such read lands in the same two of an XCD's L2 channels.
+        # Measured: C1's update pass 105.7 -> 99.1 us, the step -0.3..-0.8 %, C3 / C2 within
+        # noise (profiles/r06_feature_pad_ab.txt) - an option, off by default
+        self.feature_pad = False
         # one GPU, one-hot batches: the dot interaction gathers the embedding rows itself
         # (dlrm_interact_dot_forward_gather); the lookup launch keeps only its sort role
         self.fuse_gather = True
@@ -547,8 +554,13 @@ class DLRMTrainer:
         bufs["gb"] = [torch.zeros((Bl, wbot), **f32) for _ in range(3)]
         bufs["dx"] = torch.zeros((Bl, D), **f32)
         bufs["gx"] = torch.zeros((Bl, D), **f32)
-        bufs["E"] = torch.zeros((B, max(self.T_local, 1), D), **f32)
-        bufs["dE"] = torch.zeros_like(bufs["E"])
+        Tl = max(self.T_local, 1)
+        pad = 0
+        if self.feature_pad and not self.distributed and not self.qr_active:
+            pad = ((256 - (Tl * D * 4) % 512) % 512) // 4  # stride = 256 B mod 512 B
+        for name in ("E", "dE"):
+            store = torch.zeros((B, Tl * D + pad), **f32)
+            bufs[name] = store[:, :Tl * D].view(B, Tl, D)
         if self.qr_active:  # pooled physical tables (quotient / remainder halves)
             bufs["P"] = torch.zeros((B, self.T_phys, D), **f32)
             bufs["dP"] = torch.zeros_like(bufs["P"])
@@ -659,11 +671,13 @@ class DLRMTrainer:
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
                                             batch.max_per_table, out=None if gather else out,
+                                            out_batch_stride=out.stride(0),
                                             error_flag=self.tbe_error_flag, bottom=chain,
                                             lookup=not gather)
                 elif self.T_local > 0:
                     ops.tbe_forward(self.weights, self.row_base, self.T_phys, B, idx, off,
-                                    out=out, error_flag=self.tbe_error_flag)
+                                    out=out, out_batch_stride=out.stride(0),
+                                    error_flag=self.tbe_error_flag)
                 if self.T_local > 0 and self.qr_active:
                     self._qr_combine(bufs, B)
 
@@ -713,6 +727,8 @@ class DLRMTrainer:
                     ops.tbe_forward_presort(self.weights, self.row_base, self.T_phys, B, idx,
                                             off, self._ws_tbe(idx.numel()),
                                             batch.max_per_table, out=out,
+                                            out_batch_stride=None if out is None else
+                                            out.stride(0),
                                             error_flag=self.tbe_error_flag, bottom=chain,
                                             lookup=not gather)
                     if self.qr_active:
@@ -894,6 +910,7 @@ class DLRMTrainer:
                         torch.cuda.current_stream(self.dev).wait_stream(s1)
                     return fn(mode, self.weights, self.row_base, self.T_phys, B, idx, off,
                               grad, lr=elr, eps=cfg.adagrad_eps, momentum=self.momentum,
+                              grad_batch_stride=grad.stride(0),
                               workspace=self._ws_tbe(idx.numel()),
                               max_lookups_per_table=batch.max_per_table,
                               error_flag=self.tbe_error_flag,

@@ -776,6 +776,50 @@ def test_early_sort_matches_in_backward_sort(name, optimizer, L, graph):
         assert (a is None and b is None) or torch.equal(a, b)
 
 
+@pytest.mark.parametrize("name,optimizer,L", [("c3_small", "sgd", 20), ("c3_small", "sgd", 1),
+                                              ("c2_small", "rwsadagrad", 1)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_feature_pad_matches_dense_rows(name, optimizer, L, graph):
+    """E / dE at a padded batch stride (feature_pad: an odd number of 256-byte chunks per
+    sample) vs dense rows: 3 steps leave bitwise the same state - the lookup, the interaction
+    (pooled and gather-fused), the embedding update and the early sort read and write the
+    same values through the stride."""
+    DLRMTrainer, TrainerConfig = _trainer()
+    c = CASES[name]
+    D, rows = c["D"], c["rows"]
+    cfg = TrainerConfig(m_spa=D, ln_emb=rows, ln_bot=c["bot"],
+                        ln_top=[_num_int(len(rows), D)] + c["top"], loss_function=c["loss"],
+                        learning_rate=c["lr"] if optimizer == "sgd" else 1e-3,
+                        optimizer=optimizer)
+    B = 256
+    res = []
+    for pad in (False, True):
+        tr = DLRMTrainer(cfg, device=dev, seed=11)
+        tr.feature_pad = pad
+        batches = [tr.synthetic_batch(B, L, seed=s) for s in range(3)]
+        if graph:
+            tr.step(batches[0])
+            run = tr.capture(batches[0])
+            for b in batches[1:]:
+                for src, dst in zip((b.X, b.offsets, b.indices, b.target),
+                                    (batches[0].X, batches[0].offsets, batches[0].indices,
+                                     batches[0].target)):
+                    dst.copy_(src)
+                run()
+        else:
+            for b in batches:
+                tr.step(b)
+        torch.cuda.synchronize()
+        tr.check_errors()
+        E = tr._bufs[(B, B)]["E"]
+        assert (E.stride(0) * 4 // 256) % 2 == (1 if pad else (E.stride(0) * 4 // 256) % 2)
+        mom = tr.momentum.cpu().clone() if tr.momentum is not None else None
+        res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(), mom,
+                    tr._bufs[(B, B)]["prob"].cpu().clone()))
+    for a, b in zip(*res):
+        assert (a is None and b is None) or torch.equal(a, b)
+
+
 @pytest.mark.parametrize("name,B", [("c2_small", 128), ("c3_small", 256)])
 def test_bottom_parts_split_chain_matches_single(name, B):
     """The fused bottom MLP with 2 / 4 workgroups per 16-row block (auto at these batch
