@@ -56,7 +56,8 @@ constexpr int kMaxSplit = 32;
 constexpr int kMaxGroup = 6;
 constexpr int64_t kTicketCap = 16384;  // int32 tickets in the fixed 64 KiB workspace head
 constexpr int kBK = 32;
-constexpr int kRasterRows = 8;  // tile rows per raster group (pipe_body)
+constexpr int kRasterRows = 4;  // tile rows per raster group (pipe_body; 8 and 16 slower at C3,
+                                 // profiles/r06_raster_rows_ab.txt)
 
 struct GemmParams {
   int64_t M, N, K;
