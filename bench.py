@@ -776,7 +776,7 @@ def main():
     if args.head_role >= 0:
         tr.head_role = bool(args.head_role)
     if args.early_sort >= 0:
-        tr.early_sort = bool(args.early_sort)
+        tr.early_sort = args.early_sort  # 1: at the start of the step, 2: after the lookup
     if args.feature_pad >= 0:
         tr.feature_pad = bool(args.feature_pad)
     if args.bottom_parts >= 0:

@@ -251,7 +251,8 @@ class DLRMTrainer:
         # sort (dlrm_tbe_backward_sort) on the side stream at the start of the step, beside
         # the forward, joined before the embedding backward.  The one cross-queue join of
         # the graph costs ~11 us of idle GPU; the 6 sort launches (~69 us) hide behind the
-        # forward: C1 step 0.588 -> 0.572 ms (profiles/r06_early_sort_ab.txt)
+        # forward: C1 step 0.588 -> 0.572 ms (profiles/r06_early_sort_ab.txt).  2 = forked
+        # after the lookup launch instead: ~5 % slower (profiles/r06_early_sort_fork_ab.txt)
         self.early_sort = True
         # one GPU: the pooled embeddings E and their gradient dE with a batch stride of an odd
         # number of 256-byte chunks.  The embedding update reads dE[b, t] in sorted-row order
@@ -711,8 +712,9 @@ class DLRMTrainer:
             # first segment of the step: a launch role deferred by an aborted step (raw
             # pointers of that step) must never ride on this step's launches
             self._roles = []
-            if (self.early_sort and conc and self.T_local > 0 and presort
-                    and not 0 < batch.max_per_table <= ops.TBE_PRESORT_SEG_CAP):
+            es = (self.early_sort and conc and self.T_local > 0 and presort
+                  and not 0 < batch.max_per_table <= ops.TBE_PRESORT_SEG_CAP)
+            if es and self.early_sort != 2:  # 2: forked after the lookup launch instead
                 early_sort()
             chain = self._bottom_chain(batch, bufs) if presort and not c_fwd else None
             self.bottom_fused = chain is not None
@@ -733,11 +735,18 @@ class DLRMTrainer:
                                             lookup=not gather)
                     if self.qr_active:
                         self._qr_combine(bufs, B)
+                if es and self.early_sort == 2:
+                    early_sort()
                 return
             s0, s1 = streams()
+            if es and self.early_sort == 2:
+                lookup()
+                early_sort()
+                s0, s1 = streams()
             if c_fwd:
                 s1.wait_stream(s0)
-            lookup()
+            if not (es and self.early_sort == 2):
+                lookup()
             with side_if(c_fwd, s1):
                 bottom_fwd()
             if c_fwd:

@@ -750,7 +750,7 @@ def test_early_sort_matches_in_backward_sort(name, optimizer, L, graph):
                         optimizer=optimizer)
     B = 256
     res = []
-    for early in (False, True):
+    for early in (False, 1, 2):  # 1: forked at the start of the step, 2: after the lookup
         tr = DLRMTrainer(cfg, device=dev, seed=11)
         tr.early_sort = early
         batches = [tr.synthetic_batch(B, L, seed=s) for s in range(3)]
@@ -772,8 +772,9 @@ def test_early_sort_matches_in_backward_sort(name, optimizer, L, graph):
         mom = tr.momentum.cpu().clone() if tr.momentum is not None else None
         res.append((tr.weights.cpu().clone(), tr.params.cpu().clone(), mom,
                     tr._bufs[(B, B)]["prob"].cpu().clone()))
-    for a, b in zip(*res):
-        assert (a is None and b is None) or torch.equal(a, b)
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert (a is None and b is None) or torch.equal(a, b)
 
 
 @pytest.mark.parametrize("name,optimizer,L", [("c3_small", "sgd", 20), ("c3_small", "sgd", 1),
